@@ -1,0 +1,135 @@
+/*
+ * zs_gpu.h -- C-ABI of the MI355X batched deflate/inflate engine
+ * (libzsgpu.so, built from zlib-streams-ts_amd/csrc).
+ *
+ * The drop-in boundary for zlib-streams-ts's hot path.  Each batch entry runs
+ * N independent streams, and stream i produces exactly the bytes (or the
+ * error) that piping in[i] alone through the reference's web-streams layer
+ * yields when the whole buffer is passed in ONE write() followed by close():
+ *
+ *   zs_deflate_batch*  replaces, per stream,
+ *       new CompressionStream(format, {level})            src/mod/streams.ts:242-251
+ *         -> createZeroCopyCompressionTransform           src/mod/streams.ts:216-228
+ *         -> deflateInit2_(s, level, 8, wbits, 8, 0)      src/mod/deflate/deflate.ts:253-343
+ *         -> deflate(s, Z_NO_FLUSH) per 32 KiB, deflate(s, Z_FINISH), deflateEnd
+ *                                                         src/mod/deflate/deflate.ts:716-1013
+ *   zs_inflate_batch*  replaces, per stream,
+ *       new DecompressionStream(format)                   src/mod/streams.ts:253-262
+ *         -> inflateInit2_(s, wbits) / inflate / inflateEnd
+ *                                                         src/mod/inflate/inflate.ts:174-192,332-1185
+ *   zs_crc32_batch / zs_adler32_batch replace           src/mod/common/crc32.ts:26-58,
+ *                                                         src/mod/common/adler32.ts:4-25
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Buffers named d_* are device pointers
+ *     (HBM) on the context's device; the per-stream layout arrays (offsets,
+ *     lengths, capacities) are host arrays owned by the caller for the call.
+ *   - wbits follows the format -> windowBits mapping of streams.ts:220,233:
+ *     -15 "deflate-raw", 15 "deflate" (zlib), 31 "gzip", -16 "deflate64-raw"
+ *     (inflate only).  level: 0..9 or -1 (= 6, deflate.ts:268-270).
+ *   - Status codes are the reference's Z_* values (common/constants.ts:21-29).
+ *     Per-stream status: ZS_STREAM_END on success; ZS_BUF_ERROR if out_cap[i]
+ *     is too small (size outputs with zs_deflate_bound); decode errors as the
+ *     reference reports them (see zs_inflate_batch_device).
+ *   - Return value of every call: ZS_OK, or ZS_STREAM_ERROR for invalid
+ *     arguments (the reference's deflateInit2_ validation, deflate.ts:281-294,
+ *     which the stream layer reports as "init failed: -2", streams.ts:53), or
+ *     ZS_MEM_ERROR when device memory cannot be obtained.  zs_last_error()
+ *     describes the last failure on the calling thread.
+ *   - Output offsets and capacities must be multiples of 4 bytes (the engine
+ *     writes 32-bit words); inputs may be packed at any byte offset.
+ */
+#ifndef ZS_GPU_H
+#define ZS_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZS_OK 0
+#define ZS_STREAM_END 1
+#define ZS_NEED_DICT 2
+#define ZS_STREAM_ERROR (-2)
+#define ZS_DATA_ERROR (-3)
+#define ZS_MEM_ERROR (-4)
+#define ZS_BUF_ERROR (-5)
+
+/* stream-layer phase of a per-stream failure (streams.ts:53,117,170) */
+#define ZS_PHASE_NONE 0
+#define ZS_PHASE_INIT 1
+#define ZS_PHASE_PROCESS 2
+#define ZS_PHASE_FINISH 3
+
+typedef struct zs_ctx zs_ctx;
+
+/* One context per device (one process per GPU).  Workspaces grow on demand
+ * and are reused across calls; a context is not re-entrant across threads. */
+int zs_ctx_create(int device, zs_ctx **out);
+void zs_ctx_destroy(zs_ctx *ctx);
+const char *zs_last_error(void);
+const char *zs_version(void);
+
+/* deflateBound for a fresh stream with memLevel 8 (deflate.ts:615-674). */
+uint64_t zs_deflate_bound(uint64_t source_len, int wbits);
+
+/* Batched compression, device-resident buffers.  Enqueued on hip_stream (a
+ * hipStream_t, or NULL for the context's own stream); returns once enqueued.
+ * d_status[i] / d_out_len[i] (device int32 / uint32 arrays) are written. */
+int zs_deflate_batch_device(zs_ctx *ctx, int level, int wbits, uint32_t n_streams, const uint8_t *d_in,
+                            const uint64_t *in_off, const uint32_t *in_len, uint8_t *d_out, const uint64_t *out_off,
+                            const uint32_t *out_cap, int32_t *d_status, uint32_t *d_out_len, void *hip_stream);
+
+/* Same, host buffers: copies in, runs, copies out, synchronizes. */
+int zs_deflate_batch(zs_ctx *ctx, int level, int wbits, uint32_t n_streams, const uint8_t *in, const uint64_t *in_off,
+                     const uint32_t *in_len, uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                     int32_t *status, uint32_t *out_len);
+
+/* Batched decompression, device-resident buffers.  Per stream: d_status[i]
+ * (ZS_STREAM_END, or the Z_* code the stream layer reports), d_phase[i]
+ * (ZS_PHASE_PROCESS / ZS_PHASE_FINISH for failures), d_msg[i] (index into
+ * zs_inflate_message()), d_out_len[i], d_consumed[i] (input bytes used up to
+ * the end of the stream; trailing bytes are ignored, streams.ts:74-76). */
+int zs_inflate_batch_device(zs_ctx *ctx, int wbits, uint32_t n_streams, const uint8_t *d_in, const uint64_t *in_off,
+                            const uint32_t *in_len, uint8_t *d_out, const uint64_t *out_off, const uint32_t *out_cap,
+                            int32_t *d_status, int32_t *d_phase, int32_t *d_msg, uint32_t *d_out_len,
+                            uint32_t *d_consumed, void *hip_stream);
+
+int zs_inflate_batch(zs_ctx *ctx, int wbits, uint32_t n_streams, const uint8_t *in, const uint64_t *in_off,
+                     const uint32_t *in_len, uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                     int32_t *status, int32_t *phase, int32_t *msg, uint32_t *out_len, uint32_t *consumed);
+
+/* The z_stream message for a d_msg index (inflate.ts:397-1031, inffast.ts:108,197,210). */
+const char *zs_inflate_message(int32_t msg_index);
+
+/* Per-stream checksums of device-resident buffers (crc32.ts / adler32.ts),
+ * written to d_check[i].  crc32 of an empty stream is 0, adler32 is 1. */
+int zs_crc32_batch_device(zs_ctx *ctx, uint32_t n_streams, const uint8_t *d_in, const uint64_t *in_off,
+                          const uint32_t *in_len, uint32_t *d_check, void *hip_stream);
+int zs_adler32_batch_device(zs_ctx *ctx, uint32_t n_streams, const uint8_t *d_in, const uint64_t *in_off,
+                            const uint32_t *in_len, uint32_t *d_check, void *hip_stream);
+
+/* Kernel timing of the last batch call on this context (HIP events on the
+ * stream the kernels ran on): total device milliseconds and the duration of
+ * the named phase ("match", "parse", "trees", "emit", "prev", "inflate", ...).
+ * Returns -1 when no timing is available. */
+double zs_last_batch_ms(zs_ctx *ctx);
+double zs_last_phase_ms(zs_ctx *ctx, const char *phase);
+void zs_set_timing(zs_ctx *ctx, int on);
+
+/* Introspection for tests: copy an intermediate array of stream s of the last
+ * deflate batch to host memory (what: 0 chain links u16/position, 1 match table
+ * u32x2/position, 2 symbols u32, 3 block records, 4 stream record).  Returns
+ * the bytes copied (0 if unavailable).  Synchronizes the device. */
+uint64_t zs_debug_fetch(zs_ctx *ctx, int what, uint32_t s, void *dst, uint64_t cap);
+
+/* Synthetic workload: kind 0 = T-corpus text,
+ * 1 = M-corpus mixed, 2 = xorshift bytes; stream i uses seed
+ * 0x9e3779b9 ^ (first_index + i).  Fills host memory with n_streams x len. */
+void zs_corpus(int kind, uint32_t first_index, uint32_t n_streams, uint32_t len, uint8_t *out, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,112 @@
+"""GPU parity: the HIP deflate engine against the reference's goldens and the oracle."""
+import hashlib
+import random
+
+import pytest
+
+import corpus
+import golden_io
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+GPU_LEVELS = [4, 5, 6, 7, 8, 9]
+
+
+def test_small_goldens(engine):
+    cases = [(c, d) for c, d in golden_io.deflate_cases() if c["level"] in GPU_LEVELS]
+    groups = {}
+    for c, d in cases:
+        groups.setdefault((c["level"], c["format"]), []).append((c, d))
+    bad = []
+    for (level, fmt), items in sorted(groups.items()):
+        res = engine.compress_batch_raw([d for _, d in items], fmt, level)
+        for (c, d), (st, out) in zip(items, res):
+            if st != 1 or corpus.sha256(out) != c["out_sha256"]:
+                bad.append((c["spec"].get("kind"), c["in_len"], level, fmt, st, len(out), c["out_len"]))
+    assert not bad, bad[:10]
+
+
+def test_empty_and_hello(engine):
+    assert engine.compress_batch([b""], "deflate-raw", 6) == [bytes([3, 0])]
+    assert engine.compress_batch([b"hello"], "deflate-raw", 6)[0].hex() == "cb48cdc9c90700"
+    assert engine.compress_batch([b""], "gzip", 6)[0].hex() == "1f8b08000000000000ff0300" + "00" * 8
+
+
+@pytest.mark.parametrize("level", GPU_LEVELS)
+def test_random_inputs_vs_oracle(engine, level):
+    rng = random.Random(1000 + level)
+    inputs = []
+    for k in range(24):
+        n = rng.choice([0, 1, 2, 3, 4, 257, 258, 259, 1000, 4095, 32768, 32769, 65535, 65536, 70001,
+                        rng.randrange(1, 140000)])
+        kind = rng.choice(["text", "mixed", "rand", "zeros", "ramp"])
+        spec = {"kind": kind, "n": n, "seed": rng.randrange(1 << 32)}
+        inputs.append(corpus.make(spec))
+    for fmt in ["deflate-raw", "deflate", "gzip"]:
+        res = engine.compress_batch_raw(inputs, fmt, level)
+        for d, (st, out) in zip(inputs, res):
+            ost, ref, _ = oracle.compress(d, level, fmt)
+            assert st == 1 and out == ref, (len(d), fmt, level, len(out), len(ref))
+
+
+def test_block_boundaries_and_stored_blocks(engine):
+    # > 16383 symbols per stream (multi-block), incompressible data (stored blocks),
+    # lengths that are multiples of 16383 symbols and tiny tails
+    inputs = [corpus.rand(corpus.stream_seed(1), 16383), corpus.rand(corpus.stream_seed(2), 16384),
+              corpus.rand(corpus.stream_seed(3), 50000), bytes(200000), corpus.text(corpus.stream_seed(4), 262144),
+              corpus.rand(corpus.stream_seed(5), 16383 * 2), corpus.rand(corpus.stream_seed(6), 16383 * 2 + 1)]
+    for level in (4, 6, 9):
+        res = engine.compress_batch_raw(inputs, "deflate-raw", level)
+        for d, (st, out) in zip(inputs, res):
+            assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1], (len(d), level)
+
+
+def test_output_capacity_too_small_reports_buf_error(engine):
+    import ctypes
+    import zsamd
+
+    L = zsamd.lib()
+    d = corpus.rand(corpus.stream_seed(9), 4000)
+    out = ctypes.create_string_buffer(64)
+    st = (ctypes.c_int32 * 1)()
+    ol = (ctypes.c_uint32 * 1)()
+    r = L.zs_deflate_batch(engine.handle, 6, -15, 1, d, (ctypes.c_uint64 * 1)(0), (ctypes.c_uint32 * 1)(len(d)),
+                           out, (ctypes.c_uint64 * 1)(0), (ctypes.c_uint32 * 1)(64), st, ol)
+    assert r == 0 and st[0] == zsamd.Z_BUF_ERROR
+
+
+def test_invalid_arguments_are_init_errors(engine):
+    import zsamd
+
+    with pytest.raises(zsamd.ZsError) as e:
+        engine.compress_batch([b"x"], "deflate-raw", 10)
+    assert str(e.value) == "init failed: -2"  # streams.ts:53 with deflate.ts:281-294
+
+
+@pytest.mark.slow
+def test_c2_full_batch_matches_reference_goldens(engine):
+    """BASELINE.json configs[1]: 4096 x 64 KiB T-corpus, deflate-raw L6, byte-identical."""
+    import zsamd
+
+    recs = golden_io.batch("t64_l6_raw")
+    buf = bytes(zsamd.corpus("text", 0, 4096, 65536))
+    inputs = [buf[i * 65536:(i + 1) * 65536] for i in range(4096)]
+    res = engine.compress_batch_raw(inputs, "deflate-raw", 6)
+    bad = [i for i, (st, out) in enumerate(res) if st != 1 or (len(out), hashlib.sha256(out).digest()[:16]) != recs[i]]
+    assert not bad, bad[:10]
+    assert sum(len(o) for _, o in res) == 91855591
+
+
+@pytest.mark.slow
+def test_c5_gzip_batch_matches_reference_goldens(engine):
+    import zsamd
+
+    recs = golden_io.batch("t64_l6_gzip")
+    for lo in (0, 4096):
+        buf = bytes(zsamd.corpus("text", lo, 4096, 65536))
+        inputs = [buf[i * 65536:(i + 1) * 65536] for i in range(4096)]
+        res = engine.compress_batch_raw(inputs, "gzip", 6)
+        bad = [lo + i for i, (st, out) in enumerate(res)
+               if st != 1 or (len(out), hashlib.sha256(out).digest()[:16]) != recs[lo + i]]
+        assert not bad, bad[:10]

@@ -1,0 +1,466 @@
+// capi.cpp -- the C-ABI host layer of libzsgpu.so (include/zs_gpu.h).
+//
+// Owns one device context per GPU: a HIP stream, a growable device workspace
+// and the launch sequence of the batch engines.  No torch types cross this
+// boundary; callers hand in plain pointers (device or host) and sizes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/zs_gpu.h"
+#include "zs_common.h"
+#include "zs_kernels.h"
+
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, const char* a = "") {
+  char buf[512];
+  snprintf(buf, sizeof buf, fmt, a);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                          \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) return fail(ZS_MEM_ERROR, "%s", hipGetErrorString(e_)); \
+  } while (0)
+
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes + bytes / 8, 4096);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+const zs_level_cfg kLevels[10] = {{0, 0, 0, 0},     {4, 4, 8, 4},     {4, 5, 16, 8},     {4, 6, 32, 32},
+                                  {4, 4, 16, 16},   {8, 16, 32, 32},  {8, 16, 128, 128}, {8, 32, 128, 256},
+                                  {32, 128, 258, 1024}, {32, 258, 258, 4096}};  // deflate.ts:86-103
+
+}  // namespace
+
+struct zs_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool timing = false;
+  // workspace
+  Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate;
+  // host staging for the host-buffer entry points
+  Buf d_in, d_out, d_res;
+  std::vector<uint8_t> hmeta;
+  size_t last_n = 0;
+  // timing
+  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  std::vector<std::pair<std::string, double>> phase_ms;
+  double total_ms = -1;
+};
+
+static void mark(zs_ctx* c, hipStream_t st, const char* name) {
+  if (!c->timing) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  (void)hipEventRecord(e, st);
+  c->marks.emplace_back(name, e);
+}
+
+static void collect_marks(zs_ctx* c) {
+  c->phase_ms.clear();
+  c->total_ms = -1;
+  if (c->marks.size() < 2) {
+    for (auto& m : c->marks) (void)hipEventDestroy(m.second);
+    c->marks.clear();
+    return;
+  }
+  (void)hipEventSynchronize(c->marks.back().second);
+  for (size_t i = 1; i < c->marks.size(); i++) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->marks[i - 1].second, c->marks[i].second);
+    c->phase_ms.emplace_back(c->marks[i].first, ms);
+  }
+  float tot = 0;
+  (void)hipEventElapsedTime(&tot, c->marks.front().second, c->marks.back().second);
+  c->total_ms = tot;
+  for (auto& m : c->marks) (void)hipEventDestroy(m.second);
+  c->marks.clear();
+}
+
+extern "C" {
+
+const char* zs_last_error(void) { return g_err.c_str(); }
+const char* zs_version(void) { return "zs_gpu 0.1 (gfx950)"; }
+
+int zs_ctx_create(int device, zs_ctx** out) {
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0)
+    return fail(ZS_STREAM_ERROR, "no HIP device %s", std::to_string(device).c_str());
+  HIPCHK(hipSetDevice(device));
+  zs_ctx* c = new zs_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(ZS_MEM_ERROR, "%s", hipGetErrorString(e));
+  }
+  *out = c;
+  return ZS_OK;
+}
+
+void zs_ctx_destroy(zs_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (Buf* b : {&c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
+                 &c->istate, &c->d_in, &c->d_out, &c->d_res})
+    if (b->p) (void)hipFree(b->p);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+void zs_set_timing(zs_ctx* c, int on) { c->timing = on != 0; }
+double zs_last_batch_ms(zs_ctx* c) { return c->total_ms; }
+double zs_last_phase_ms(zs_ctx* c, const char* phase) {
+  double t = -1;
+  for (auto& p : c->phase_ms)
+    if (p.first == phase) t = (t < 0 ? 0 : t) + p.second;
+  return t;
+}
+
+uint64_t zs_deflate_bound(uint64_t n, int wbits) {  // deflate.ts:615-674, memLevel 8 / windowBits 15
+  const uint64_t wraplen = wbits < 0 ? 0 : (wbits > 15 ? 18 : 6);
+  const uint64_t b = n + (n >> 12) + (n >> 14) + (n >> 25) + 13 - 6 + wraplen;
+  return (b + 3) & ~3ull;  // the engine writes whole 32-bit words
+}
+
+}  // extern "C"
+
+// Device metadata block: in_off | in_len | out_off | out_cap | pos_base | blk_base
+struct MetaLayout {
+  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, bytes;
+  explicit MetaLayout(uint32_t n) {
+    size_t o = 0;
+    auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~size_t(255); return r; };
+    in_off = take(8ull * n);
+    in_len = take(4ull * n);
+    out_off = take(8ull * n);
+    out_cap = take(4ull * n);
+    pos_base = take(8ull * n);
+    blk_base = take(4ull * n);
+    bytes = o;
+  }
+};
+
+__global__ void zs_k_finish(const zs_stream* streams, int32_t* status, uint32_t* out_len, int n) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  status[s] = streams[s].status;
+  out_len[s] = streams[s].status == ZS_Z_STREAM_END ? streams[s].out_len : 0u;
+}
+
+__global__ void zs_k_copy_check(const uint32_t* check, zs_stream* streams, int n) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) streams[s].check = check[s];
+}
+
+extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* d_in,
+                                       const uint64_t* in_off, const uint32_t* in_len, uint8_t* d_out,
+                                       const uint64_t* out_off, const uint32_t* out_cap, int32_t* d_status,
+                                       uint32_t* d_out_len, void* hip_stream) {
+  if (!c) return fail(ZS_STREAM_ERROR, "null context");
+  if (level == -1) level = 6;  // Z_DEFAULT_COMPRESSION, deflate.ts:268-270
+  int wrap;
+  if (wbits == -15) wrap = 0;
+  else if (wbits == 15) wrap = 1;
+  else if (wbits == 31) wrap = 2;
+  else return fail(ZS_STREAM_ERROR, "unsupported windowBits (use -15, 15 or 31)");
+  if (level < 0 || level > 9) return fail(ZS_STREAM_ERROR, "invalid level");  // deflate.ts:281-294
+  if (level == 0) return fail(ZS_STREAM_ERROR, "level 0 (deflate_stored) is not implemented by the GPU engine");
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  HIPCHK(hipSetDevice(c->device));
+  if (n == 0) return ZS_OK;
+  // host-side layout: workspace bases
+  MetaLayout ml(n);
+  c->hmeta.resize(ml.bytes);
+  c->last_n = n;
+  uint8_t* hm = c->hmeta.data();
+  memcpy(hm + ml.in_off, in_off, 8ull * n);
+  memcpy(hm + ml.in_len, in_len, 4ull * n);
+  memcpy(hm + ml.out_off, out_off, 8ull * n);
+  memcpy(hm + ml.out_cap, out_cap, 4ull * n);
+  uint64_t* pos_base = (uint64_t*)(hm + ml.pos_base);
+  uint32_t* blk_base = (uint32_t*)(hm + ml.blk_base);
+  uint64_t P = 0;
+  uint32_t B = 0, max_len = 0, max_blk = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
+    pos_base[i] = P;
+    blk_base[i] = B;
+    P += in_len[i];
+    const uint32_t nb = in_len[i] / ZS_SYM_END + 2;
+    B += nb;
+    max_len = std::max(max_len, in_len[i]);
+    max_blk = std::max(max_blk, nb);
+  }
+  HIPCHK(c->meta.ensure(ml.bytes));
+  HIPCHK(c->prevd.ensure(2 * P + 64));
+  HIPCHK(c->mres.ensure(8 * P + 64));
+  HIPCHK(c->syms.ensure(4 * (P + n) + 64));
+  HIPCHK(c->blocks.ensure(sizeof(zs_block) * (size_t)B));
+  HIPCHK(c->streams.ensure(sizeof(zs_stream) * (size_t)n));
+  HIPCHK(c->codes.ensure(4ull * (ZS_L_CODES + ZS_D_CODES) * B));
+  HIPCHK(c->hdr.ensure(4ull * ZS_HDR_WORDS * B));
+  HIPCHK(c->check.ensure(4ull * n));
+  HIPCHK(hipMemcpyAsync(c->meta.p, hm, ml.bytes, hipMemcpyHostToDevice, st));
+  uint8_t* dm = c->meta.as<uint8_t>();
+  const uint64_t* d_in_off = (const uint64_t*)(dm + ml.in_off);
+  const uint32_t* d_in_len = (const uint32_t*)(dm + ml.in_len);
+  const uint64_t* d_out_off = (const uint64_t*)(dm + ml.out_off);
+  const uint32_t* d_out_cap = (const uint32_t*)(dm + ml.out_cap);
+  const uint64_t* d_pos = (const uint64_t*)(dm + ml.pos_base);
+  const uint32_t* d_blk = (const uint32_t*)(dm + ml.blk_base);
+  zs_stream* d_st = c->streams.as<zs_stream>();
+  zs_block* d_bk = c->blocks.as<zs_block>();
+  const zs_level_cfg cfg = kLevels[level];
+  const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
+
+  mark(c, st, "start");
+  if (wrap) {
+    zs_k_checksum<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, c->check.as<uint32_t>(), wrap == 1 ? 1 : 2);
+    zs_k_copy_check<<<nblocks_s, nthreads_s, 0, st>>>(c->check.as<uint32_t>(), d_st, (int)n);
+    mark(c, st, "checksum");
+  }
+  if (level >= 4) {
+    zs_k_prev<<<n, 256, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+    mark(c, st, "prev");
+    dim3 g((max_len + 8191) / 8192, n);
+    if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
+                                                 c->mres.as<uint2>(), cfg.chain, cfg.nice);
+    mark(c, st, "match");
+    zs_k_parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), c->syms.as<uint32_t>(),
+                                 d_bk, d_st, cfg.good, cfg.lazy);
+    mark(c, st, "parse");
+  } else {
+    zs_k_fast<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st, cfg.chain,
+                                cfg.lazy, cfg.nice);
+    mark(c, st, "parse");
+  }
+  zs_k_trees<<<dim3(max_blk, n), 64, 0, st>>>(d_in, d_in_off, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
+                                              c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), (int)n);
+  mark(c, st, "trees");
+  zs_k_layout<<<nblocks_s, nthreads_s, 0, st>>>(d_blk, d_bk, d_st, d_out_cap, d_out, d_out_off, wrap, (int)n);
+  mark(c, st, "layout");
+  zs_k_emit<<<dim3(max_blk, n), 256, 0, st>>>(d_in, d_in_off, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
+                                              c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), d_out, d_out_off, wrap);
+  mark(c, st, "emit");
+  if (wrap) zs_k_wrap<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_out, d_out_off, d_in_len, wrap, level, (int)n);
+  zs_k_finish<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_status, d_out_len, (int)n);
+  mark(c, st, "finish");
+  HIPCHK(hipGetLastError());
+  collect_marks(c);
+  return ZS_OK;
+}
+
+// host-buffer wrapper shared by deflate / inflate
+static int stage_in(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                    std::vector<uint64_t>& doff, uint64_t& total) {
+  total = 0;
+  doff.resize(n);
+  for (uint32_t i = 0; i < n; i++) { doff[i] = total; total += in_len[i]; }
+  HIPCHK(c->d_in.ensure(total + 16));
+  for (uint32_t i = 0; i < n; i++)
+    if (in_len[i]) HIPCHK(hipMemcpyAsync(c->d_in.as<uint8_t>() + doff[i], in + in_off[i], in_len[i], hipMemcpyHostToDevice, c->stream));
+  return ZS_OK;
+}
+
+extern "C" int zs_deflate_batch(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* in, const uint64_t* in_off,
+                                const uint32_t* in_len, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                int32_t* status, uint32_t* out_len) {
+  if (!c) return fail(ZS_STREAM_ERROR, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<uint64_t> doff, ooff(n);
+  uint64_t total = 0, ototal = 0;
+  int r = stage_in(c, n, in, in_off, in_len, doff, total);
+  if (r != ZS_OK) return r;
+  std::vector<uint32_t> ocap(n);
+  for (uint32_t i = 0; i < n; i++) {
+    ooff[i] = ototal;
+    ocap[i] = out_cap[i] & ~3u;
+    ototal += ocap[i];
+  }
+  HIPCHK(c->d_out.ensure(ototal + 16));
+  HIPCHK(c->d_res.ensure(8ull * n + 16));
+  int32_t* d_status = c->d_res.as<int32_t>();
+  uint32_t* d_len = (uint32_t*)(d_status + n);
+  r = zs_deflate_batch_device(c, level, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len, c->d_out.as<uint8_t>(),
+                              ooff.data(), ocap.data(), d_status, d_len, c->stream);
+  if (r != ZS_OK) return r;
+  HIPCHK(hipMemcpyAsync(status, d_status, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(out_len, d_len, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < n; i++)
+    if (status[i] == ZS_STREAM_END && out_len[i])
+      HIPCHK(hipMemcpyAsync(out + out_off[i], c->d_out.as<uint8_t>() + ooff[i], out_len[i], hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return ZS_OK;
+}
+
+extern "C" int zs_crc32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                                     const uint32_t* in_len, uint32_t* d_check, void* hip_stream);
+extern "C" int zs_adler32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                                       const uint32_t* in_len, uint32_t* d_check, void* hip_stream);
+
+static int checksum_batch(zs_ctx* c, int kind, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                          const uint32_t* in_len, uint32_t* d_check, void* hip_stream) {
+  if (!c) return fail(ZS_STREAM_ERROR, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  if (n == 0) return ZS_OK;
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  MetaLayout ml(n);
+  c->hmeta.resize(ml.bytes);
+  memcpy(c->hmeta.data() + ml.in_off, in_off, 8ull * n);
+  memcpy(c->hmeta.data() + ml.in_len, in_len, 4ull * n);
+  HIPCHK(c->meta.ensure(ml.bytes));
+  HIPCHK(hipMemcpyAsync(c->meta.p, c->hmeta.data(), ml.bytes, hipMemcpyHostToDevice, st));
+  mark(c, st, "start");
+  zs_k_checksum<<<n, 64, 0, st>>>(d_in, (const uint64_t*)(c->meta.as<uint8_t>() + ml.in_off),
+                                  (const uint32_t*)(c->meta.as<uint8_t>() + ml.in_len), d_check, kind);
+  mark(c, st, "checksum");
+  HIPCHK(hipGetLastError());
+  collect_marks(c);
+  return ZS_OK;
+}
+
+extern "C" int zs_crc32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                                     const uint32_t* in_len, uint32_t* d_check, void* hip_stream) {
+  return checksum_batch(c, 2, n, d_in, in_off, in_len, d_check, hip_stream);
+}
+extern "C" int zs_adler32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                                       const uint32_t* in_len, uint32_t* d_check, void* hip_stream) {
+  return checksum_batch(c, 1, n, d_in, in_off, in_len, d_check, hip_stream);
+}
+
+// ------------------------------------------------------------------ corpus
+namespace {
+const char* kVocab =
+    "the of and to in is that for it as was with be by on not he this are or his from at which but have an they you "
+    "were her she there been one all we their has would when if so no will more can out said up what about its into "
+    "them than only other new some could time these two may then do first any my now such like our over man me even "
+    "most made after also did many before must through back years where much your way well down should because each "
+    "just those people how too little state good very make world still own see men work long get here between both "
+    "life being under never day same another know while last might us great old year off come since against go came "
+    "right used take three";
+
+struct XS {
+  uint32_t s;
+  explicit XS(uint32_t seed) : s(seed ? seed : 1) {}
+  uint32_t operator()() {
+    s ^= s << 13;
+    s ^= s >> 17;
+    s ^= s << 5;
+    return s;
+  }
+};
+
+void gen_text(uint32_t seed, uint8_t* out, uint32_t n, const std::vector<std::string>& V) {
+  XS r(seed);
+  uint32_t o = 0, w = 0;
+  while (o < n) {
+    const uint32_t a = r();
+    const uint32_t idx = std::min(a % 144u, (a >> 12) % 144u);
+    const std::string& word = V[idx];
+    for (size_t i = 0; i < word.size() && o < n; i++) out[o++] = (uint8_t)word[i];
+    if (o < n) out[o++] = (++w % 13 == 0) ? 10 : 32;
+  }
+}
+}  // namespace
+
+extern "C" void zs_corpus(int kind, uint32_t first, uint32_t n_streams, uint32_t len, uint8_t* out, int threads) {
+  std::vector<std::string> V;
+  {
+    std::string all(kVocab), cur;
+    for (char ch : all) {
+      if (ch == ' ') { V.push_back(cur); cur.clear(); }
+      else cur.push_back(ch);
+    }
+    V.push_back(cur);
+  }
+  auto one = [&](uint32_t i) {
+    const uint32_t seed = 0x9e3779b9u ^ (first + i);
+    uint8_t* o = out + (size_t)i * len;
+    if (kind == 2) {
+      XS r(seed);
+      for (uint32_t j = 0; j < len; j++) o[j] = (uint8_t)r();
+      return;
+    }
+    gen_text(seed, o, len, V);
+    if (kind == 1) {
+      XS r(seed ^ 0x85ebca6bu);
+      for (uint32_t k = 0; k + 8192 <= len; k += 8192)
+        for (uint32_t j = 0; j < 1024; j++) o[k + 4096 + j] = (uint8_t)r();
+    }
+  };
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([&, t] {
+      for (uint32_t i = (uint32_t)t; i < n_streams; i += (uint32_t)threads) one(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+// ------------------------------------------------------------ introspection
+// Copies an intermediate array of stream `s` of the last deflate batch to host
+// memory: what = 0 prevd (u16/position), 1 match table (u32x2/position),
+// 2 symbols (u32 each; count = streams[s].nsym), 3 blocks (zs_block each),
+// 4 stream record (zs_stream).  Returns the number of bytes copied.
+extern "C" uint64_t zs_debug_fetch(zs_ctx* c, int what, uint32_t s, void* dst, uint64_t cap) {
+  if (!c || !c->streams.p) return 0;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipDeviceSynchronize();
+  zs_stream st;
+  if (hipMemcpy(&st, c->streams.as<zs_stream>() + s, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  uint64_t pos_base = 0;
+  uint32_t blk_base = 0, n = 0;
+  // meta layout of the last call: recompute offsets from the host copy
+  const size_t nstreams = c->last_n;
+  MetaLayout m2((uint32_t)nstreams);
+  const uint8_t* hm = c->hmeta.data();
+  pos_base = ((const uint64_t*)(hm + m2.pos_base))[s];
+  blk_base = ((const uint32_t*)(hm + m2.blk_base))[s];
+  n = ((const uint32_t*)(hm + m2.in_len))[s];
+  const void* src = nullptr;
+  uint64_t bytes = 0;
+  switch (what) {
+    case 0: src = c->prevd.as<uint16_t>() + pos_base; bytes = 2ull * n; break;
+    case 1: src = c->mres.as<uint2>() + pos_base; bytes = 8ull * n; break;
+    case 2: src = c->syms.as<uint32_t>() + pos_base + s; bytes = 4ull * st.nsym; break;
+    case 3: src = c->blocks.as<zs_block>() + blk_base; bytes = sizeof(zs_block) * st.nblk; break;
+    case 4: src = c->streams.as<zs_stream>() + s; bytes = sizeof(zs_stream); break;
+    case 5: src = c->codes.as<uint32_t>() + (size_t)blk_base * (ZS_L_CODES + ZS_D_CODES); bytes = 4ull * (ZS_L_CODES + ZS_D_CODES) * st.nblk; break;
+    case 6: src = c->hdr.as<uint32_t>() + (size_t)blk_base * ZS_HDR_WORDS; bytes = 4ull * ZS_HDR_WORDS * st.nblk; break;
+    default: return 0;
+  }
+  bytes = std::min(bytes, cap);
+  if (bytes && hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  return bytes;
+}

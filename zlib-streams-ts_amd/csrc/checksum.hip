@@ -1,0 +1,96 @@
+// checksum.hip -- per-stream Adler-32 / CRC-32 of the input, for the zlib and
+// gzip wrappers (deflate.ts:155-159 update them in read_buf; the trailer is
+// written at deflate.ts:971-983).
+//
+// One wave per stream; lane i owns the i-th contiguous 1/64 of the stream.
+//   CRC-32 (common/crc32.ts:26-58): each lane computes the standard CRC of its
+//   segment from an LDS byte table; lane 0 then folds the 64 segment CRCs with
+//   crc32_combine arithmetic (multiplication by x^(8*len) modulo the reflected
+//   polynomial 0xedb88320).
+//   Adler-32 (common/adler32.ts:4-25): A = 1 + sum x_j, B = n + sum (n-j) x_j
+//   (mod 65521); each lane sums its segment, a wave reduction finishes it.
+#include <hip/hip_runtime.h>
+#include "zs_common.h"
+#include "zs_kernels.h"
+
+static __device__ uint32_t zs_multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ 0xedb88320u : b >> 1;
+  }
+  return p;
+}
+
+// x^(8 * len) mod P (reflected), by repeated squaring of x^8
+static __device__ uint32_t zs_x8nmodp(uint64_t len) {
+  uint32_t p = 1u << 31;   // x^0
+  uint32_t sq = 1u << 23;  // x^8
+  while (len) {
+    if (len & 1) p = zs_multmodp(sq, p);
+    sq = zs_multmodp(sq, sq);
+    len >>= 1;
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                    const uint32_t* __restrict__ in_len, uint32_t* __restrict__ check,
+                                                    int kind) {
+  __shared__ uint32_t T[256];
+  __shared__ uint32_t seg_crc[64];
+  const int s = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = in_len[s];
+  const uint8_t* src = in + in_off[s];
+  const uint32_t per = (n + 63) / 64;
+  const uint32_t b0 = min(n, lane * per), b1 = min(n, b0 + per);
+  if (kind == 2) {
+    for (uint32_t i = lane; i < 256; i += 64) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+      T[i] = c;
+    }
+    __syncthreads();
+    uint32_t c = 0xffffffffu;
+    for (uint32_t i = b0; i < b1; i++) c = (c >> 8) ^ T[(c ^ src[i]) & 0xff];
+    seg_crc[lane] = c ^ 0xffffffffu;
+    __syncthreads();
+    if (lane == 0) {
+      uint32_t crc = 0;  // crc32 of nothing (crc32.ts:27-29)
+      if (n) {
+        crc = seg_crc[0];
+        const uint32_t xp = zs_x8nmodp(per);
+        for (uint32_t i = 1; i < 64; i++) {
+          const uint32_t lo = min(n, i * per), hi = min(n, lo + per);
+          if (hi == lo) break;
+          const uint32_t xl = hi - lo == per ? xp : zs_x8nmodp(hi - lo);
+          crc = zs_multmodp(xl, crc) ^ seg_crc[i];
+        }
+      }
+      check[s] = crc;
+    }
+  } else {
+    uint64_t a = 0, w = 0;
+    for (uint32_t i = b0; i < b1; i++) {
+      a += src[i];
+      w += (uint64_t)(n - i) * src[i];
+      if (((i - b0) & 4095) == 4095) { a %= 65521; w %= 65521; }
+    }
+    a %= 65521;
+    w %= 65521;
+    for (int d = 32; d >= 1; d >>= 1) {
+      a += __shfl_down(a, d, 64);
+      w += __shfl_down(w, d, 64);
+    }
+    if (lane == 0) {
+      const uint32_t A = (uint32_t)((1 + a) % 65521);
+      const uint32_t B = (uint32_t)(((uint64_t)n % 65521 + w) % 65521);
+      check[s] = (B << 16) | A;
+    }
+  }
+}

@@ -1,0 +1,557 @@
+// deflate_emit.hip -- Huffman tree construction, block layout and bit packing.
+//
+//   zs_k_trees  : one wave per block.  The wave histograms the block's symbols
+//                 with LDS atomics; lane 0 then runs the reference's exact tree
+//                 construction (heap ordered by freq then depth, overflow
+//                 repair, canonical bit-reversed codes -- trees.ts:167-316),
+//                 the tree run-length coding (trees.ts:318-447) and the
+//                 stored/static/dynamic choice (trees.ts:554-583).  The code
+//                 table and the dynamic header bits go to global memory.
+//   zs_k_layout : one lane per stream: bit offset of every block (stored
+//                 blocks depend on byte alignment), output length, status, and
+//                 zeroing of the words that two writers share.
+//   zs_k_emit   : one 256-thread workgroup per block.  Symbol bit lengths are
+//                 prefix-summed across the workgroup; codes are OR-ed into an
+//                 LDS bit buffer aligned to the output's 32-bit word grid and
+//                 written out with coalesced stores (atomic OR only on the two
+//                 words a block shares with its neighbours).
+//   zs_k_wrap   : zlib / gzip header and trailer (deflate.ts:753-806, 964-983).
+#include <hip/hip_runtime.h>
+#include "zs_common.h"
+#include "zs_kernels.h"
+
+// ------------------------------------------------------------ tree building
+static constexpr int ZS_EXTRA_BLBITS[ZS_BL_CODES] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
+struct zs_tw {  // LDS workspace of one wave, common/types.ts DeflateState tree fields
+  uint16_t lfreq[ZS_HEAP_SIZE], llen[ZS_HEAP_SIZE], ldad[ZS_HEAP_SIZE], lcode[ZS_HEAP_SIZE];
+  uint16_t dfreq[2 * ZS_D_CODES + 1], dlen[2 * ZS_D_CODES + 1], ddad[2 * ZS_D_CODES + 1], dcode[2 * ZS_D_CODES + 1];
+  uint16_t bfreq[2 * ZS_BL_CODES + 1], blen[2 * ZS_BL_CODES + 1], bdad[2 * ZS_BL_CODES + 1], bcode[2 * ZS_BL_CODES + 1];
+  int16_t heap[2 * ZS_L_CODES + 1];
+  uint8_t depth[2 * ZS_L_CODES + 1];
+  uint16_t bl_count[16];
+  uint32_t hist[ZS_L_CODES + ZS_D_CODES];
+  uint32_t hdr[ZS_HDR_WORDS];
+};
+
+struct zs_tdesc {
+  uint16_t *freq, *len, *dad, *code;
+  const uint32_t* stat;  // static tree (code | len << 16) or nullptr
+  const int* extra;
+  int extra_base, elems, max_length, max_code;
+};
+
+struct zs_tstate {
+  zs_tw* w;
+  int heap_len, heap_max;
+  uint32_t opt_len, static_len;
+  // header bit writer
+  uint32_t hbits;
+};
+
+static __device__ __forceinline__ bool zs_smaller(const uint16_t* f, const uint8_t* depth, int n, int m) {
+  return f[n] < f[m] || (f[n] == f[m] && depth[n] <= depth[m]);  // trees.ts:163-165
+}
+
+static __device__ void zs_pqdownheap(zs_tstate& t, const uint16_t* f, int k) {  // trees.ts:167-185
+  int16_t* heap = t.w->heap;
+  const int v = heap[k];
+  int j = k << 1;
+  while (j <= t.heap_len) {
+    if (j < t.heap_len && zs_smaller(f, t.w->depth, heap[j + 1], heap[j])) j++;
+    if (zs_smaller(f, t.w->depth, v, heap[j])) break;
+    heap[k] = heap[j];
+    k = j;
+    j <<= 1;
+  }
+  heap[k] = (int16_t)v;
+}
+
+static __device__ void zs_gen_bitlen(zs_tstate& t, zs_tdesc& d) {  // trees.ts:187-259
+  int16_t* heap = t.w->heap;
+  uint16_t* bl_count = t.w->bl_count;
+  int h, n, m, bits, xbits, overflow = 0;
+  for (bits = 0; bits <= 15; bits++) bl_count[bits] = 0;
+  d.len[heap[t.heap_max]] = 0;
+  for (h = t.heap_max + 1; h < ZS_HEAP_SIZE; h++) {
+    n = heap[h];
+    bits = d.len[d.dad[n]] + 1;
+    if (bits > d.max_length) { bits = d.max_length; overflow++; }
+    d.len[n] = (uint16_t)bits;
+    if (n > d.max_code) continue;
+    bl_count[bits]++;
+    xbits = n >= d.extra_base ? d.extra[n - d.extra_base] : 0;
+    const uint32_t f = d.freq[n];
+    t.opt_len += f * (uint32_t)(bits + xbits);
+    if (d.stat) t.static_len += f * ((d.stat[n] >> 16) + (uint32_t)xbits);
+  }
+  if (overflow == 0) return;
+  do {
+    bits = d.max_length - 1;
+    while (bl_count[bits] == 0) bits--;
+    bl_count[bits]--;
+    bl_count[bits + 1] += 2;
+    bl_count[d.max_length]--;
+    overflow -= 2;
+  } while (overflow > 0);
+  for (bits = d.max_length; bits != 0; bits--) {
+    n = bl_count[bits];
+    while (n != 0) {
+      m = heap[--h];
+      if (m > d.max_code) continue;
+      if (d.len[m] != bits) {
+        t.opt_len += (uint32_t)((bits - (int)d.len[m]) * (int)d.freq[m]);
+        d.len[m] = (uint16_t)bits;
+      }
+      n--;
+    }
+  }
+}
+
+static __device__ void zs_gen_codes(zs_tstate& t, zs_tdesc& d) {  // trees.ts:54-76
+  uint16_t next_code[16];
+  uint32_t code = 0;
+  for (int bits = 1; bits <= 15; bits++) { code = (code + t.w->bl_count[bits - 1]) << 1; next_code[bits] = (uint16_t)code; }
+  for (int n = 0; n <= d.max_code; n++) {
+    const int len = d.len[n];
+    if (len == 0) continue;
+    const uint32_t c = next_code[len]++;
+    d.code[n] = (uint16_t)(__builtin_bitreverse32(c) >> (32 - len));
+  }
+}
+
+static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:261-316
+  int16_t* heap = t.w->heap;
+  uint8_t* depth = t.w->depth;
+  int n, m, max_code = -1, node;
+  t.heap_len = 0;
+  t.heap_max = ZS_HEAP_SIZE;
+  for (n = 0; n < d.elems; n++) {
+    if (d.freq[n] != 0) { heap[++t.heap_len] = (int16_t)(max_code = n); depth[n] = 0; }
+    else d.len[n] = 0;
+  }
+  while (t.heap_len < 2) {
+    node = heap[++t.heap_len] = (int16_t)(max_code < 2 ? ++max_code : 0);
+    d.freq[node] = 1;
+    depth[node] = 0;
+    t.opt_len--;
+    if (d.stat) t.static_len -= d.stat[node] >> 16;
+  }
+  d.max_code = max_code;
+  for (n = t.heap_len / 2; n >= 1; n--) zs_pqdownheap(t, d.freq, n);
+  node = d.elems;
+  do {
+    n = heap[1];
+    heap[1] = heap[t.heap_len--];
+    zs_pqdownheap(t, d.freq, 1);
+    m = heap[1];
+    heap[--t.heap_max] = (int16_t)n;
+    heap[--t.heap_max] = (int16_t)m;
+    d.freq[node] = (uint16_t)(d.freq[n] + d.freq[m]);
+    depth[node] = (uint8_t)((depth[n] >= depth[m] ? depth[n] : depth[m]) + 1);
+    d.dad[n] = d.dad[m] = (uint16_t)node;
+    heap[1] = (int16_t)node++;
+    zs_pqdownheap(t, d.freq, 1);
+  } while (t.heap_len >= 2);
+  heap[--t.heap_max] = heap[1];
+  zs_gen_bitlen(t, d);
+  zs_gen_codes(t, d);
+}
+
+static __device__ void zs_scan_tree(zs_tstate& t, zs_tdesc& d, int max_code) {  // trees.ts:318-363
+  uint16_t* bf = t.w->bfreq;
+  int prevlen = -1, curlen, nextlen = d.len[0], count = 0, max_count = 7, min_count = 4;
+  if (nextlen == 0) { max_count = 138; min_count = 3; }
+  d.len[max_code + 1] = 0xffff;
+  for (int n = 0; n <= max_code; n++) {
+    curlen = nextlen;
+    nextlen = d.len[n + 1];
+    if (++count < max_count && curlen == nextlen) continue;
+    else if (count < min_count) bf[curlen] = (uint16_t)(bf[curlen] + count);
+    else if (curlen != 0) { if (curlen != prevlen) bf[curlen]++; bf[16]++; }
+    else if (count <= 10) bf[17]++;
+    else bf[18]++;
+    count = 0;
+    prevlen = curlen;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+    else { max_count = 7; min_count = 4; }
+  }
+}
+
+static __device__ __forceinline__ void zs_hput(zs_tstate& t, uint32_t v, int n) {
+  uint32_t* h = t.w->hdr;
+  const uint32_t pos = t.hbits;
+  h[pos >> 5] |= v << (pos & 31);
+  if ((pos & 31) + n > 32) h[(pos >> 5) + 1] |= v >> (32 - (pos & 31));
+  t.hbits += n;
+}
+
+static __device__ void zs_send_tree(zs_tstate& t, zs_tdesc& d, int max_code) {  // trees.ts:365-414
+  const uint16_t* bc = t.w->bcode;
+  const uint16_t* bl = t.w->blen;
+  int prevlen = -1, curlen, nextlen = d.len[0], count = 0, max_count = 7, min_count = 4;
+  if (nextlen == 0) { max_count = 138; min_count = 3; }
+  for (int n = 0; n <= max_code; n++) {
+    curlen = nextlen;
+    nextlen = d.len[n + 1];
+    if (++count < max_count && curlen == nextlen) continue;
+    else if (count < min_count) { do zs_hput(t, bc[curlen], bl[curlen]); while (--count != 0); }
+    else if (curlen != 0) {
+      if (curlen != prevlen) { zs_hput(t, bc[curlen], bl[curlen]); count--; }
+      zs_hput(t, bc[16], bl[16]);
+      zs_hput(t, (uint32_t)(count - 3), 2);
+    } else if (count <= 10) { zs_hput(t, bc[17], bl[17]); zs_hput(t, (uint32_t)(count - 3), 3); }
+    else { zs_hput(t, bc[18], bl[18]); zs_hput(t, (uint32_t)(count - 11), 7); }
+    count = 0;
+    prevlen = curlen;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+    else { max_count = 7; min_count = 4; }
+  }
+}
+
+__global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                 const uint64_t* __restrict__ pos_base,
+                                                 const uint32_t* __restrict__ blk_base,
+                                                 const uint32_t* __restrict__ syms, zs_block* __restrict__ blocks,
+                                                 const zs_stream* __restrict__ streams, uint32_t* __restrict__ codes,
+                                                 uint32_t* __restrict__ hdr, int nstreams) {
+  __shared__ zs_tw w;
+  const int s = blockIdx.y;
+  const uint32_t b = blockIdx.x;
+  if (b >= streams[s].nblk) return;
+  const uint32_t bi = blk_base[s] + b;
+  zs_block blk = blocks[bi];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t* sy = syms + pos_base[s] + s + blk.sym_start;
+  for (uint32_t i = lane; i < ZS_L_CODES + ZS_D_CODES; i += 64) w.hist[i] = 0;
+  for (uint32_t i = lane; i < ZS_HDR_WORDS; i += 64) w.hdr[i] = 0;
+  __syncthreads();
+  // histogram (deflate/utils.ts:55-81 tallies, done in parallel)
+  for (uint32_t i = lane; i < blk.sym_count; i += 64) {
+    const uint32_t v = sy[i];
+    if (v & 0x80000000u) {
+      const uint32_t lc = (v >> 16) & 0xff, dist = (v & 0xffffu) - 1;
+      atomicAdd(&w.hist[ZS_LENGTH_CODE[lc] + 257], 1u);
+      atomicAdd(&w.hist[ZS_L_CODES + (dist < 256 ? ZS_DIST_CODE[dist] : ZS_DIST_CODE[256 + (dist >> 7)])], 1u);
+    } else {
+      atomicAdd(&w.hist[v], 1u);
+    }
+  }
+  __syncthreads();
+  if (lane != 0) return;
+
+  // init_block (trees.ts:90-103) + tally counts
+  for (int i = 0; i < ZS_L_CODES; i++) w.lfreq[i] = (uint16_t)w.hist[i];
+  w.lfreq[ZS_END_BLOCK] = 1;
+  for (int i = 0; i < ZS_D_CODES; i++) w.dfreq[i] = (uint16_t)w.hist[ZS_L_CODES + i];
+  for (int i = 0; i < ZS_BL_CODES; i++) w.bfreq[i] = 0;
+  zs_tstate t;
+  t.w = &w;
+  t.opt_len = 0;
+  t.static_len = 0;
+  t.hbits = 0;
+  zs_tdesc L = {w.lfreq, w.llen, w.ldad, w.lcode, ZS_STATIC_LTREE, ZS_EXTRA_LBITS, 257, ZS_L_CODES, 15, 0};
+  zs_tdesc D = {w.dfreq, w.dlen, w.ddad, w.dcode, ZS_STATIC_DTREE, ZS_EXTRA_DBITS, 0, ZS_D_CODES, 15, 0};
+  zs_tdesc B = {w.bfreq, w.blen, w.bdad, w.bcode, nullptr, nullptr, 0, ZS_BL_CODES, 7, 0};
+  B.extra = ZS_EXTRA_BLBITS;
+  zs_build_tree(t, L);
+  zs_build_tree(t, D);
+  // build_bl_tree (trees.ts:416-432)
+  zs_scan_tree(t, L, L.max_code);
+  zs_scan_tree(t, D, D.max_code);
+  zs_build_tree(t, B);
+  int max_blindex;
+  for (max_blindex = ZS_BL_CODES - 1; max_blindex >= 3; max_blindex--)
+    if (w.blen[ZS_BL_ORDER[max_blindex]] != 0) break;
+  t.opt_len += 3u * ((uint32_t)max_blindex + 1) + 5 + 5 + 4;
+  uint32_t opt_lenb = (t.opt_len + 3 + 7) >> 3;
+  const uint32_t static_lenb = (t.static_len + 3 + 7) >> 3;
+  if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+  const uint32_t stored_len = blk.in_end - blk.in_start;
+  uint32_t type;
+  if (stored_len + 4 <= opt_lenb) type = 0;
+  else if (static_lenb == opt_lenb) type = 1;
+  else type = 2;
+  // exact payload bits of the chosen coding, from the true counts
+  uint32_t data_bits = 0;
+  uint32_t* cout = codes + (size_t)bi * (ZS_L_CODES + ZS_D_CODES);
+  if (type != 0) {
+    for (int i = 0; i < ZS_L_CODES; i++) {
+      const uint32_t f = i == ZS_END_BLOCK ? 1u : w.hist[i];
+      if (!f) continue;
+      const uint32_t len = type == 1 ? ZS_STATIC_LTREE[i] >> 16 : w.llen[i];
+      data_bits += f * (len + (i >= 257 ? (uint32_t)ZS_EXTRA_LBITS[i - 257] : 0u));
+    }
+    for (int i = 0; i < ZS_D_CODES; i++) {
+      const uint32_t f = w.hist[ZS_L_CODES + i];
+      if (!f) continue;
+      const uint32_t len = type == 1 ? 5u : w.dlen[i];
+      data_bits += f * (len + (uint32_t)ZS_EXTRA_DBITS[i]);
+    }
+  }
+  if (type == 2) {
+    // send_all_trees (trees.ts:434-447)
+    const int lcodes = L.max_code + 1, dcodes = D.max_code + 1, blcodes = max_blindex + 1;
+    zs_hput(t, (uint32_t)(lcodes - 257), 5);
+    zs_hput(t, (uint32_t)(dcodes - 1), 5);
+    zs_hput(t, (uint32_t)(blcodes - 4), 4);
+    for (int rank = 0; rank < blcodes; rank++) zs_hput(t, w.blen[ZS_BL_ORDER[rank]], 3);
+    zs_send_tree(t, L, lcodes - 1);
+    zs_send_tree(t, D, dcodes - 1);
+    for (int i = 0; i < ZS_L_CODES; i++) cout[i] = w.lcode[i] | ((uint32_t)w.llen[i] << 16);
+    for (int i = 0; i < ZS_D_CODES; i++) cout[ZS_L_CODES + i] = w.dcode[i] | ((uint32_t)w.dlen[i] << 16);
+    uint32_t* hout = hdr + (size_t)bi * ZS_HDR_WORDS;
+    for (uint32_t i = 0; i < (t.hbits + 31) / 32; i++) hout[i] = w.hdr[i];
+  }
+  blk.type = type;
+  blk.hdr_bits = type == 2 ? t.hbits : 0;
+  blk.data_bits = data_bits;
+  blocks[bi] = blk;
+}
+
+// --------------------------------------------------------------- layout
+__global__ void zs_k_layout(const uint32_t* __restrict__ blk_base, zs_block* __restrict__ blocks,
+                            zs_stream* __restrict__ streams, const uint32_t* __restrict__ out_cap,
+                            uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, int wrap, int nstreams) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstreams) return;
+  zs_stream st = streams[s];
+  const uint32_t hl = wrap == 1 ? 2u : wrap == 2 ? 10u : 0u, tl = wrap == 1 ? 4u : wrap == 2 ? 8u : 0u;
+  uint64_t off = (uint64_t)hl * 8;
+  zs_block* blk = blocks + blk_base[s];
+  int bad = 0;
+  for (uint32_t b = 0; b < st.nblk; b++) {
+    zs_block k = blk[b];
+    k.bit_off = off;
+    if (k.type == 0) {
+      if (k.last & 2u) bad = 1;  // stored block starting before the slid window: not reproducible
+      off += 3;
+      off = (off + 7) & ~7ull;
+      off += 32 + 8ull * (k.in_end - k.in_start);
+    } else {
+      off += 3 + k.hdr_bits + k.data_bits;
+    }
+    k.bit_end = off;
+    if (k.last & 1u) off = (off + 7) & ~7ull;  // bi_windup (trees.ts:587-589)
+    blk[b] = k;
+  }
+  st.total_bits = off;
+  const uint64_t out_len = off / 8 + tl;
+  st.out_len = (uint32_t)out_len;
+  st.status = bad ? ZS_Z_STREAM_ERROR : (out_len <= out_cap[s] ? ZS_Z_STREAM_END : ZS_Z_BUF_ERROR);
+  streams[s] = st;
+  if (st.status != ZS_Z_STREAM_END) return;
+  // zero the words written by more than one writer (atomic OR targets)
+  uint32_t* ow = (uint32_t*)(out + out_off[s]);
+  for (uint32_t i = 0; i < (hl + 3) / 4; i++) ow[i] = 0;
+  for (uint32_t b = 0; b < st.nblk; b++) {
+    const zs_block k = blk[b];
+    ow[k.bit_off >> 5] = 0;
+    ow[(k.bit_end - 1) >> 5] = 0;
+  }
+  const uint64_t tb = off / 8;
+  for (uint64_t by = tb > 0 ? tb - 1 : 0; by < (out_len + 3) / 4 * 4; by += 4) ow[by >> 2] = 0;
+}
+
+// -------------------------------------------------------------------- emit
+#define ZS_EMIT_THREADS 256
+#define ZS_STAGE_WORDS 2048
+#define ZS_EMIT_PER_THREAD 4
+
+static __device__ __forceinline__ uint32_t zs_block_scan(uint32_t v, uint32_t* tmp, uint32_t& total) {
+  // exclusive scan over the 256-thread workgroup
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) tmp[wv] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (uint32_t i = 0; i < wv; i++) pre += tmp[i];
+  total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+  __syncthreads();
+  return pre + x - v;
+}
+
+static __device__ __forceinline__ void zs_stage_or(uint32_t* st, uint64_t rel, uint64_t v, uint32_t n) {
+  if (!n) return;
+  const uint32_t wi = (uint32_t)(rel >> 5), sh = (uint32_t)(rel & 31);
+  atomicOr(&st[wi], (uint32_t)(v << sh));
+  if (sh + n > 32) atomicOr(&st[wi + 1], (uint32_t)(v >> (32 - sh)));
+  if (sh + n > 64) atomicOr(&st[wi + 2], (uint32_t)(v >> (64 - sh)));
+}
+
+__global__ __launch_bounds__(ZS_EMIT_THREADS) void zs_k_emit(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ pos_base,
+    const uint32_t* __restrict__ blk_base, const uint32_t* __restrict__ syms, const zs_block* __restrict__ blocks,
+    const zs_stream* __restrict__ streams, const uint32_t* __restrict__ codes, const uint32_t* __restrict__ hdr,
+    uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, int wrap) {
+  __shared__ uint32_t stage[ZS_STAGE_WORDS + 4];
+  __shared__ uint32_t tbl[ZS_L_CODES + ZS_D_CODES];
+  __shared__ uint32_t scan_tmp[4];
+  const int s = blockIdx.y;
+  const uint32_t b = blockIdx.x;
+  const zs_stream st = streams[s];
+  if (b >= st.nblk || st.status != ZS_Z_STREAM_END) return;
+  const uint32_t bi = blk_base[s] + b;
+  const zs_block blk = blocks[bi];
+  uint32_t* ow = (uint32_t*)(out + out_off[s]);
+  const uint64_t off0 = blk.bit_off, off1 = blk.bit_end;
+  const uint64_t first_w = off0 >> 5, last_w = (off1 - 1) >> 5;
+  const bool first_shared = (off0 & 31) != 0, last_shared = (off1 & 31) != 0;
+  auto put_word = [&](uint64_t gw, uint32_t v) {
+    if ((gw == first_w && first_shared) || (gw == last_w && last_shared)) {
+      if (v) atomicOr(&ow[gw], v);
+    } else {
+      ow[gw] = v;
+    }
+  };
+  const uint32_t hdr3 = (blk.type << 1) | (blk.last & 1u);  // block header (trees.ts:449-451,578,581)
+
+  if (blk.type == 0) {  // stored block: every word computed independently (trees.ts:449-464)
+    const uint8_t* src = in + in_off[s] + blk.in_start;
+    const uint32_t slen = blk.in_end - blk.in_start;
+    const uint64_t B0 = ((off0 + 3 + 7) & ~7ull) >> 3;  // first byte after bi_windup
+    const uint64_t B1 = B0 + 4 + slen;
+    for (uint64_t gw = first_w + threadIdx.x; gw <= last_w; gw += ZS_EMIT_THREADS) {
+      uint32_t v = 0;
+      if (gw == first_w) v |= hdr3 << (off0 & 31);
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint64_t by = gw * 4 + k;
+        if (by < B0 || by >= B1) continue;
+        const uint64_t r = by - B0;
+        uint32_t c;
+        if (r < 2) c = (slen >> (8 * r)) & 0xff;
+        else if (r < 4) c = (~slen >> (8 * (r - 2))) & 0xff;
+        else c = src[r - 4];
+        v |= c << (8 * k);
+      }
+      put_word(gw, v);
+    }
+    return;
+  }
+
+  // Huffman-coded block
+  const uint32_t* ctab = codes + (size_t)bi * (ZS_L_CODES + ZS_D_CODES);
+  for (uint32_t i = threadIdx.x; i < ZS_L_CODES + ZS_D_CODES; i += ZS_EMIT_THREADS) {
+    if (blk.type == 1) tbl[i] = i < ZS_L_CODES ? ZS_STATIC_LTREE[i] : ZS_STATIC_DTREE[i - ZS_L_CODES];
+    else tbl[i] = ctab[i];
+  }
+  for (uint32_t i = threadIdx.x; i < ZS_STAGE_WORDS + 4; i += ZS_EMIT_THREADS) stage[i] = 0;
+  __syncthreads();
+  uint64_t wbase = first_w;  // global word index of stage[0]
+  uint64_t pos = off0;
+  if (threadIdx.x == 0) zs_stage_or(stage, pos - wbase * 32, hdr3, 3);
+  pos += 3;
+  if (blk.type == 2) {
+    const uint32_t* hsrc = hdr + (size_t)bi * ZS_HDR_WORDS;
+    const uint32_t hw = (blk.hdr_bits + 31) / 32;
+    for (uint32_t i = threadIdx.x; i < hw; i += ZS_EMIT_THREADS) {
+      const uint32_t nb = min(32u, blk.hdr_bits - 32 * i);
+      const uint32_t v = nb == 32 ? hsrc[i] : (hsrc[i] & ((1u << nb) - 1));
+      zs_stage_or(stage, pos - wbase * 32 + 32 * i, v, nb);
+    }
+    pos += blk.hdr_bits;
+  }
+  __syncthreads();
+  const uint32_t* sy = syms + pos_base[s] + s + blk.sym_start;
+  const uint32_t nsym = blk.sym_count;
+  const uint32_t chunk = ZS_EMIT_THREADS * ZS_EMIT_PER_THREAD;
+  for (uint32_t c0 = 0;; c0 += chunk) {
+    const bool final_chunk = c0 + chunk >= nsym;
+    uint64_t v[ZS_EMIT_PER_THREAD];
+    uint32_t n[ZS_EMIT_PER_THREAD];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < ZS_EMIT_PER_THREAD; k++) {
+      const uint32_t i = c0 + threadIdx.x * ZS_EMIT_PER_THREAD + k;
+      v[k] = 0;
+      n[k] = 0;
+      if (i < nsym) {
+        const uint32_t x = sy[i];
+        if (x & 0x80000000u) {  // compress_block (trees.ts:476-520)
+          const uint32_t lc = (x >> 16) & 0xff, dist = (x & 0xffffu) - 1;
+          const uint32_t code = ZS_LENGTH_CODE[lc];
+          const uint32_t e1 = tbl[code + 257];
+          uint32_t nb = e1 >> 16;
+          uint64_t acc = e1 & 0xffffu;
+          const uint32_t xl = (uint32_t)ZS_EXTRA_LBITS[code];
+          // code 285 (length 258) has no extra bits: lc - base must not leak (trees.ts:495-499)
+          acc |= (uint64_t)((lc - (uint32_t)ZS_BASE_LENGTH[code]) & ((1u << xl) - 1)) << nb;
+          nb += xl;
+          const uint32_t dc = dist < 256 ? ZS_DIST_CODE[dist] : ZS_DIST_CODE[256 + (dist >> 7)];
+          const uint32_t e2 = tbl[ZS_L_CODES + dc];
+          acc |= (uint64_t)(e2 & 0xffffu) << nb;
+          nb += e2 >> 16;
+          acc |= (uint64_t)(dist - (uint32_t)ZS_BASE_DIST[dc]) << nb;
+          nb += (uint32_t)ZS_EXTRA_DBITS[dc];
+          v[k] = acc;
+          n[k] = nb;
+        } else {
+          const uint32_t e = tbl[x];
+          v[k] = e & 0xffffu;
+          n[k] = e >> 16;
+        }
+      }
+      tot += n[k];
+    }
+    uint32_t total;
+    const uint32_t pre = zs_block_scan(tot, scan_tmp, total);
+    uint64_t rel = pos - wbase * 32 + pre;
+#pragma unroll
+    for (int k = 0; k < ZS_EMIT_PER_THREAD; k++) {
+      zs_stage_or(stage, rel, v[k], n[k]);
+      rel += n[k];
+    }
+    pos += total;
+    if (final_chunk && threadIdx.x == 0) {  // END_BLOCK
+      const uint32_t e = tbl[ZS_END_BLOCK];
+      zs_stage_or(stage, pos - wbase * 32, e & 0xffffu, e >> 16);
+    }
+    if (final_chunk) pos += tbl[ZS_END_BLOCK] >> 16;
+    __syncthreads();
+    // write out complete words; keep the partial one
+    const uint64_t done_w = final_chunk ? ((pos + 31) >> 5) : (pos >> 5);
+    const uint32_t nw = (uint32_t)(done_w - wbase);
+    for (uint32_t i = threadIdx.x; i < nw; i += ZS_EMIT_THREADS) put_word(wbase + i, stage[i]);
+    if (final_chunk) break;
+    __syncthreads();
+    const uint32_t carry = stage[nw];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ZS_STAGE_WORDS + 4; i += ZS_EMIT_THREADS) stage[i] = i == 0 ? carry : 0u;
+    wbase = done_w;
+    __syncthreads();
+  }
+}
+
+// -------------------------------------------------------------------- wrap
+__global__ void zs_k_wrap(const zs_stream* __restrict__ streams, uint8_t* __restrict__ out,
+                          const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ in_len, int wrap,
+                          int level, int nstreams) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstreams || wrap == 0) return;
+  const zs_stream st = streams[s];
+  if (st.status != ZS_Z_STREAM_END) return;
+  uint32_t* ow = (uint32_t*)(out + out_off[s]);
+  auto put_byte = [&](uint64_t at, uint32_t c) { atomicOr(&ow[at >> 2], (c & 0xffu) << (8 * (at & 3))); };
+  const uint64_t tb = st.total_bits / 8;
+  if (wrap == 1) {  // zlib: deflate.ts:753-786, 980-983
+    uint32_t header = (8u + ((15u - 8u) << 4)) << 8;
+    const uint32_t lf = level < 2 ? 0u : level < 6 ? 1u : level == 6 ? 2u : 3u;
+    header |= lf << 6;
+    header += 31 - (header % 31);
+    put_byte(0, header >> 8);
+    put_byte(1, header);
+    for (int i = 0; i < 4; i++) put_byte(tb + i, st.check >> (24 - 8 * i));
+  } else {  // gzip: deflate.ts:787-806, 971-979
+    const uint32_t xfl = level == 9 ? 2u : level < 2 ? 4u : 0u;
+    const uint8_t h[10] = {31, 139, 8, 0, 0, 0, 0, 0, (uint8_t)xfl, 255};
+    for (int i = 0; i < 10; i++) put_byte(i, h[i]);
+    for (int i = 0; i < 4; i++) put_byte(tb + i, st.check >> (8 * i));
+    for (int i = 0; i < 4; i++) put_byte(tb + 4 + i, in_len[s] >> (8 * i));
+  }
+}

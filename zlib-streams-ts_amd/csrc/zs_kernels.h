@@ -1,0 +1,54 @@
+// zs_kernels.h -- kernel entry points and the batch descriptor shared by the
+// HIP translation units and the C-ABI host layer (capi.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// Per-block record written by the parse / tree kernels.
+struct zs_block {
+  uint32_t sym_start;   // first symbol (index into the stream's symbol array)
+  uint32_t sym_count;
+  uint32_t in_start;    // input byte range covered by the block
+  uint32_t in_end;
+  uint32_t type;        // 0 stored, 1 static, 2 dynamic (trees.ts:574-583)
+  uint32_t hdr_bits;    // dynamic-tree header bits (send_all_trees)
+  uint32_t data_bits;   // symbol bits incl. END_BLOCK
+  uint32_t last;        // bit 0: final block; bit 1: block began before the slid window (reference would copy from a negative index)
+  uint32_t pad;
+  uint64_t bit_off;     // bit offset of the 3-bit block header in the stream output
+  uint64_t bit_end;     // bit offset just past the block (before the final byte pad)
+};
+
+// Per-stream record.
+struct zs_stream {
+  uint32_t nsym;
+  uint32_t nblk;
+  uint64_t total_bits;  // deflate payload bits (after the wrapper header)
+  uint32_t out_len;     // bytes incl. wrapper
+  int32_t status;       // Z_STREAM_END / Z_BUF_ERROR
+  uint32_t check;       // adler32 / crc32 of the input (wrappers)
+  uint32_t pad;
+};
+
+__global__ void zs_k_prev(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                          uint16_t* prevd);
+__global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                           const uint16_t* prevd, uint2* mres, int chain, int nice);
+__global__ void zs_k_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                           const uint32_t* blk_base, const uint2* mres, uint32_t* syms, zs_block* blocks,
+                           zs_stream* streams, int good, int lazy);
+__global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                          const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,
+                          int lazy, int nice);
+__global__ void zs_k_trees(const uint8_t* in, const uint64_t* in_off, const uint64_t* pos_base, const uint32_t* blk_base,
+                           const uint32_t* syms, zs_block* blocks, const zs_stream* streams, uint32_t* codes,
+                           uint32_t* hdr, int nstreams);
+__global__ void zs_k_layout(const uint32_t* blk_base, zs_block* blocks, zs_stream* streams, const uint32_t* out_cap,
+                            uint8_t* out, const uint64_t* out_off, int wrap, int nstreams);
+__global__ void zs_k_emit(const uint8_t* in, const uint64_t* in_off, const uint64_t* pos_base, const uint32_t* blk_base,
+                          const uint32_t* syms, const zs_block* blocks, const zs_stream* streams, const uint32_t* codes,
+                          const uint32_t* hdr, uint8_t* out, const uint64_t* out_off, int wrap);
+__global__ void zs_k_wrap(const zs_stream* streams, uint8_t* out, const uint64_t* out_off, const uint32_t* in_len,
+                          int wrap, int level, int nstreams);
+__global__ void zs_k_checksum(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t* check,
+                              int kind);

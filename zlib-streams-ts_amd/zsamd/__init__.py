@@ -1,0 +1,329 @@
+"""zsamd -- Python host binding of the MI355X batched deflate/inflate engine.
+
+Mirrors the reference's public surface (src/streams-api.ts, src/mod/streams.ts):
+
+* ``CompressionStream(format, level=...)`` / ``DecompressionStream(format)`` with
+  ``write()`` / ``close()`` / ``read()`` -- one stream, run as a batch of one.
+* ``compress_batch(inputs, format, level)`` / ``decompress_batch(inputs, format)``
+  -- the batch entry the north star adds to ``streams-api.ts``; stream i yields
+  exactly what piping ``inputs[i]`` alone through the reference stream class
+  (one ``write()`` then ``close()``) yields, or raises/reports the same error.
+
+Everything runs on the GPU through the C-ABI in ``libzsgpu.so``
+(include/zs_gpu.h).  There is no CPU fallback: if the library or a GPU is
+missing, every entry point raises ``ZsUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libzsgpu.so")
+
+Z_OK, Z_STREAM_END, Z_NEED_DICT = 0, 1, 2
+Z_STREAM_ERROR, Z_DATA_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = -2, -3, -4, -5
+PHASE_NONE, PHASE_INIT, PHASE_PROCESS, PHASE_FINISH = 0, 1, 2, 3
+
+# format -> windowBits, streams.ts:220 (compression) and :233 (decompression).
+# Unknown strings fall through to 15 there ("deflate"); the same here.
+def compress_wbits(fmt: str) -> int:
+    return 31 if fmt == "gzip" else (-15 if fmt == "deflate-raw" else 15)
+
+
+def decompress_wbits(fmt: str) -> int:
+    if fmt == "gzip":
+        return 31
+    if fmt == "deflate-raw":
+        return -15
+    if fmt == "deflate64-raw":
+        return -16
+    return 15
+
+
+class ZsUnavailable(RuntimeError):
+    """The HIP engine (libzsgpu.so) or a GPU is not available."""
+
+
+class ZsError(Exception):
+    """Mirrors the Error the reference stream layer throws (streams.ts:53,117,170)."""
+
+    def __init__(self, message: str, status: int = 0, phase: int = 0, msg: str = ""):
+        super().__init__(message)
+        self.status, self.phase, self.msg = status, phase, msg
+
+
+def stream_error_text(status: int, phase: int) -> str:
+    if phase == PHASE_INIT:
+        return "init failed: %d" % status
+    if phase == PHASE_FINISH:
+        return "finalization error: %d" % status
+    return "process error: %d" % status
+
+
+_lib = None
+_P = ctypes.c_void_p
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_U32P = ctypes.POINTER(ctypes.c_uint32)
+_I32P = ctypes.POINTER(ctypes.c_int32)
+
+
+def lib():
+    """Load libzsgpu.so (raises ZsUnavailable when it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ZsUnavailable("libzsgpu.so not built: run `make -C zlib-streams-ts_amd/csrc` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    L.zs_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(_P)]
+    L.zs_ctx_destroy.argtypes = [_P]
+    L.zs_last_error.restype = ctypes.c_char_p
+    L.zs_version.restype = ctypes.c_char_p
+    L.zs_deflate_bound.restype = ctypes.c_uint64
+    L.zs_deflate_bound.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    L.zs_deflate_batch_device.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, _P, _U64P, _U32P, _P, _U64P,
+                                          _U32P, _P, _P, _P]
+    L.zs_deflate_batch.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p, _U64P, _U32P,
+                                   _P, _U64P, _U32P, _I32P, _U32P]
+    if hasattr(L, "zs_inflate_batch"):
+        L.zs_inflate_batch.argtypes = [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p, _U64P, _U32P, _P, _U64P,
+                                       _U32P, _I32P, _I32P, _I32P, _U32P, _U32P]
+        L.zs_inflate_batch_device.argtypes = [_P, ctypes.c_int, ctypes.c_uint32, _P, _U64P, _U32P, _P, _U64P, _U32P,
+                                              _P, _P, _P, _P, _P, _P]
+        L.zs_inflate_message.restype = ctypes.c_char_p
+        L.zs_inflate_message.argtypes = [ctypes.c_int32]
+    L.zs_crc32_batch_device.argtypes = [_P, ctypes.c_uint32, _P, _U64P, _U32P, _P, _P]
+    L.zs_adler32_batch_device.argtypes = [_P, ctypes.c_uint32, _P, _U64P, _U32P, _P, _P]
+    L.zs_last_batch_ms.restype = ctypes.c_double
+    L.zs_last_batch_ms.argtypes = [_P]
+    L.zs_last_phase_ms.restype = ctypes.c_double
+    L.zs_last_phase_ms.argtypes = [_P, ctypes.c_char_p]
+    L.zs_set_timing.argtypes = [_P, ctypes.c_int]
+    L.zs_corpus.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P, ctypes.c_int]
+    _lib = L
+    return L
+
+
+def _arr(ctype, values):
+    a = (ctype * max(1, len(values)))(*values)
+    return a
+
+
+def deflate_bound(n: int, fmt: str = "deflate-raw") -> int:
+    return int(lib().zs_deflate_bound(n, compress_wbits(fmt)))
+
+
+class Engine:
+    """One device context (one per GPU / process)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        ctx = _P()
+        r = L.zs_ctx_create(device, ctypes.byref(ctx))
+        if r != 0:
+            raise ZsUnavailable("zs_ctx_create(%d) failed: %s" % (device, L.zs_last_error().decode()))
+        self._L, self._ctx, self.device = L, ctx, device
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._L.zs_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def set_timing(self, on: bool):
+        self._L.zs_set_timing(self._ctx, 1 if on else 0)
+
+    def last_ms(self, phase: Optional[str] = None) -> float:
+        if phase is None:
+            return self._L.zs_last_batch_ms(self._ctx)
+        return self._L.zs_last_phase_ms(self._ctx, phase.encode())
+
+    def _check(self, r: int, what: str):
+        if r != 0:
+            msg = self._L.zs_last_error().decode()
+            if r == Z_STREAM_ERROR:
+                raise ZsError("init failed: %d" % r, r, PHASE_INIT, msg)
+            raise ZsUnavailable("%s failed (%d): %s" % (what, r, msg))
+
+    # ---------------------------------------------------------- host buffers
+    def compress_batch_raw(self, inputs: Sequence[bytes], fmt: str = "deflate-raw", level: int = -1
+                           ) -> List[Tuple[int, bytes]]:
+        """Returns [(status, bytes)] -- status Z_STREAM_END on success."""
+        n = len(inputs)
+        if n == 0:
+            return []
+        wbits = compress_wbits(fmt)
+        blob = b"".join(inputs)
+        offs, lens, o = [], [], 0
+        for b in inputs:
+            offs.append(o)
+            lens.append(len(b))
+            o += len(b)
+        caps = [int(self._L.zs_deflate_bound(len(b), wbits)) for b in inputs]
+        ooffs, oo = [], 0
+        for c in caps:
+            ooffs.append(oo)
+            oo += c
+        out = ctypes.create_string_buffer(max(1, oo))
+        status = (ctypes.c_int32 * n)()
+        olen = (ctypes.c_uint32 * n)()
+        r = self._L.zs_deflate_batch(self._ctx, level, wbits, n, blob, _arr(ctypes.c_uint64, offs),
+                                     _arr(ctypes.c_uint32, lens), out, _arr(ctypes.c_uint64, ooffs),
+                                     _arr(ctypes.c_uint32, caps), status, olen)
+        self._check(r, "zs_deflate_batch")
+        raw = out.raw
+        return [(status[i], raw[ooffs[i]: ooffs[i] + olen[i]]) for i in range(n)]
+
+    def compress_batch(self, inputs: Sequence[bytes], fmt: str = "deflate-raw", level: int = -1) -> List[bytes]:
+        res = []
+        for st, b in self.compress_batch_raw(inputs, fmt, level):
+            if st != Z_STREAM_END:
+                raise ZsError(stream_error_text(st, PHASE_FINISH), st, PHASE_FINISH)
+            res.append(b)
+        return res
+
+    def decompress_batch_raw(self, inputs: Sequence[bytes], fmt: str = "deflate-raw",
+                             out_caps: Optional[Sequence[int]] = None):
+        """Returns [(status, phase, msg, bytes, consumed)]."""
+        L = self._L
+        if not hasattr(L, "zs_inflate_batch"):
+            raise ZsUnavailable("this libzsgpu.so has no inflate engine")
+        n = len(inputs)
+        if n == 0:
+            return []
+        wbits = decompress_wbits(fmt)
+        blob = b"".join(inputs)
+        offs, lens, o = [], [], 0
+        for b in inputs:
+            offs.append(o)
+            lens.append(len(b))
+            o += len(b)
+        if out_caps is None:
+            out_caps = [max(1 << 16, 16 * len(b)) for b in inputs]
+        caps = [(int(c) + 3) & ~3 for c in out_caps]
+        ooffs, oo = [], 0
+        for c in caps:
+            ooffs.append(oo)
+            oo += c
+        out = ctypes.create_string_buffer(max(1, oo))
+        status, phase, msg = (ctypes.c_int32 * n)(), (ctypes.c_int32 * n)(), (ctypes.c_int32 * n)()
+        olen, cons = (ctypes.c_uint32 * n)(), (ctypes.c_uint32 * n)()
+        r = L.zs_inflate_batch(self._ctx, wbits, n, blob, _arr(ctypes.c_uint64, offs), _arr(ctypes.c_uint32, lens),
+                               out, _arr(ctypes.c_uint64, ooffs), _arr(ctypes.c_uint32, caps), status, phase, msg,
+                               olen, cons)
+        self._check(r, "zs_inflate_batch")
+        raw = out.raw
+        return [(status[i], phase[i], L.zs_inflate_message(msg[i]).decode(), raw[ooffs[i]: ooffs[i] + olen[i]],
+                 cons[i]) for i in range(n)]
+
+    def decompress_batch(self, inputs: Sequence[bytes], fmt: str = "deflate-raw",
+                         out_caps: Optional[Sequence[int]] = None) -> List[bytes]:
+        res = []
+        for st, ph, msg, b, _ in self.decompress_batch_raw(inputs, fmt, out_caps):
+            if st != Z_STREAM_END:
+                raise ZsError(stream_error_text(st, ph), st, ph, msg)
+            res.append(b)
+        return res
+
+    # ---------------------------------------------------- device-resident
+    def compress_device(self, level: int, fmt: str, n: int, d_in: int, in_off, in_len, d_out: int, out_off, out_cap,
+                        d_status: int, d_out_len: int, hip_stream: int = 0):
+        """Device pointers (ints) + host layout arrays (ctypes arrays)."""
+        r = self._L.zs_deflate_batch_device(self._ctx, level, compress_wbits(fmt), n, _P(d_in), in_off, in_len,
+                                            _P(d_out), out_off, out_cap, _P(d_status), _P(d_out_len),
+                                            _P(hip_stream) if hip_stream else None)
+        self._check(r, "zs_deflate_batch_device")
+
+    def decompress_device(self, fmt: str, n: int, d_in: int, in_off, in_len, d_out: int, out_off, out_cap,
+                          d_status: int, d_phase: int, d_msg: int, d_out_len: int, d_consumed: int,
+                          hip_stream: int = 0):
+        r = self._L.zs_inflate_batch_device(self._ctx, decompress_wbits(fmt), n, _P(d_in), in_off, in_len, _P(d_out),
+                                            out_off, out_cap, _P(d_status), _P(d_phase), _P(d_msg), _P(d_out_len),
+                                            _P(d_consumed), _P(hip_stream) if hip_stream else None)
+        self._check(r, "zs_inflate_batch_device")
+
+    def checksum_device(self, kind: str, n: int, d_in: int, in_off, in_len, d_check: int, hip_stream: int = 0):
+        fn = self._L.zs_crc32_batch_device if kind == "crc32" else self._L.zs_adler32_batch_device
+        r = fn(self._ctx, n, _P(d_in), in_off, in_len, _P(d_check), _P(hip_stream) if hip_stream else None)
+        self._check(r, "checksum")
+
+
+_default: Optional[Engine] = None
+
+
+def default_engine() -> Engine:
+    global _default
+    if _default is None:
+        _default = Engine(0)
+    return _default
+
+
+def compress_batch(inputs: Sequence[bytes], fmt: str = "deflate-raw", level: int = -1) -> List[bytes]:
+    return default_engine().compress_batch(inputs, fmt, level)
+
+
+def decompress_batch(inputs: Sequence[bytes], fmt: str = "deflate-raw") -> List[bytes]:
+    return default_engine().decompress_batch(inputs, fmt)
+
+
+class _OneShotStream:
+    """write()/close()/read() over a single-stream GPU batch (streams.ts semantics:
+    the whole input is collected, then processed as ONE write() + close())."""
+
+    def __init__(self):
+        self._chunks: List[bytes] = []
+        self._out: Optional[bytes] = None
+
+    def write(self, chunk: bytes):
+        if self._out is not None:
+            raise ZsError("stream closed")
+        self._chunks.append(bytes(chunk))
+
+    def read(self) -> bytes:
+        if self._out is None:
+            raise ZsError("stream not closed")
+        return self._out
+
+
+class CompressionStream(_OneShotStream):
+    """streams.ts:242-251 (format 'deflate' | 'gzip' | 'deflate-raw', {level})."""
+
+    def __init__(self, fmt: str = "deflate", level: Optional[int] = None):
+        super().__init__()
+        self.format, self.level = fmt, (-1 if level is None else level)
+
+    def close(self) -> bytes:
+        self._out = default_engine().compress_batch([b"".join(self._chunks)], self.format, self.level)[0]
+        return self._out
+
+
+class DecompressionStream(_OneShotStream):
+    """streams.ts:253-262 (format 'deflate' | 'gzip' | 'deflate-raw' | 'deflate64-raw')."""
+
+    def __init__(self, fmt: str = "deflate"):
+        super().__init__()
+        self.format = fmt
+
+    def close(self) -> bytes:
+        self._out = default_engine().decompress_batch([b"".join(self._chunks)], self.format)[0]
+        return self._out
+
+
+def corpus(kind: str, first_index: int, n_streams: int, length: int, threads: int = 8) -> bytearray:
+    """Synthetic T ('text') / M ('mixed') / 'rand' corpora."""
+    k = {"text": 0, "mixed": 1, "rand": 2}[kind]
+    buf = bytearray(n_streams * length)
+    cbuf = (ctypes.c_char * len(buf)).from_buffer(buf)
+    lib().zs_corpus(k, first_index, n_streams, length, ctypes.cast(cbuf, _P), threads)
+    return buf
