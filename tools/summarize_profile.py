@@ -1,0 +1,36 @@
+"""Summarize a tools/profile.sh directory into profiles/<round>/summary.json:
+per kernel: calls, average duration (kernel trace), FETCH_SIZE / WRITE_SIZE
+(KiB per dispatch as rocprofv3 reports them) and the HBM bytes per launch.
+gfx950 FETCH_SIZE counts half of the bytes of wide coalesced reads
+(MI355X_MICROARCH.md, HBM): hbm_bytes_corrected doubles the read side."""
+import collections, csv, json, os, sys
+
+src, dst = sys.argv[1], sys.argv[2]
+stats = {}
+for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
+    stats[r["Name"].split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                       "total_ns": float(r["TotalDurationNs"])}
+cnt = collections.defaultdict(lambda: collections.defaultdict(list))
+for kind in ("fetch", "write"):
+    p = os.path.join(src, kind, "run_counter_collection.csv")
+    if not os.path.exists(p):
+        continue
+    for r in csv.DictReader(open(p)):
+        cnt[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+out = {}
+for k, v in stats.items():
+    e = dict(v)
+    f, w = cnt[k].get("FETCH_SIZE"), cnt[k].get("WRITE_SIZE")
+    if f:
+        e["fetch_kib"] = sum(f) / len(f)
+    if w:
+        e["write_kib"] = sum(w) / len(w)
+    if f and w:
+        e["hbm_bytes_raw"] = (e["fetch_kib"] + e["write_kib"]) * 1024
+        e["hbm_bytes_corrected"] = (2 * e["fetch_kib"] + e["write_kib"]) * 1024
+    out[k] = e
+os.makedirs(os.path.dirname(dst), exist_ok=True)
+json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
+for k, e in sorted(out.items(), key=lambda kv: -kv[1]["total_ns"]):
+    print("%-32s calls %3d avg %10.3f ms  hbm(raw) %s" % (k[:32], e["calls"], e["avg_ns"] / 1e6,
+                                                        "%.1f MB" % (e["hbm_bytes_raw"] / 1e6) if "hbm_bytes_raw" in e else "-"))
