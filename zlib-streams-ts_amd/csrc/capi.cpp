@@ -16,6 +16,7 @@
 #include "../../include/zs_gpu.h"
 #include "zs_common.h"
 #include "zs_kernels.h"
+#include "zs_inflate.h"
 
 
 namespace {
@@ -463,4 +464,113 @@ extern "C" uint64_t zs_debug_fetch(zs_ctx* c, int what, uint32_t s, void* dst, u
   bytes = std::min(bytes, cap);
   if (bytes && hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   return bytes;
+}
+
+// ------------------------------------------------------------------ inflate
+static const char* kInflateMsgs[ZS_MSG_COUNT] = {
+    "",
+    "incorrect header check",
+    "unknown compression method",
+    "invalid window size",
+    "unknown header flags set",
+    "header crc mismatch",
+    "invalid block type",
+    "invalid stored block lengths",
+    "too many length or distance symbols",
+    "too many length",
+    "invalid code lengths set",
+    "invalid bit length repeat",
+    "invalid code -- missing end-of-block",
+    "invalid literal/lengths set",
+    "invalid distances set",
+    "invalid literal/length code",
+    "invalid distance code",
+    "invalid distance too far back",
+    "incorrect data check",
+    "incorrect length check",
+    "output capacity exceeded",
+};
+
+extern "C" const char* zs_inflate_message(int32_t i) { return (i >= 0 && i < ZS_MSG_COUNT) ? kInflateMsgs[i] : ""; }
+
+__global__ void zs_k_inflate_finish(const zs_inflate_result* r, int32_t* status, int32_t* phase, int32_t* msg,
+                                    uint32_t* out_len, uint32_t* consumed, int n) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  status[s] = r[s].status;
+  phase[s] = r[s].phase;
+  msg[s] = r[s].msg;
+  out_len[s] = r[s].out_len;
+  consumed[s] = r[s].consumed;
+}
+
+extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                                       const uint32_t* in_len, uint8_t* d_out, const uint64_t* out_off,
+                                       const uint32_t* out_cap, int32_t* d_status, int32_t* d_phase, int32_t* d_msg,
+                                       uint32_t* d_out_len, uint32_t* d_consumed, void* hip_stream) {
+  if (!c) return fail(ZS_STREAM_ERROR, "null context");
+  // inflateInit2_ / inflateReset2 validation (inflate.ts:138-192) for the stream-layer formats
+  if (!(wbits == -15 || wbits == 15 || wbits == 31 || wbits == -16))
+    return fail(ZS_STREAM_ERROR, "unsupported windowBits (use -15, 15, 31 or -16)");
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  HIPCHK(hipSetDevice(c->device));
+  if (n == 0) return ZS_OK;
+  MetaLayout ml(n);
+  c->hmeta.resize(ml.bytes);
+  c->last_n = n;
+  uint8_t* hm = c->hmeta.data();
+  memcpy(hm + ml.in_off, in_off, 8ull * n);
+  memcpy(hm + ml.in_len, in_len, 4ull * n);
+  memcpy(hm + ml.out_off, out_off, 8ull * n);
+  memcpy(hm + ml.out_cap, out_cap, 4ull * n);
+  HIPCHK(c->meta.ensure(ml.bytes));
+  HIPCHK(c->istate.ensure(sizeof(zs_inflate_result) * (size_t)n));
+  HIPCHK(hipMemcpyAsync(c->meta.p, hm, ml.bytes, hipMemcpyHostToDevice, st));
+  uint8_t* dm = c->meta.as<uint8_t>();
+  const size_t smem = zs_inflate_smem_bytes(wbits);
+  HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  mark(c, st, "start");
+  zs_k_inflate<<<n, 64, smem, st>>>(d_in, (const uint64_t*)(dm + ml.in_off), (const uint32_t*)(dm + ml.in_len), d_out,
+                                    (const uint64_t*)(dm + ml.out_off), (const uint32_t*)(dm + ml.out_cap), wbits,
+                                    c->istate.as<zs_inflate_result>());
+  mark(c, st, "inflate");
+  zs_k_inflate_finish<<<(n + 255) / 256, 256, 0, st>>>(c->istate.as<zs_inflate_result>(), d_status, d_phase, d_msg,
+                                                       d_out_len, d_consumed, (int)n);
+  mark(c, st, "finish");
+  HIPCHK(hipGetLastError());
+  collect_marks(c);
+  return ZS_OK;
+}
+
+extern "C" int zs_inflate_batch(zs_ctx* c, int wbits, uint32_t n, const uint8_t* in, const uint64_t* in_off,
+                                const uint32_t* in_len, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                                int32_t* status, int32_t* phase, int32_t* msg, uint32_t* out_len, uint32_t* consumed) {
+  if (!c) return fail(ZS_STREAM_ERROR, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  std::vector<uint64_t> doff, ooff(n);
+  uint64_t total = 0, ototal = 0;
+  int r = stage_in(c, n, in, in_off, in_len, doff, total);
+  if (r != ZS_OK) return r;
+  for (uint32_t i = 0; i < n; i++) { ooff[i] = ototal; ototal += out_cap[i]; }
+  HIPCHK(c->d_out.ensure(ototal + 16));
+  HIPCHK(c->d_res.ensure(20ull * n + 16));
+  int32_t* d_status = c->d_res.as<int32_t>();
+  int32_t* d_phase = d_status + n;
+  int32_t* d_msg = d_phase + n;
+  uint32_t* d_len = (uint32_t*)(d_msg + n);
+  uint32_t* d_cons = d_len + n;
+  r = zs_inflate_batch_device(c, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len, c->d_out.as<uint8_t>(),
+                              ooff.data(), out_cap, d_status, d_phase, d_msg, d_len, d_cons, c->stream);
+  if (r != ZS_OK) return r;
+  HIPCHK(hipMemcpyAsync(status, d_status, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(phase, d_phase, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(msg, d_msg, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(out_len, d_len, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(consumed, d_cons, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < n; i++)
+    if (out_len[i])
+      HIPCHK(hipMemcpyAsync(out + out_off[i], c->d_out.as<uint8_t>() + ooff[i], out_len[i], hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return ZS_OK;
 }
