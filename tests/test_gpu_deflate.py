@@ -10,7 +10,7 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 
-GPU_LEVELS = [4, 5, 6, 7, 8, 9]
+GPU_LEVELS = [1, 2, 3, 4, 5, 6, 7, 8, 9]
 
 
 def test_small_goldens(engine):
@@ -56,7 +56,7 @@ def test_block_boundaries_and_stored_blocks(engine):
     inputs = [corpus.rand(corpus.stream_seed(1), 16383), corpus.rand(corpus.stream_seed(2), 16384),
               corpus.rand(corpus.stream_seed(3), 50000), bytes(200000), corpus.text(corpus.stream_seed(4), 262144),
               corpus.rand(corpus.stream_seed(5), 16383 * 2), corpus.rand(corpus.stream_seed(6), 16383 * 2 + 1)]
-    for level in (4, 6, 9):
+    for level in (1, 3, 4, 6, 9):
         res = engine.compress_batch_raw(inputs, "deflate-raw", level)
         for d, (st, out) in zip(inputs, res):
             assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1], (len(d), level)
@@ -110,3 +110,18 @@ def test_c5_gzip_batch_matches_reference_goldens(engine):
         bad = [lo + i for i, (st, out) in enumerate(res)
                if st != 1 or (len(out), hashlib.sha256(out).digest()[:16]) != recs[lo + i]]
         assert not bad, bad[:10]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name,level", [("t256_l1_raw", 1), ("t256_l9_raw", 9)])
+def test_c4_256k_streams_match_reference_goldens(engine, name, level):
+    """BASELINE.json configs[3]: 256 KiB T-corpus streams at L1 (deflate_fast) and L9 (slides, chain 4096)."""
+    import zsamd
+
+    recs = golden_io.batch(name)
+    n = 512
+    buf = bytes(zsamd.corpus("text", 0, n, 262144))
+    inputs = [buf[i * 262144:(i + 1) * 262144] for i in range(n)]
+    res = engine.compress_batch_raw(inputs, "deflate-raw", level)
+    bad = [i for i, (st, out) in enumerate(res) if st != 1 or (len(out), hashlib.sha256(out).digest()[:16]) != recs[i]]
+    assert not bad, bad[:10]

@@ -1,10 +1,176 @@
-// deflate_fast.hip -- placeholder for the greedy levels 1..3 (deflate_fast,
-// deflate.ts:1281-1350); see DESIGN.md.  Marks every stream unsupported.
+// deflate_fast.hip -- the greedy parser of levels 1..3 (deflate_fast,
+// deflate.ts:1281-1350) on gfx950.
+//
+// Unlike levels 4..9, deflate_fast does not insert the positions inside a
+// match longer than max_lazy (deflate.ts:1310-1322), so its hash chains depend
+// on the parse and cannot be precomputed per position.  One
+// workgroup (one wave) per stream therefore replays the reference serially,
+// with the exact window-relative head[] / prev[] tables of the reference
+// (u16, 32 K entries each, slid by 32 K on the same schedule as fill_window,
+// deflate.ts:180-190) resident in LDS.  All 64 lanes run the state machine in
+// lock-step and cooperate on the byte work: a candidate is compared 64 bytes
+// per step (one coalesced load + ballot), the input bytes the hash needs are
+// prefetched 256 at a time into registers and read back with readlane.
 #include <hip/hip_runtime.h>
 #include "zs_common.h"
 #include "zs_kernels.h"
 
-__global__ void zs_k_fast(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*, uint32_t*,
-                          zs_block*, zs_stream* streams, int, int, int) {
-  if (threadIdx.x == 0) { streams[blockIdx.x].nsym = 0; streams[blockIdx.x].nblk = 0; }
+struct zs_fast_lds {
+  uint16_t head[32768];
+  uint16_t prev[32768];
+};
+
+// Prefetched input window: lane l holds bytes [pf0 + 4l, pf0 + 4l + 4).
+struct zs_pf {
+  uint32_t pf0;
+  uint32_t w;
+};
+
+static __device__ __forceinline__ uint32_t zs_load_word(const uint8_t* src, uint32_t n, uint32_t at) {
+  uint32_t v = 0;
+  if (at + 4 <= n && ((uintptr_t)(src + at) & 3u) == 0) return *(const uint32_t*)(src + at);
+  for (uint32_t k = 0; k < 4; k++)
+    if (at + k < n) v |= (uint32_t)src[at + k] << (8 * k);
+  return v;
+}
+
+// byte q of the input through the register window (q in [pf0, pf0 + 252))
+static __device__ __forceinline__ uint32_t zs_pf_byte(const zs_pf& pf, uint32_t q) {
+  const uint32_t o = q - pf.pf0;
+  const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)pf.w, (int)(o >> 2));
+  return (word >> (8 * (o & 3))) & 0xffu;
+}
+
+__global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                const uint32_t* __restrict__ in_len,
+                                                const uint64_t* __restrict__ pos_base,
+                                                const uint32_t* __restrict__ blk_base, uint32_t* __restrict__ syms,
+                                                zs_block* __restrict__ blocks, zs_stream* __restrict__ streams,
+                                                int chain, int lazy, int nice_cfg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t zs_fast_smem[];
+  zs_fast_lds& L = *reinterpret_cast<zs_fast_lds*>(zs_fast_smem);
+  const int s = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = in_len[s];
+  const uint8_t* src = in + in_off[s];
+  uint32_t* sy = syms + pos_base[s] + s;
+  zs_block* blk = blocks + blk_base[s];
+  for (uint32_t i = lane; i < 32768; i += 64) { L.head[i] = 0; L.prev[i] = 0; }  // CLEAR_HASH (deflate.ts:120-123)
+  __syncthreads();
+
+  zs_pf pf;
+  pf.pf0 = 0;
+  pf.w = zs_load_word(src, n, 4 * lane);
+  auto refill = [&](uint32_t q) {  // make [q, q + 8) readable
+    if (q - pf.pf0 + 8 > 252) {
+      pf.pf0 = q;
+      pf.w = zs_load_word(src, n, q + 4 * lane);
+    }
+  };
+  auto hash_at = [&](uint32_t q) -> uint32_t {  // SURVEY A1; caller guarantees q + 2 < n
+    refill(q);
+    return ((zs_pf_byte(pf, q) << 10) ^ (zs_pf_byte(pf, q + 1) << 5) ^ zs_pf_byte(pf, q + 2)) & ZS_HASH_MASK;
+  };
+
+  uint32_t base = 0;  // absolute position of window index 0
+  uint32_t nsym = 0, in_blk = 0, nflush = 0, blk_start = 0;
+  uint32_t ml = 0, ms_rel = 0;  // match_length / match_start (window-relative)
+  uint32_t p = 0;
+  auto insert = [&](uint32_t q) -> uint32_t {  // INSERT_STRING (deflate.ts:113-118), window-relative
+    const uint32_t h = hash_at(q);
+    const uint32_t rel = q - base;
+    const uint32_t hh = L.head[h];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    if (lane == 0) { L.prev[rel & 0x7fffu] = (uint16_t)hh; L.head[h] = (uint16_t)rel; }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    return hh;
+  };
+  auto emit = [&](uint32_t v) {
+    if (lane == 0) sy[nsym] = v;
+    nsym++;
+    in_blk++;
+  };
+  auto close_block = [&](uint32_t end, uint32_t last) {
+    if (lane == 0) {
+      zs_block b;
+      b.sym_start = nsym - in_blk;
+      b.sym_count = in_blk;
+      b.in_start = blk_start;
+      b.in_end = end;
+      b.type = 0; b.hdr_bits = 0; b.data_bits = 0; b.pad = 0; b.bit_off = 0; b.bit_end = 0;
+      b.last = last | (blk_start < base ? 2u : 0u);
+      blk[nflush] = b;
+    }
+    nflush++;
+    in_blk = 0;
+    blk_start = end;
+  };
+
+  while (p < n) {
+    // fill_window slide (deflate.ts:180-190): same schedule as deflate_slow
+    if (p - base >= ZS_SLIDE_AT && min(n, base + 65536u) - p < ZS_MIN_LOOKAHEAD) {
+      for (uint32_t i = lane; i < 32768; i += 64) {
+        const uint32_t a = L.head[i], b = L.prev[i];
+        L.head[i] = (uint16_t)(a >= 32768u ? a - 32768u : 0u);
+        L.prev[i] = (uint16_t)(b >= 32768u ? b - 32768u : 0u);
+      }
+      __syncthreads();
+      base += 32768u;
+      ms_rel -= 32768u;
+    }
+    const uint32_t look = n - p;
+    uint32_t hash_head = 0;
+    if (look >= ZS_MIN_MATCH) hash_head = insert(p);
+    const uint32_t srel = p - base;
+    if (hash_head != 0 && srel - hash_head <= ZS_MAX_DIST) {
+      // longest_match with prev_length = MIN_MATCH - 1 (deflate_fast never sets it), deflate.ts:1053-1115
+      uint32_t chain_length = (uint32_t)chain;
+      const uint32_t maxc = look < ZS_MAX_MATCH ? look : ZS_MAX_MATCH;
+      const uint32_t nice = look < (uint32_t)nice_cfg ? look : (uint32_t)nice_cfg;
+      const uint32_t limit = srel > ZS_MAX_DIST ? srel - ZS_MAX_DIST : 0;
+      uint32_t best = ZS_MIN_MATCH - 1, cur = hash_head;
+      const uint32_t sb = p + lane < n ? src[p + lane] : 0x100u;  // scan bytes 0..63
+      do {
+        const uint32_t mpos = base + cur;
+        uint32_t k = 0;
+        // compare 64 bytes per step
+        uint32_t mb = mpos + lane < n ? src[mpos + lane] : 0x1ffu;
+        uint64_t neq = __ballot(mb != sb || lane >= maxc);
+        while (neq == 0 && k + 64 < maxc) {
+          k += 64;
+          const uint32_t sbk = p + k + lane < n ? src[p + k + lane] : 0x100u;
+          mb = mpos + k + lane < n ? src[mpos + k + lane] : 0x1ffu;
+          neq = __ballot(mb != sbk || k + lane >= maxc);
+        }
+        k += neq ? (uint32_t)__builtin_ctzll(neq) : 64u;
+        const uint32_t len = k < maxc ? k : maxc;
+        if (len > best) {
+          ms_rel = cur;
+          best = len;
+          if (len >= nice) break;
+        }
+        cur = L.prev[cur & 0x7fffu];
+      } while (cur > limit && --chain_length != 0);
+      ml = best <= look ? best : look;
+    }
+    if (ml >= ZS_MIN_MATCH) {
+      emit(0x80000000u | ((ml - ZS_MIN_MATCH) << 16) | (srel - ms_rel));
+      const uint32_t after = p + ml;
+      if (ml <= (uint32_t)lazy && n - after >= ZS_MIN_MATCH) {
+        for (uint32_t q = p + 1; q < after; q++) insert(q);  // insert inside short matches
+      }
+      p = after;
+      ml = 0;
+    } else {
+      emit(p < n ? (refill(p), zs_pf_byte(pf, p)) : 0u);
+      p++;
+    }
+    if (in_blk == ZS_SYM_END) close_block(p, 0);
+  }
+  close_block(n, 1);
+  if (lane == 0) {
+    streams[s].nsym = nsym;
+    streams[s].nblk = nflush;
+  }
 }
