@@ -11,11 +11,8 @@
 //
 //   zs_k_prev  : prevd[p] = distance to the previous position with the same
 //                hash (0 = none / farther than 32767), i.e. the reference's
-//                prev[] chain in absolute coordinates.  One workgroup per
-//                stream; its four waves split the hash space (h & 3) so they
-//                never touch each other's head-table entries and need no
-//                barriers.  The head table lives in LDS as u16 with a sliding
-//                base, exactly like the reference's window-relative head[].
+//                prev[] chain in absolute coordinates.  One wave per stream,
+//                one lane-ordered LDS exchange per position.
 //
 //   zs_k_match : per position, the (length, distance) longest_match returns
 //                for the full chain budget and for the budget >> 2 used when
@@ -28,68 +25,69 @@
 #include "zs_kernels.h"
 
 // ---------------------------------------------------------------- zs_k_prev
-// 256 threads = 4 waves; wave w owns hash values h with (h & 3) == w.
-__global__ __launch_bounds__(256) void zs_k_prev(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                 const uint32_t* __restrict__ in_len,
-                                                 const uint64_t* __restrict__ pos_base, uint16_t* __restrict__ prevd) {
-  __shared__ uint16_t head[32768];  // entry = q - base + 1, 0 = none
+// One wave per stream walks the positions in order, 64 at a time.  Lane l of
+// a 64-position group swaps its position into head[h] with ONE ds_wrxchg_rtn:
+// gfx950 applies same-address LDS atomics of one wave instruction in increasing
+// lane order (probed: tools/probes/lds_atomic_order.hip, re-checked at run time
+// by zs_selftest), so the value each lane gets back is exactly the previous
+// position with the same hash -- the reference's prev[] link.  head[] holds
+// q + 1 (absolute, 32-bit), so no slide (deflate.ts:125-141) is needed.
+#define ZS_PREV_STAGE 4096u
+__global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                const uint32_t* __restrict__ in_len,
+                                                const uint64_t* __restrict__ pos_base, uint16_t* __restrict__ prevd) {
+  __shared__ uint32_t head[32768];
+  __shared__ uint32_t stg[ZS_PREV_STAGE / 4 + 2];  // input bytes [c0, c0 + 4096 + 8)
   const int s = blockIdx.x;
   const uint32_t n = in_len[s];
   const uint8_t* src = in + in_off[s];
   uint16_t* out = prevd + pos_base[s];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t w = threadIdx.x >> 6;
-  for (uint32_t i = lane; i < 8192; i += 64) head[4 * i + w] = 0;
-  uint32_t base = 0;
-  const uint64_t lt_mask = (1ull << lane) - 1;
-  const uint64_t gt_mask = lane == 63 ? 0ull : ~((2ull << lane) - 1);
-  // software-pipelined byte loads: the 3 bytes each lane hashes
-  uint32_t p = lane;
-  uint32_t b0 = p < n ? src[p] : 0, b1 = p + 1 < n ? src[p + 1] : 0, b2 = p + 2 < n ? src[p + 2] : 0;
-  for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-    p = c0 + lane;
-    const uint32_t pn = p + 64;
-    const uint32_t nb0 = pn < n ? src[pn] : 0, nb1 = pn + 1 < n ? src[pn + 1] : 0, nb2 = pn + 2 < n ? src[pn + 2] : 0;
-    // slide the head table so that entries stay in 1..65535 (zlib's slide_hash, deflate.ts:125-141)
-    if (c0 + 63 - base + 1 > 65535u) {
-      base += 32768;
-      for (uint32_t i = lane; i < 8192; i += 64) {
-        uint32_t e = head[4 * i + w];
-        head[4 * i + w] = (uint16_t)(e > 32768u ? e - 32768u : 0u);
-      }
-    }
-    const bool valid = p + 2 < n;  // positions <= n-3 are inserted (deflate.ts:1367-1370, 1397-1401)
-    const uint32_t h = ((b0 << 10) ^ (b1 << 5) ^ b2) & ZS_HASH_MASK;  // rolling UPDATE_HASH, SURVEY A1
-    const bool mine = valid && (h & 3u) == w;
-    uint64_t active = __ballot(mine);
-    int pred = -1;
-    bool is_last = false;
-    while (active) {
-      const int l = __builtin_ctzll(active);
-      const uint32_t hl = __builtin_amdgcn_readlane(h, l);
-      const uint64_t m = __ballot(mine && h == hl);
-      if (mine && h == hl) {
-        const uint64_t below = m & lt_mask;
-        pred = below ? 63 - __builtin_clzll(below) : -1;
-        is_last = (m & gt_mask) == 0;
-      }
-      active &= ~m;
-    }
-    if (mine) {
-      uint32_t d;
-      if (pred >= 0) {
-        d = lane - (uint32_t)pred;
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t i = lane; i < 32768; i += 64) head[i] = 0;
+  const bool aligned = ((uintptr_t)src & 3u) == 0;
+  for (uint32_t c0 = 0; c0 < n; c0 += ZS_PREV_STAGE) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < ZS_PREV_STAGE / 4 + 2; i += 64) {
+      const uint32_t at = c0 + 4 * i;
+      uint32_t v = 0;
+      if (aligned && at + 4 <= n) {
+        v = *(const uint32_t*)(src + at);
       } else {
-        const uint32_t e = head[h];
-        d = e ? p - (base + e - 1) : 0;
+        for (uint32_t k = 0; k < 4; k++)
+          if (at + k < n) v |= (uint32_t)src[at + k] << (8 * k);
       }
-      out[p] = (uint16_t)(d <= 32767u ? d : 0u);
-    } else if (!valid && w == 0 && p < n) {
-      out[p] = 0;
+      stg[i] = v;
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // reads of head[] complete before the updates below
-    if (mine && is_last) head[h] = (uint16_t)(p - base + 1);
-    b0 = nb0; b1 = nb1; b2 = nb2;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t c1 = min(n, c0 + ZS_PREV_STAGE);
+    for (uint32_t g0 = c0; g0 < c1; g0 += 256) {
+      uint32_t h[4], e[4];
+      bool valid[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t p = g0 + 64 * j + lane;
+        const uint32_t o = p - c0;
+        const uint32_t w = __builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u);
+        valid[j] = p + 2 < n && p < c1;  // positions <= n-3 are inserted (deflate.ts:1367-1370)
+        h[j] = (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
+      }
+      // in order: group j's exchanges land after group j-1's (LDS executes a wave's ops in order)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t p = g0 + 64 * j + lane;
+        e[j] = valid[j] ? atomicExch(&head[h[j]], p + 1) : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t p = g0 + 64 * j + lane;
+        if (p < c1) {
+          const uint32_t d = e[j] ? p - (e[j] - 1) : 0u;
+          out[p] = (uint16_t)(valid[j] && d <= 32767u ? d : 0u);
+        }
+      }
+    }
   }
 }
 
@@ -168,34 +166,33 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       uint32_t cur = q0;
       for (;;) {
         const uint32_t cp = cur - w0;
-        // longest common prefix of window[p..] and window[cur..], capped at maxc
-        uint32_t x = win_word(wb, cp) ^ s0, k = 0;
-        if (x == 0) {
-          k = 4;
-          x = win_word(wb, cp + 4) ^ s1;
-          if (x == 0) {
-            k = 8;
-            while (k < maxc) {
-              x = win_word(wb, cp + k) ^ win_word(wb, sp + k);
-              if (x) break;
-              k += 4;
-            }
+        // first 8 bytes from three aligned LDS words; longer matches fall to the loop
+        const uint32_t wi = cp >> 2, sh = cp & 3u;
+        const uint32_t a0 = wb[wi], a1 = wb[wi + 1], a2 = wb[wi + 2];
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, sh) ^ s0;
+        const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, sh) ^ s1;
+        uint32_t k = x0 ? (uint32_t)(__builtin_ctz(x0) >> 3) : x1 ? 4u + (uint32_t)(__builtin_ctz(x1) >> 3) : 8u;
+        if (k == 8u) {
+          while (k < maxc) {
+            const uint32_t x = win_word(wb, cp + k) ^ win_word(wb, sp + k);
+            if (x) { k += (uint32_t)(__builtin_ctz(x) >> 3); break; }
+            k += 4;
           }
         }
-        if (x) k += __builtin_ctz(x) >> 3;
         const uint32_t len = k < maxc ? k : maxc;
-        if (len > best) {  // first strictly longer match wins (deflate.ts:1100-1105)
-          best = len;
-          bq = cur;
-          if (len >= nice) break;
-        }
-        cnt++;
-        if (cnt == budget_small) { best_s = best; bq_s = bq; small_set = true; }
-        if (cnt >= budget) break;
+        const bool improve = len > best;  // the first strictly longer match wins (deflate.ts:1100-1105)
+        best = improve ? len : best;
+        bq = improve ? cur : bq;
+        const bool nice_stop = improve && len >= nice;
+        cnt += nice_stop ? 0u : 1u;
+        const bool snap = !small_set && cnt == budget_small;
+        best_s = snap ? best : best_s;
+        bq_s = snap ? bq : bq_s;
+        small_set = small_set || snap;
         const uint32_t d = pv[cp];
-        if (d == 0) break;
         const uint32_t nxt = cur - d;
-        if (nxt <= limit) break;  // chain candidates need cur > limit (deflate.ts:1109)
+        // chain ends: nice match, budget spent, no link, or cur <= limit (deflate.ts:1109)
+        if (nice_stop || cnt >= budget || d == 0 || nxt <= limit) break;
         cur = nxt;
       }
       if (!small_set) { best_s = best; bq_s = bq; }
