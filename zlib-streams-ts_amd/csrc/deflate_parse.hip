@@ -1,131 +1,259 @@
 // deflate_parse.hip -- the lazy-match parse of deflate_slow (deflate.ts:1352-1448)
 // replayed over the per-position match table built by zs_k_match.
 //
-// One wave per stream.  The parse is a serial state machine,
-// so all 64 lanes run it in lock-step on identical values (no divergence,
-// LDS reads broadcast) and cooperate only to stage the next 2 K positions of
-// match results / input bytes into LDS and to drain the symbol buffer with
-// coalesced stores.  Blocks close every 16383 tallied symbols (deflate.ts:336,
-// deflate/utils.ts:68,80); a block's input range ends right after its last
-// symbol, as FLUSH_BLOCK_ONLY sets block_start = strstart (deflate.ts:1120-1124).
+// The parse is a serial state machine whose state is (position,
+// match_available, prev_length, prev_match).  Whenever prev_length is
+// MIN_MATCH - 1 -- after every emitted match (deflate.ts:1408-1409), after
+// every literal that found no match, and at position 0 -- prev_match is dead,
+// so two parses of the same match table that reach the same (position,
+// match_available) in that state produce identical symbols from there on.
+// One wave per stream therefore works on rounds of 64 segments of ZS_SEG
+// positions:
+//
+//   pass A  lane k parses segment k from the state at position 0 placed at the
+//           segment's first position ("speculative"), recording its symbols
+//           and the (position, match_available) pairs it passes with
+//           prev_length = 2 inside the segment (sync points);
+//   pass B  lane 0 replays the TRUE parse across each segment boundary only
+//           until it reaches a sync point of the next segment -- from there the
+//           speculative symbols are exact (2-3 steps per segment on text);
+//   pass C  the wave splices catch-up + speculative symbols into the stream's
+//           symbol array and closes a block after every 16383rd tallied symbol
+//           (deflate.ts:336; FLUSH_BLOCK sets block_start = strstart,
+//           deflate.ts:1120-1124) from a prefix sum of symbol lengths.
+//
+// fill_window's slide schedule (deflate.ts:180-190) enters the parse only
+// through the NIL head slot at exactly MAX_DIST: that happens iff
+// the slide falls on p itself, i.e. p = 32768 j + 65274 with the input ending
+// within the window (n - p < 262) -- a pure function of p, so no state is needed.
 #include <hip/hip_runtime.h>
 #include "zs_common.h"
 #include "zs_kernels.h"
 
-#define ZS_PARSE_MB 2048u  // staged positions
-#define ZS_PARSE_SB 1024u  // staged symbols
+#define ZS_SEG 1024u                        // positions per speculative segment
+#define ZS_SPEC_SLOTS 1284u                 // >= ZS_SEG + MAX_MATCH - 1 symbols
+#define ZS_SYNC_SLOTS 1028u                 // >= ZS_SEG sync points + sentinel
+#define ZS_FIX_SLOTS 1284u
+#define ZS_SEG_WORDS (ZS_SPEC_SLOTS + ZS_SYNC_SLOTS + ZS_FIX_SLOTS)
+#define ZS_NONE 0xffffffffu
+static_assert(ZS_SEG == ZS_PARSE_SEG && ZS_SEG_WORDS == ZS_PARSE_SEG_WORDS, "scratch layout shared with capi.cpp");
 
-// symbol encoding: literal = byte; match = 0x80000000 | (len-3) << 16 | dist
+struct zs_seg_info {
+  uint32_t end;         // first position >= the segment end visited by the speculative parse
+  uint32_t nspec;       // speculative symbols
+  uint32_t ma, ml, ms;  // speculative state at `end`
+  uint32_t start;       // position where the segment's final symbol run starts
+  uint32_t nfix;        // catch-up symbols (true parse) preceding the splice
+  uint32_t from;        // first speculative symbol kept (ZS_NONE: none)
+};
+
+struct zs_pstate {
+  uint32_t p, ma, ml, ms;
+};
+
+// One iteration of deflate_slow's loop at position p (deflate.ts:1356-1426),
+// given the match-table entry e of p and the byte in[p-1].  Returns the symbol
+// tallied (ZS_NONE: none).  Symbols: literal = byte, match = 0x80000000 |
+// (len - 3) << 16 | dist.
+static __device__ __forceinline__ uint32_t zs_parse_step(zs_pstate& st, uint2 e, uint32_t lit, uint32_t n, int good,
+                                                         int lazy) {
+  const uint32_t p = st.p, pl = st.ml, pm = st.ms;
+  uint32_t ml = ZS_MIN_MATCH - 1, ms = pm;
+  // head slot emptied by a slide at exactly this position
+  const bool nil =
+      (e.x & 0x8000u) && p >= ZS_SLIDE_AT && ((p - ZS_SLIDE_AT) & 32767u) == 0 && n - p < (uint32_t)ZS_MIN_LOOKAHEAD;
+  if ((e.x >> 16) != 0 && pl < (uint32_t)lazy && !nil) {
+    const uint32_t u = pl >= (uint32_t)good ? e.y : e.x;  // chain >> 2 when prev_length >= good (deflate.ts:1075-1077)
+    const uint32_t L = u >> 16, D = u & 0x7fffu;
+    if (L > pl) {
+      ml = L;
+      ms = p - D;
+      if (L == ZS_MIN_MATCH && D > ZS_TOO_FAR) ml = ZS_MIN_MATCH - 1;  // deflate.ts:1381-1387
+    }
+  }
+  if (pl >= ZS_MIN_MATCH && ml <= pl) {  // emit the previous match (deflate.ts:1389-1411)
+    st.p = p + pl - 1;
+    st.ma = 0;
+    st.ml = ZS_MIN_MATCH - 1;
+    st.ms = ms;
+    return 0x80000000u | ((pl - ZS_MIN_MATCH) << 16) | (p - 1 - pm);
+  }
+  st.ml = ml;
+  st.ms = ms;
+  st.p = p + 1;
+  if (st.ma) return lit;  // deferred literal (deflate.ts:1412-1421)
+  st.ma = 1;
+  return ZS_NONE;
+}
+
+// Number of fill_window slides performed by the time the parse visits v
+// (slide j happens at the first visited position >= T_j with
+// T_j = max(32768 j + 65274, min(n, 32768 j + 65536) - 261), deflate.ts:180-190).
+static __device__ __forceinline__ uint32_t zs_slides(uint32_t v, uint32_t n) {
+  if (n <= v + 261u) return v >= ZS_SLIDE_AT ? (v - ZS_SLIDE_AT) / 32768u + 1u : 0u;
+  return v >= ZS_SLIDE_AT + 1u ? (v - ZS_SLIDE_AT - 1u) / 32768u + 1u : 0u;
+}
+
 __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                  const uint32_t* __restrict__ in_len,
                                                  const uint64_t* __restrict__ pos_base,
                                                  const uint32_t* __restrict__ blk_base, const uint2* __restrict__ mres,
                                                  uint32_t* __restrict__ syms, zs_block* __restrict__ blocks,
-                                                 zs_stream* __restrict__ streams, int good, int lazy) {
-  __shared__ uint2 mb[ZS_PARSE_MB];
-  __shared__ uint8_t bb[ZS_PARSE_MB + 4];
-  __shared__ uint32_t sb[ZS_PARSE_SB];
+                                                 zs_stream* __restrict__ streams, uint32_t* __restrict__ scratch,
+                                                 int good, int lazy) {
+  __shared__ zs_seg_info seg[64];
+  __shared__ uint32_t sh_tail[1];  // true parse's match_available after the round
   const int s = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint32_t n = in_len[s];
   const uint8_t* src = in + in_off[s];
   const uint2* M = mres + pos_base[s];
   uint32_t* sy = syms + pos_base[s] + s;  // each stream owns n+1 symbol slots
+  uint32_t* scr = scratch + (size_t)ZS_SEG_WORDS * (pos_base[s] / ZS_SEG + s);
   zs_block* blk = blocks + blk_base[s];
+  const uint32_t nseg = (n + ZS_SEG - 1) / ZS_SEG;
 
-  uint32_t p = 0, ma = 0, ml = ZS_MIN_MATCH - 1, ms = 0, base = 0;
-  uint32_t nsym = 0, sbn = 0, in_blk = 0, nflush = 0, blk_start = 0;
-  uint32_t c0 = 0u - ZS_PARSE_MB;  // staged range [c0, c0 + MB); forces the first stage
+  zs_pstate t = {0, 0, ZS_MIN_MATCH - 1, 0};  // true parse state (lane 0)
+  uint32_t total = 0;  // symbols written (wave-uniform)
+  uint32_t last_start = 0;  // start position of the last symbol written (lane 63 of the last chunk)
 
-  auto stage = [&](uint32_t at) {
-    __syncthreads();
-    for (uint32_t i = lane; i < ZS_PARSE_MB; i += 64) {
-      const uint32_t q = at + i;
-      mb[i] = q < n ? M[q] : make_uint2(0, 0);
-      bb[i + 1] = q < n ? src[q] : 0;
+  for (uint32_t r0 = 0; r0 < nseg; r0 += 64) {
+    const uint32_t nr = min(64u, nseg - r0);
+    // ---- pass A: speculative parse of segment r0 + lane
+    if (lane < nr) {
+      const uint32_t k = r0 + lane;
+      const uint32_t a = k * ZS_SEG, b = min(n, a + ZS_SEG);
+      uint32_t* spec = scr + (size_t)lane * ZS_SEG_WORDS;
+      uint32_t* sync = spec + ZS_SPEC_SLOTS;
+      zs_pstate st = {a, 0, ZS_MIN_MATCH - 1, 0};
+      uint32_t cnt = 0, nsync = 0;
+      while (st.p < b) {
+        // sync key: (position - a) << 1 | match_available, with the symbol count
+        if (st.ml == ZS_MIN_MATCH - 1) sync[nsync++] = ((st.p - a) << 17) | (st.ma << 16) | cnt;
+        const uint32_t p = st.p;
+        const uint32_t v = zs_parse_step(st, M[p], p > 0 ? src[p - 1] : 0u, n, good, lazy);
+        if (v != ZS_NONE) spec[cnt++] = v;
+      }
+      sync[nsync] = ZS_NONE;
+      if (b == n && st.ma) spec[cnt++] = src[n - 1];  // final deferred literal (deflate.ts:1429-1432)
+      seg[lane].end = st.p;
+      seg[lane].nspec = cnt;
+      seg[lane].ma = st.ma;
+      seg[lane].ml = st.ml;
+      seg[lane].ms = st.ms;
     }
-    if (lane == 0) bb[0] = at > 0 ? src[at - 1] : 0;  // bb[i] = in[at - 1 + i]
     __syncthreads();
-  };
-  auto drain = [&]() {
-    __syncthreads();
-    const uint32_t o = nsym - sbn;
-    for (uint32_t i = lane; i < sbn; i += 64) sy[o + i] = sb[i];
-    sbn = 0;
-    __syncthreads();
-  };
-  auto emit = [&](uint32_t v) {
-    if (lane == 0) sb[sbn] = v;
-    sbn++;
-    nsym++;
-    in_blk++;
-    if (sbn == ZS_PARSE_SB) drain();
-  };
-  auto close_block = [&](uint32_t end) {  // FLUSH_BLOCK(s, 0)
+
+    // ---- pass B: the true parse across each boundary, until it meets a sync point
     if (lane == 0) {
-      zs_block b;
-      b.sym_start = nsym - in_blk;
-      b.sym_count = in_blk;
-      b.in_start = blk_start;
-      b.in_end = end;
-      b.type = 0; b.hdr_bits = 0; b.data_bits = 0; b.pad = 0; b.bit_off = 0; b.bit_end = 0;
-      b.last = blk_start < base ? 2u : 0u;
-      blk[nflush] = b;
+      for (uint32_t j = 0; j < nr; j++) {
+        const uint32_t a = (r0 + j) * ZS_SEG, b = min(n, a + ZS_SEG);
+        const uint32_t* spec = scr + (size_t)j * ZS_SEG_WORDS;
+        const uint32_t* sync = spec + ZS_SPEC_SLOTS;
+        uint32_t* fix = scr + (size_t)j * ZS_SEG_WORDS + ZS_SPEC_SLOTS + ZS_SYNC_SLOTS;
+        uint32_t nf = 0, from = ZS_NONE, si = 0, sv = sync[0];
+        seg[j].start = t.p - t.ma;  // a pending literal in[t.p - 1] opens the run
+        while (t.p < b) {
+          if (t.ml == ZS_MIN_MATCH - 1) {
+            const uint32_t key = ((t.p - a) << 1) | t.ma;
+            while ((sv >> 16) < key) sv = sync[++si];  // sentinel 0xffffffff stops the scan
+            if ((sv >> 16) == key) { from = sv & 0xffffu; break; }
+          }
+          const uint32_t p = t.p;
+          const uint32_t v = zs_parse_step(t, M[p], p > 0 ? src[p - 1] : 0u, n, good, lazy);
+          if (v != ZS_NONE) fix[nf++] = v;
+        }
+        if (from != ZS_NONE) {  // continue from the speculative end state
+          t.p = seg[j].end;
+          t.ma = seg[j].ma;
+          t.ml = seg[j].ml;
+          t.ms = seg[j].ms;
+        } else if (b == n && t.ma) {
+          fix[nf++] = src[n - 1];  // final deferred literal
+        }
+        seg[j].nfix = nf;
+        seg[j].from = from;
+      }
+      sh_tail[0] = t.ma;
     }
-    nflush++;
-    in_blk = 0;
-    blk_start = end;
-  };
+    __syncthreads();
+    const bool last_round = r0 + nr == nseg;
+    const bool final_lit = last_round && sh_tail[0] != 0;
+    uint32_t round_total = 0;
+    if (last_round) {
+      for (uint32_t j = 0; j < nr; j++)
+        round_total += seg[j].nfix + (seg[j].from == ZS_NONE ? 0u : seg[j].nspec - seg[j].from);
+    }
+    const uint32_t unchecked = final_lit ? total + round_total - 1 : ZS_NONE;  // global index of the final literal
 
-  while (p < n) {
-    if (p - c0 >= ZS_PARSE_MB) { stage(p); c0 = p; }
-    // fill_window's slide schedule (deflate.ts:180-190): only needed
-    // to know whether the head candidate at exactly MAX_DIST is the NIL slot.
-    bool slid = false;
-    if (p - base >= ZS_SLIDE_AT && min(n, base + 65536u) - p < ZS_MIN_LOOKAHEAD) { base += 32768u; slid = true; }
-    const uint32_t pl = ml, pm = ms;
-    ml = ZS_MIN_MATCH - 1;
-    const uint2 e = mb[p - c0];
-    if ((e.x >> 16) != 0 && pl < (uint32_t)lazy && !(slid && (e.x & 0x8000u))) {
-      const uint32_t u = pl >= (uint32_t)good ? e.y : e.x;  // chain >> 2 when prev_length >= good
-      const uint32_t L = u >> 16, D = u & 0x7fffu;
-      if (L > pl) {
-        ml = L;
-        ms = p - D;
-        if (L == ZS_MIN_MATCH && D > ZS_TOO_FAR) ml = ZS_MIN_MATCH - 1;  // deflate.ts:1381-1387
+    // ---- pass C: splice and cut blocks
+    for (uint32_t j = 0; j < nr; j++) {
+      const zs_seg_info si = seg[j];
+      uint32_t pos = si.start;
+      const uint32_t* base = scr + (size_t)j * ZS_SEG_WORDS;
+      for (int part = 0; part < 2; part++) {
+        const uint32_t* from = part == 0 ? base + ZS_SPEC_SLOTS + ZS_SYNC_SLOTS : base + si.from;
+        const uint32_t cnt = part == 0 ? si.nfix : (si.from == ZS_NONE ? 0u : si.nspec - si.from);
+        for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+          const uint32_t i = c0 + lane;
+          const uint32_t v = i < cnt ? from[i] : 0u;
+          const uint32_t len = i < cnt ? ((v & 0x80000000u) ? ((v >> 16) & 0xffu) + ZS_MIN_MATCH : 1u) : 0u;
+          uint32_t x = len;  // inclusive scan of symbol lengths
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= (uint32_t)d) x += y;
+          }
+          if (i < cnt) {
+            const uint32_t gi = total + lane;  // `total` already counts the previous chunks
+            sy[gi] = v;
+            if ((gi + 1) % ZS_SYM_END == 0 && gi != unchecked) {
+              // FLUSH_BLOCK after this symbol; remember the window base for the stored-block check
+              const uint32_t bi = (gi + 1) / ZS_SYM_END - 1;
+              const uint32_t st0 = pos + x - len;
+              blk[bi].in_end = pos + x;
+              blk[bi].pad = zs_slides(st0 + 1, n);
+            }
+          }
+          const uint32_t m = min(64u, cnt - c0);
+          last_start = __shfl(pos + x - len, (int)m - 1, 64);
+          pos += __shfl(x, 63, 64);
+          total += m;
+        }
       }
     }
-    if (pl >= ZS_MIN_MATCH && ml <= pl) {  // emit the previous match (deflate.ts:1389-1411)
-      emit(0x80000000u | ((pl - ZS_MIN_MATCH) << 16) | (p - 1 - pm));
-      p += pl - 1;
-      ma = 0;
-      ml = ZS_MIN_MATCH - 1;
-      if (in_blk == ZS_SYM_END) close_block(p);
-    } else if (ma) {  // deferred literal (deflate.ts:1412-1421)
-      emit(bb[p - c0]);
-      if (in_blk == ZS_SYM_END) close_block(p);
-      p++;
-    } else {
-      ma = 1;
-      p++;
+    __syncthreads();
+  }
+
+  // ---- block records (deflate.ts:1434-1440: the final block takes the rest, possibly empty)
+  const bool final_lit = nseg > 0 && sh_tail[0] != 0;
+  const uint32_t checked = final_lit ? total - 1 : total;
+  const uint32_t nflush = checked / ZS_SYM_END;
+  // window base when the final block is flushed: slides up to the last visited position
+  const uint32_t v_last = total == 0 ? 0u : final_lit ? n - 1 : last_start + 1;
+  const uint32_t final_slides = zs_slides(v_last, n);
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 <= nflush; b0 += 64) {
+    const uint32_t b = b0 + lane;
+    zs_block k;
+    if (b <= nflush) {
+      const uint32_t in_start = b == 0 ? 0u : blk[b - 1].in_end;
+      const uint32_t in_end = b < nflush ? blk[b].in_end : n;
+      const uint32_t slides = b < nflush ? blk[b].pad : final_slides;
+      k.sym_start = b * ZS_SYM_END;
+      k.sym_count = b < nflush ? ZS_SYM_END : total - nflush * ZS_SYM_END;
+      k.in_start = in_start;
+      k.in_end = in_end;
+      k.type = 0; k.hdr_bits = 0; k.data_bits = 0; k.pad = 0; k.bit_off = 0; k.bit_end = 0;
+      // bit 1: the block began before the slid window (matters for stored blocks)
+      k.last = (b == nflush ? 1u : 0u) | ((uint64_t)in_start < 32768ull * slides ? 2u : 0u);
     }
+    __syncthreads();  // every read of in_end / pad in this chunk precedes the writes
+    if (b <= nflush) blk[b] = k;
+    __syncthreads();
   }
-  if (ma) {  // final deferred literal, tallied without a flush check (deflate.ts:1429-1432)
-    if (p - c0 > ZS_PARSE_MB) { stage(p - 1); c0 = p - 1; }
-    emit(bb[p - c0]);
-  }
-  drain();
-  // final block (deflate.ts:1434-1440): whatever is left, possibly empty
   if (lane == 0) {
-    zs_block b;
-    b.sym_start = nsym - in_blk;
-    b.sym_count = in_blk;
-    b.in_start = blk_start;
-    b.in_end = n;
-    b.type = 0; b.hdr_bits = 0; b.data_bits = 0; b.pad = 0; b.bit_off = 0; b.bit_end = 0;
-    b.last = 1u | (blk_start < base ? 2u : 0u);
-    blk[nflush] = b;
-    streams[s].nsym = nsym;
+    streams[s].nsym = total;
     streams[s].nblk = nflush + 1;
   }
 }

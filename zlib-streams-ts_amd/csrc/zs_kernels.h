@@ -36,7 +36,10 @@ __global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint
                            const uint16_t* prevd, uint2* mres, int chain, int nice);
 __global__ void zs_k_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint32_t* blk_base, const uint2* mres, uint32_t* syms, zs_block* blocks,
-                           zs_stream* streams, int good, int lazy);
+                           zs_stream* streams, uint32_t* scratch, int good, int lazy);
+// parse scratch words per 1024-position segment (deflate_parse.hip)
+#define ZS_PARSE_SEG 1024u
+#define ZS_PARSE_SEG_WORDS 3596u
 __global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,
                           int lazy, int nice);
