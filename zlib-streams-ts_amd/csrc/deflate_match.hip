@@ -166,12 +166,15 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       uint32_t cur = q0;
       for (;;) {
         const uint32_t cp = cur - w0;
-        // first 8 bytes from three aligned LDS words; longer matches fall to the loop
+        // the chain link and the first 8 bytes (three aligned LDS words) are read
+        // together: one LDS round trip per candidate; longer matches fall to the loop
+        const uint32_t d = pv[cp];
         const uint32_t wi = cp >> 2, sh = cp & 3u;
         const uint32_t a0 = wb[wi], a1 = wb[wi + 1], a2 = wb[wi + 2];
         const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, sh) ^ s0;
         const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, sh) ^ s1;
-        uint32_t k = x0 ? (uint32_t)(__builtin_ctz(x0) >> 3) : x1 ? 4u + (uint32_t)(__builtin_ctz(x1) >> 3) : 8u;
+        const uint64_t x = ((uint64_t)x1 << 32) | x0;
+        uint32_t k = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
         if (k == 8u) {
           while (k < maxc) {
             const uint32_t x = win_word(wb, cp + k) ^ win_word(wb, sp + k);
@@ -189,7 +192,6 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
         best_s = snap ? best : best_s;
         bq_s = snap ? bq : bq_s;
         small_set = small_set || snap;
-        const uint32_t d = pv[cp];
         const uint32_t nxt = cur - d;
         // chain ends: nice match, budget spent, no link, or cur <= limit (deflate.ts:1109)
         if (nice_stop || cnt >= budget || d == 0 || nxt <= limit) break;
