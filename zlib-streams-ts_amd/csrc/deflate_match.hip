@@ -91,6 +91,49 @@ __global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, 
   }
 }
 
+// --------------------------------------------------------------- zs_k_depth
+// Chain depth of every position: the number of links of its chain of
+// prevd[] links (capped at 255), depth(p) = depth(p - prevd[p]) + 1.  It only
+// orders the work of zs_k_match (positions with similar chain lengths share a
+// wave), never its results.  One wave per stream, 64 positions per step; links
+// inside the step are resolved by pointer jumping, earlier ones from an LDS ring.
+__global__ __launch_bounds__(64) void zs_k_depth(const uint32_t* __restrict__ in_len,
+                                                 const uint64_t* __restrict__ pos_base,
+                                                 const uint16_t* __restrict__ prevd, uint8_t* __restrict__ depth) {
+  __shared__ uint8_t ring[32768];
+  const int s = blockIdx.x;
+  const uint32_t n = in_len[s];
+  const uint16_t* pd = prevd + pos_base[s];
+  uint8_t* dp = depth + pos_base[s];
+  const int lane = (int)threadIdx.x;
+  for (uint32_t g0 = 0; g0 < n; g0 += 64) {
+    const uint32_t p = g0 + (uint32_t)lane;
+    const uint32_t d = p < n ? pd[p] : 0u;
+    // list ranking: link = lane of the previous position in this step, or -1
+    int link = -1;
+    uint32_t sum = 0;
+    if (d != 0) {
+      const uint32_t q = p - d;
+      if (q >= g0) { link = (int)(q - g0); sum = 1; }
+      else sum = (uint32_t)ring[q & 32767u] + 1u;
+    }
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+      const uint32_t ls = __shfl(sum, link < 0 ? lane : link, 64);
+      const int ll = __shfl(link, link < 0 ? lane : link, 64);
+      if (link >= 0) { sum += ls; link = ll; }
+    }
+    const uint32_t v = sum < 255u ? sum : 255u;
+    __builtin_amdgcn_wave_barrier();
+    if (p < n) {
+      ring[p & 32767u] = (uint8_t)v;
+      dp[p] = (uint8_t)v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // --------------------------------------------------------------- zs_k_match
 #define ZS_TILE 8192u
 #define ZS_LOOKBACK 32768u
@@ -105,10 +148,13 @@ static __device__ __forceinline__ uint32_t win_word(const uint32_t* wb, uint32_t
 __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                    const uint32_t* __restrict__ in_len,
                                                    const uint64_t* __restrict__ pos_base,
-                                                   const uint16_t* __restrict__ prevd, uint2* __restrict__ mres,
+                                                   const uint16_t* __restrict__ prevd,
+                                                   const uint8_t* __restrict__ depth, uint2* __restrict__ mres,
                                                    int chain, int nice_cfg) {
   __shared__ uint32_t wb[ZS_WIN_WORDS + 2];
   __shared__ uint16_t pv[ZS_LOOKBACK + ZS_TILE];
+  __shared__ uint16_t order[ZS_TILE];  // tile positions, longest expected chains first
+  __shared__ uint32_t bins[256];
   const int s = blockIdx.y;
   const uint32_t n = in_len[s];
   const uint32_t t0 = blockIdx.x * ZS_TILE;
@@ -145,11 +191,47 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
     }
   }
   for (uint32_t i = threadIdx.x; i < t1 - w0; i += blockDim.x) pv[i] = pd[w0 + i];
+  // Deal positions to lanes by decreasing chain depth (a counting sort): the
+  // 64 chains a wave walks in lock-step then have similar lengths, instead of
+  // every wave waiting for its longest chain.
+  const uint32_t cap = (uint32_t)chain < 255u ? (uint32_t)chain : 255u;
+  const uint8_t* dp = depth + pos_base[s];
+  if (threadIdx.x < 256) bins[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t key[ZS_TILE / 1024];
+#pragma unroll
+  for (uint32_t i = 0; i < ZS_TILE / 1024; i++) {
+    const uint32_t p = t0 + threadIdx.x + 1024 * i;
+    key[i] = p < t1 ? 255u - min((uint32_t)dp[p], cap) : 0u;
+    if (p < t1) atomicAdd(&bins[key[i]], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the 256 bins, one wave
+    uint32_t v[4], t = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) { v[j] = bins[threadIdx.x * 4 + j]; t += v[j]; }
+    uint32_t x = t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (threadIdx.x >= (uint32_t)d) x += y;
+    }
+    uint32_t run = x - t;
+#pragma unroll
+    for (int j = 0; j < 4; j++) { bins[threadIdx.x * 4 + j] = run; run += v[j]; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < ZS_TILE / 1024; i++) {
+    const uint32_t o = threadIdx.x + 1024 * i;
+    if (t0 + o < t1) order[atomicAdd(&bins[key[i]], 1u)] = (uint16_t)o;
+  }
   __syncthreads();
 
   const uint32_t budget = (uint32_t)chain, budget_small = (uint32_t)chain >> 2;
   uint2* out = mres + pos_base[s];
-  for (uint32_t p = t0 + threadIdx.x; p < t1; p += blockDim.x) {
+  for (uint32_t oi = threadIdx.x; oi < t1 - t0; oi += blockDim.x) {
+    const uint32_t p = t0 + order[oi];
     uint2 r = make_uint2(0, 0);
     const uint32_t d0 = p + 2 < n ? pv[p - w0] : 0;
     const uint32_t q0 = p - d0;
