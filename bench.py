@@ -90,13 +90,15 @@ def main():
     out_cap = (ctypes.c_uint32 * S)(*([cap] * S))
     eng = zsamd.Engine(local)
     stream = torch.cuda.current_stream(dev)
-    gathered = [torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(world)] if world > 1 else None
+    import zsamd.shard as shard
 
     def step():
         eng.compress_device(args.level, args.format, S, d_in.data_ptr(), in_off, in_len, d_out.data_ptr(), out_off,
                             out_cap, d_status.data_ptr(), d_len.data_ptr(), stream.cuda_stream)
         if world > 1:
-            dist.all_gather(gathered, d_len)
+            # the final size gather (RCCL all_gather over xGMI): global output layout on every rank
+            sizes = shard.gather_sizes(d_len, world * S)
+            shard.global_offsets(sizes)
 
     for _ in range(args.warmup):
         step()

@@ -125,3 +125,9 @@ def test_c4_256k_streams_match_reference_goldens(engine, name, level):
     res = engine.compress_batch_raw(inputs, "deflate-raw", level)
     bad = [i for i, (st, out) in enumerate(res) if st != 1 or (len(out), hashlib.sha256(out).digest()[:16]) != recs[i]]
     assert not bad, bad[:10]
+
+
+@pytest.mark.gpu
+def test_lds_atomic_lane_order_selftest(engine):
+    """The chain builder's hardware assumption (selftest.hip) holds on this part."""
+    assert engine.selftest() == 0

@@ -122,7 +122,36 @@ int zs_ctx_create(int device, zs_ctx** out) {
     delete c;
     return fail(ZS_MEM_ERROR, "%s", hipGetErrorString(e));
   }
+  // the chain builder relies on lane-ordered LDS atomics: check before any use
+  uint64_t bad = 0;
+  const int st = zs_selftest(c, &bad);
+  if (st != ZS_OK || bad != 0) {
+    const std::string why = st != ZS_OK ? std::string(zs_last_error())
+                                        : std::to_string(bad) + " lane-order violations of same-address LDS atomics";
+    zs_ctx_destroy(c);
+    return fail(ZS_STREAM_ERROR, "self-test failed: %s", why.c_str());
+  }
   *out = c;
+  return ZS_OK;
+}
+
+int zs_selftest(zs_ctx* c, uint64_t* violations) {
+  if (!c || !violations) return fail(ZS_STREAM_ERROR, "invalid arguments");
+  *violations = 0;
+  HIPCHK(hipSetDevice(c->device));
+  uint32_t* d_bad = nullptr;
+  HIPCHK(hipMalloc(&d_bad, sizeof(uint32_t)));
+  hipError_t e = hipMemsetAsync(d_bad, 0, sizeof(uint32_t), c->stream);
+  if (e == hipSuccess) {
+    zs_k_selftest<<<256, 64, 0, c->stream>>>(d_bad, 32);
+    e = hipGetLastError();
+  }
+  uint32_t h = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&h, d_bad, sizeof h, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_bad);
+  if (e != hipSuccess) return fail(ZS_MEM_ERROR, "%s", hipGetErrorString(e));
+  *violations = h;
   return ZS_OK;
 }
 

@@ -56,3 +56,4 @@ __global__ void zs_k_wrap(const zs_stream* streams, uint8_t* out, const uint64_t
                           int wrap, int level, int nstreams);
 __global__ void zs_k_checksum(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t* check,
                               int kind);
+__global__ void zs_k_selftest(uint32_t* bad, int rounds);

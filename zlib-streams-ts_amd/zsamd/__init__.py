@@ -20,7 +20,8 @@ import os
 from typing import List, Optional, Sequence, Tuple
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libzsgpu.so")
+# ZS_LIB overrides the library path (A/B runs of kernel variants)
+LIB_PATH = os.environ.get("ZS_LIB") or os.path.join(os.path.dirname(_HERE), "libzsgpu.so")
 
 Z_OK, Z_STREAM_END, Z_NEED_DICT = 0, 1, 2
 Z_STREAM_ERROR, Z_DATA_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = -2, -3, -4, -5
@@ -102,6 +103,7 @@ def lib():
     L.zs_last_phase_ms.argtypes = [_P, ctypes.c_char_p]
     L.zs_set_timing.argtypes = [_P, ctypes.c_int]
     L.zs_corpus.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P, ctypes.c_int]
+    L.zs_selftest.argtypes = [_P, _U64P]
     _lib = L
     return L
 
@@ -125,6 +127,14 @@ class Engine:
         if r != 0:
             raise ZsUnavailable("zs_ctx_create(%d) failed: %s" % (device, L.zs_last_error().decode()))
         self._L, self._ctx, self.device = L, ctx, device
+
+    def selftest(self) -> int:
+        """Lane-order violations of same-address LDS atomics (0 expected; see selftest.hip)."""
+        v = ctypes.c_uint64(0)
+        r = self._L.zs_selftest(self._ctx, ctypes.byref(v))
+        if r != 0:
+            raise ZsError("zs_selftest failed: %s" % self._L.zs_last_error().decode())
+        return int(v.value)
 
     def close(self):
         if getattr(self, "_ctx", None):
