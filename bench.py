@@ -80,7 +80,7 @@ def main():
     first = rank * S
     host = zsamd.corpus(args.corpus, first, S, L, threads=8)
     d_in = torch.frombuffer(host, dtype=torch.uint8).to(dev)
-    cap = zsamd.deflate_bound(L, args.format)
+    cap = zsamd.deflate_capacity(L, args.format)
     d_out = torch.zeros(S * cap, dtype=torch.uint8, device=dev)
     d_status = torch.zeros(S, dtype=torch.int32, device=dev)
     d_len = torch.zeros(S, dtype=torch.int32, device=dev)

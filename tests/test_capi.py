@@ -46,11 +46,12 @@ def test_no_gpu_means_loud_failure():
 def test_deflate_bound_matches_reference_formula():
     import zsamd
 
-    # deflate.ts:615-674 (memLevel 8, wbits 15): n + n>>12 + n>>14 + n>>25 + 7 + wraplen, rounded to 4
+    # deflate.ts:615-674 (memLevel 8, wbits 15): n + n>>12 + n>>14 + n>>25 + 7 + wraplen
     for n in [0, 1, 100, 65536, 262144, 10 ** 7]:
         for fmt, wl in [("deflate-raw", 0), ("deflate", 6), ("gzip", 18)]:
             b = n + (n >> 12) + (n >> 14) + (n >> 25) + 7 + wl
-            assert zsamd.deflate_bound(n, fmt) == (b + 3) & ~3
+            assert zsamd.deflate_bound(n, fmt) == b
+            assert zsamd.deflate_capacity(n, fmt) == (b + 3) & ~3
 
 
 def test_corpus_generator_matches_spec():

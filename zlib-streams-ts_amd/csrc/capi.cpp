@@ -178,7 +178,7 @@ double zs_last_phase_ms(zs_ctx* c, const char* phase) {
 uint64_t zs_deflate_bound(uint64_t n, int wbits) {  // deflate.ts:615-674, memLevel 8 / windowBits 15
   const uint64_t wraplen = wbits < 0 ? 0 : (wbits > 15 ? 18 : 6);
   const uint64_t b = n + (n >> 12) + (n >> 14) + (n >> 25) + 13 - 6 + wraplen;
-  return (b + 3) & ~3ull;  // the engine writes whole 32-bit words
+  return b;  // (output capacities must still be multiples of 4: round up when allocating)
 }
 
 }  // extern "C"

@@ -1,0 +1,109 @@
+// streams-api.mjs -- the batch entry the reference's src/streams-api.ts gains
+// (SURVEY.md 8(b)): compressBatch / decompressBatch route whole batches of
+// independent streams to the MI355X engine through the N-API addon.
+//
+// Per stream the result is exactly what piping that buffer alone through
+//   new CompressionStream(format, {level})   (src/streams-api.ts -> src/mod/streams.ts:242-251)
+//   new DecompressionStream(format)          (src/mod/streams.ts:253-262)
+// yields when the whole buffer is written in ONE write() followed by close(),
+// including the stream layer's error strings ("init failed: N",
+// "process error: N", "finalization error: N", streams.ts:53,117,170).
+// The CPU CompressionStream / DecompressionStream classes stay the
+// reference's own; this module only adds the batch path.
+import { createRequire } from "module";
+
+const require = createRequire(import.meta.url);
+const addon = require("./zsnapi.node");
+
+// format -> windowBits, streams.ts:220 (compression) and 233 (decompression)
+const COMPRESS_WBITS = { "deflate": 15, "deflate-raw": -15, "gzip": 31 };
+const DECOMPRESS_WBITS = { "deflate": 15, "deflate-raw": -15, "gzip": 31, "deflate64-raw": -16 };
+const Z_STREAM_END = 1;
+const Z_STREAM_ERROR = -2;
+const PHASE_INIT = 1, PHASE_FINISH = 3;
+
+function streamError(status, phase) {
+  if (phase === PHASE_INIT) return new Error(`init failed: ${status}`);
+  if (phase === PHASE_FINISH) return new Error(`finalization error: ${status}`);
+  return new Error(`process error: ${status}`);
+}
+
+function checkInputs(inputs) {
+  if (!Array.isArray(inputs)) throw new TypeError("inputs must be an array of Uint8Array");
+  return inputs.map((x) => {
+    if (x instanceof Uint8Array) return x;
+    if (ArrayBuffer.isView(x)) return new Uint8Array(x.buffer, x.byteOffset, x.byteLength);
+    if (x instanceof ArrayBuffer) return new Uint8Array(x);
+    throw new TypeError("inputs must be Uint8Array / ArrayBufferView / ArrayBuffer");
+  });
+}
+
+function compressWbits(format) {
+  const w = COMPRESS_WBITS[format];
+  if (w === undefined) throw new TypeError(`Unsupported compression format: ${format}`);
+  return w;
+}
+
+function decompressWbits(format) {
+  const w = DECOMPRESS_WBITS[format];
+  if (w === undefined) throw new TypeError(`Unsupported decompression format: ${format}`);
+  return w;
+}
+
+function runCompress(inputs, format, options) {
+  const wbits = compressWbits(format);
+  const level = options.level === undefined ? -1 : options.level;  // -1 -> 6, deflate.ts:268-270
+  let res;
+  try {
+    res = addon.compressBatch(checkInputs(inputs), wbits, level, options.device || 0);
+  } catch (e) {
+    // argument validation of deflateInit2_ (deflate.ts:281-294) surfaces as the stream layer's init error
+    if (e.code === String(Z_STREAM_ERROR)) throw streamError(Z_STREAM_ERROR, PHASE_INIT);
+    throw e;
+  }
+  return res.outputs.map((out, i) => (res.status[i] === Z_STREAM_END ? out : streamError(res.status[i], PHASE_FINISH)));
+}
+
+function runDecompress(inputs, format, options) {
+  const wbits = decompressWbits(format);
+  const ins = checkInputs(inputs);
+  const cap = options.outCapacity === undefined ? ins.map((x) => Math.max(65536, 16 * x.length)) : options.outCapacity;
+  const res = addon.decompressBatch(ins, wbits, cap, options.device || 0);
+  return res.outputs.map((out, i) => {
+    if (res.status[i] === Z_STREAM_END) return out;
+    const err = streamError(res.status[i], res.phase[i]);
+    err.zmsg = res.message[i];  // the z_stream msg (inflate.ts:397-1031, inffast.ts:108,197,210)
+    return err;
+  });
+}
+
+const settle = (xs) => xs.map((x) => (x instanceof Error ? { status: "rejected", reason: x } : { status: "fulfilled", value: x }));
+
+/** Compress every input as an independent stream; rejects with the first stream's error. */
+export async function compressBatch(inputs, format = "deflate", options = {}) {
+  const out = runCompress(inputs, format, options);
+  const bad = out.find((x) => x instanceof Error);
+  if (bad) throw bad;
+  return out;
+}
+
+/** Decompress every input as an independent stream; rejects with the first stream's error. */
+export async function decompressBatch(inputs, format = "deflate", options = {}) {
+  const out = runDecompress(inputs, format, options);
+  const bad = out.find((x) => x instanceof Error);
+  if (bad) throw bad;
+  return out;
+}
+
+/** Per-stream outcomes, Promise.allSettled style. */
+export async function compressBatchSettled(inputs, format = "deflate", options = {}) {
+  return settle(runCompress(inputs, format, options));
+}
+
+export async function decompressBatchSettled(inputs, format = "deflate", options = {}) {
+  return settle(runDecompress(inputs, format, options));
+}
+
+export const deflateBound = (length, format = "deflate") => addon.deflateBound(length, compressWbits(format));
+export const engineVersion = () => addon.version();
+export const selfTest = (device = 0) => addon.selfTest(device);

@@ -1,0 +1,79 @@
+// GPU parity through the JavaScript host path (streams-api.mjs -> zsnapi.node
+// -> libzsgpu.so): the reference's golden fixtures (tests/golden/, produced by
+// the reference bundle) must come out byte-identical, and failing streams must
+// reject with the stream layer's error strings.
+import { createHash } from "crypto";
+import { readFileSync } from "fs";
+import { dirname, join } from "path";
+import { fileURLToPath } from "url";
+
+import * as corpus from "../../../tests/golden/corpus.mjs";
+import * as api from "../streams-api.mjs";
+
+const here = dirname(fileURLToPath(import.meta.url));
+const golden = join(here, "..", "..", "..", "tests", "golden");
+const sha = (b) => createHash("sha256").update(b).digest("hex");
+let checks = 0;
+const expect = (c, m) => { if (!c) throw new Error("FAIL " + m); checks++; };
+
+function deflateCases() {
+  const g = JSON.parse(readFileSync(join(golden, "deflate_small.json"), "utf8"));
+  const side = JSON.parse(readFileSync(join(golden, "deflate_small_inputs.json"), "utf8"));
+  return g.cases.map((c) => ({ c, data: c.spec.kind === "hex_sha" ? new Uint8Array(Buffer.from(side[c.spec.sha256], "hex")) : corpus.make(c.spec) }));
+}
+
+function inflateCases() {
+  const g = JSON.parse(readFileSync(join(golden, "inflate_small.json"), "utf8"));
+  const out = [];
+  for (const c of g.cases) {
+    if (c.in_hex != null) out.push({ c, data: new Uint8Array(Buffer.from(c.in_hex, "hex")) });
+    else if (c.name.startsWith("d64_")) out.push({ c, data: new Uint8Array(readFileSync(join(golden, "d64", c.name.slice(4)))) });
+    else if (c.in_len === 0) out.push({ c, data: new Uint8Array(0) });
+  }
+  return out;
+}
+
+async function main() {
+  // deflate: every golden case at levels 1..9, batched per (level, format)
+  const groups = new Map();
+  for (const x of deflateCases()) {
+    if (x.c.level < 1) continue;  // level 0 (deflate_stored) is not offered by the GPU engine
+    const k = x.c.level + "/" + x.c.format;
+    if (!groups.has(k)) groups.set(k, []);
+    groups.get(k).push(x);
+  }
+  for (const [k, xs] of groups) {
+    const [level, format] = k.split("/");
+    const outs = await api.compressBatch(xs.map((x) => x.data), format, { level: Number(level) });
+    xs.forEach((x, i) => expect(outs[i].length === x.c.out_len && sha(outs[i]) === x.c.out_sha256,
+                                `deflate ${k} ${x.c.spec.kind} ${x.c.in_len}`));
+  }
+  // inflate: KATs, deflate64 fixtures, corrupt streams -> bytes or the reference's error string
+  const byFmt = new Map();
+  for (const x of inflateCases()) {
+    if (!byFmt.has(x.c.format)) byFmt.set(x.c.format, []);
+    byFmt.get(x.c.format).push(x);
+  }
+  for (const [format, xs] of byFmt) {
+    const res = await api.decompressBatchSettled(xs.map((x) => x.data), format,
+                                                 { outCapacity: xs.map((x) => Math.max(65536, (x.c.out_len || 0) + 4096)) });
+    xs.forEach((x, i) => {
+      if (x.c.ok) expect(res[i].status === "fulfilled" && sha(res[i].value) === x.c.out_sha256, `inflate ${x.c.name}`);
+      else expect(res[i].status === "rejected" && res[i].reason.message === x.c.err, `inflate error ${x.c.name}`);
+    });
+  }
+  // round trip of T-corpus streams in every format
+  const inputs = [0, 1, 2, 3].map((i) => corpus.text(corpus.streamSeed(i), 65536));
+  for (const format of ["deflate", "deflate-raw", "gzip"]) {
+    const back = await api.decompressBatch(await api.compressBatch(inputs, format), format);
+    back.forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(inputs[i])) === 0, `round trip ${format} ${i}`));
+  }
+  // deflateInit2_ validation (deflate.ts:281-294) surfaces as the stream layer's init error
+  let msg = "";
+  try { await api.compressBatch([inputs[0]], "deflate", { level: 10 }); } catch (e) { msg = e.message; }
+  expect(msg === "init failed: -2", "level 10 -> init failed: -2");
+  expect(api.selfTest() === 0, "LDS lane-order self-test");
+  console.log("ok " + checks);
+}
+
+main().catch((e) => { console.error(e.message || e); process.exit(1); });

@@ -114,7 +114,13 @@ def _arr(ctype, values):
 
 
 def deflate_bound(n: int, fmt: str = "deflate-raw") -> int:
+    """deflateBound (deflate.ts:615-674) for a fresh stream, memLevel 8."""
     return int(lib().zs_deflate_bound(n, compress_wbits(fmt)))
+
+
+def deflate_capacity(n: int, fmt: str = "deflate-raw") -> int:
+    """deflate_bound rounded up to the engine's 4-byte output granularity."""
+    return (deflate_bound(n, fmt) + 3) & ~3
 
 
 class Engine:
@@ -180,7 +186,7 @@ class Engine:
             offs.append(o)
             lens.append(len(b))
             o += len(b)
-        caps = [int(self._L.zs_deflate_bound(len(b), wbits)) for b in inputs]
+        caps = [(int(self._L.zs_deflate_bound(len(b), wbits)) + 3) & ~3 for b in inputs]
         ooffs, oo = [], 0
         for c in caps:
             ooffs.append(oo)
