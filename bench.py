@@ -37,7 +37,26 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check every output against the batch golden")
+    ap.add_argument("--mode", default="deflate", choices=["deflate", "inflate"],
+                    help="deflate: the headline (configs[1]); inflate: C3 decode of pre-built members (configs[2])")
+    ap.add_argument("--replicas", type=int, default=16, help="inflate: members = streams x replicas (C3: 4096 x 16)")
     return ap.parse_args()
+
+
+def profiled_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary (FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction applied by
+    tools/summarize_profile.py), or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")))
+    for f in reversed(files):
+        try:
+            e = json.load(open(f)).get(kernel)
+        except (OSError, ValueError):
+            continue
+        if e and "hbm_bytes_corrected" in e:
+            return int(e["hbm_bytes_corrected"]), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def cpu_baseline(args):
@@ -63,6 +82,8 @@ def cpu_baseline(args):
 
 def main():
     args = parse()
+    if args.mode == "inflate":
+        return main_inflate(args)
     import torch
     import torch.distributed as dist
     import zsamd
@@ -150,8 +171,9 @@ def main():
         if dom:
             alg = in_total + out_total  # bytes_in + bytes_out per stream, x streams per launch
             achieved = alg / (phase_avg[dom] / 1e3) / 1e9
+            traffic, tsrc = profiled_traffic("zs_k_" + dom)
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
                     "algorithmic_bytes": alg, "kernel_ms": phase_avg[dom], "phase_ms": phase_avg,
                     "pipeline_ms": round(sum(phase_avg.values()), 4)}
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
@@ -166,6 +188,113 @@ def main():
                        "compressed_bytes_per_gpu": out_total, "ratio": round(in_total / max(1, out_total), 4),
                        "parallelism": "dp%d" % world},
             "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_inflate(args):
+    """C3: 4096 unique M-corpus 64 KiB buffers compressed at
+    deflate-raw L6 (by this engine, bit-exact to the reference; the batch golden
+    is checked), replicated x16 = 65,536 members, decoded on one GPU.  Metric:
+    uncompressed (output) MB/s.  Weak scaling: rank r decodes its own copy."""
+    import torch
+    import torch.distributed as dist
+    import zsamd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    S, L, R = args.streams, args.stream_bytes, args.replicas
+    eng = zsamd.Engine(local)
+    host = zsamd.corpus("mixed", 0, S, L, threads=8)
+    comp = eng.compress_batch([bytes(host[i * L:(i + 1) * L]) for i in range(S)], "deflate-raw", 6)
+    members = comp * R
+    N = len(members)
+    blob = b"".join(members)
+    d_in = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    offs, o = [], 0
+    for m in members:
+        offs.append(o)
+        o += len(m)
+    in_off = (ctypes.c_uint64 * N)(*offs)
+    in_len = (ctypes.c_uint32 * N)(*[len(m) for m in members])
+    cap = L
+    d_out = torch.zeros(N * cap, dtype=torch.uint8, device=dev)
+    out_off = (ctypes.c_uint64 * N)(*[i * cap for i in range(N)])
+    out_cap = (ctypes.c_uint32 * N)(*([cap] * N))
+    i32 = lambda: torch.zeros(N, dtype=torch.int32, device=dev)
+    d_status, d_phase, d_msg, d_len, d_cons = i32(), i32(), i32(), i32(), i32()
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.decompress_device("deflate-raw", N, d_in.data_ptr(), in_off, in_len, d_out.data_ptr(), out_off, out_cap,
+                              d_status.data_ptr(), d_phase.data_ptr(), d_msg.data_ptr(), d_len.data_ptr(),
+                              d_cons.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.set_timing(True)
+    kms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kms += max(0.0, eng.last_ms("inflate"))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    eng.set_timing(False)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    assert int((d_status != 1).sum()) == 0, "some members failed"
+    assert int(d_len.sum()) == N * L
+    if args.verify:
+        ob = d_out.cpu().numpy()
+        for i in range(S):
+            assert ob[i * cap:(i + 1) * cap].tobytes() == bytes(host[i * L:(i + 1) * L]), "member %d differs" % i
+    if rank == 0:
+        out_total, in_total = N * L, len(blob)
+        k_ms = kms / args.steps
+        alg = in_total + out_total  # SURVEY.md 8(d): compressed_in + uncompressed_out per member
+        achieved = alg / (k_ms / 1e3) / 1e9
+        cpu = None
+        if not (args.no_cpu_baseline or world > 1):
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle
+            done, tt, i = 0, 0.0, 0
+            while tt < args.cpu_seconds and i < S:
+                t1 = time.perf_counter()
+                oracle.decompress(comp[i], "deflate-raw", cap=L)
+                tt += time.perf_counter() - t1
+                done += L
+                i += 1
+            cpu = {"value": round(done / tt / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+                   "sample": "%d of the %d unique members, oracle/ C restatement, 1 thread" % (i, S)}
+        line = {
+            "metric": "uncompressed MB/s, inflate deflate-raw L6 members (C3)",
+            "value": round(world * out_total / (elapsed / args.steps) / 1e6, 2), "unit": "MB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "%d members (%d unique M-corpus %d B buffers x %d), deflate-raw L6, decode" % (N, S, L, R),
+                       "members_per_gpu": N, "compressed_bytes_per_gpu": in_total, "parallelism": "dp%d" % world},
+            "roofline": {"bound": "hbm", "kernel": "inflate", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "algorithmic_bytes": alg, "kernel_ms": round(k_ms, 4)},
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
