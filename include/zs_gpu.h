@@ -124,6 +124,10 @@ int zs_adler32_batch_device(zs_ctx *ctx, uint32_t n_streams, const uint8_t *d_in
 double zs_last_batch_ms(zs_ctx *ctx);
 double zs_last_phase_ms(zs_ctx *ctx, const char *phase);
 void zs_set_timing(zs_ctx *ctx, int on);
+/* Engine options: "timing" (0/1, as zs_set_timing); "inflate_fast" (default 1):
+ * decode members lane-per-member and re-run only those that do not end cleanly
+ * on the exact stream-layer state machine (0: exact path for every member). */
+int zs_set_option(zs_ctx *ctx, const char *name, int value);
 
 /* Introspection for tests: copy an intermediate array of stream s of the last
  * deflate batch to host memory (what: 0 chain links u16/position, 1 match table

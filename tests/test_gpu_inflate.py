@@ -114,3 +114,46 @@ def test_c3_members_decode(engine):
         assert (len(c), hashlib.sha256(c).digest()[:16]) == recs[i]
     outs = engine.decompress_batch(comps, "deflate-raw")
     assert outs == srcs
+
+
+def _fast_vs_exact_corpus():
+    rng = random.Random(2024)
+    items = []
+    for c, d in golden_io.inflate_cases():
+        if d is not None and c["format"] != "deflate64-raw":
+            items.append((c["format"], d, max(1 << 17, 40 * len(d))))
+    for k in range(60):
+        fmt = rng.choice(["deflate-raw", "deflate", "gzip"])
+        n = rng.choice([0, 1, 7, 258, 5000, 65536, 70000, rng.randrange(1, 200000)])
+        src = corpus.make({"kind": rng.choice(["text", "mixed", "rand", "zeros", "ramp"]), "n": n,
+                           "seed": rng.randrange(1 << 32)})
+        comp = oracle.compress(src, rng.choice([1, 3, 6, 9]), fmt)[1]
+        cap = len(src) + 64
+        variant = k % 6
+        if variant == 1 and len(comp) > 4:
+            comp = comp[: rng.randrange(1, len(comp))]  # truncated
+        elif variant == 2:
+            comp = comp + bytes(rng.randrange(256) for _ in range(9))  # trailing bytes
+        elif variant == 3 and len(comp) > 8:
+            b = bytearray(comp)
+            b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)  # bit flip
+            comp = bytes(b)
+        elif variant == 4 and len(src) > 10:
+            cap = (len(src) // 2 + 3) & ~3  # too small
+        items.append((fmt, comp, cap))
+    return items
+
+
+def test_lane_fast_path_matches_exact_path(engine):
+    """The lane-per-member decoder (inflate_fast option) and the exact stream-layer
+    state machine agree on status, phase, message, bytes and consumed input."""
+    items = _fast_vs_exact_corpus()
+    for fmt in ("deflate-raw", "deflate", "gzip"):
+        its = [(d, cap) for f, d, cap in items if f == fmt]
+        engine.set_option("inflate_fast", 1)
+        fast = engine.decompress_batch_raw([d for d, _ in its], fmt, out_caps=[c for _, c in its])
+        engine.set_option("inflate_fast", 0)
+        exact = engine.decompress_batch_raw([d for d, _ in its], fmt, out_caps=[c for _, c in its])
+        engine.set_option("inflate_fast", 1)
+        for i, (a, b) in enumerate(zip(fast, exact)):
+            assert a == b, (fmt, i, a[:3], b[:3], len(a[3]), len(b[3]), a[4], b[4])

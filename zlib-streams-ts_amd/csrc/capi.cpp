@@ -64,7 +64,8 @@ struct zs_ctx {
   hipStream_t stream = nullptr;
   bool timing = false;
   // workspace
-  Buf meta, prevd, depth, mres, syms, blocks, streams, codes, hdr, check, istate, pscr;
+  Buf meta, prevd, depth, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
+  bool inflate_fast = true;
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res;
   std::vector<uint8_t> hmeta;
@@ -159,7 +160,7 @@ void zs_ctx_destroy(zs_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (Buf* b : {&c->pscr, &c->meta, &c->prevd, &c->depth, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
+  for (Buf* b : {&c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->depth, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
                  &c->istate, &c->d_in, &c->d_out, &c->d_res})
     if (b->p) (void)hipFree(b->p);
   (void)hipStreamDestroy(c->stream);
@@ -167,6 +168,14 @@ void zs_ctx_destroy(zs_ctx* c) {
 }
 
 void zs_set_timing(zs_ctx* c, int on) { c->timing = on != 0; }
+
+int zs_set_option(zs_ctx* c, const char* name, int value) {
+  if (!c || !name) return fail(ZS_STREAM_ERROR, "invalid arguments");
+  if (!strcmp(name, "timing")) c->timing = value != 0;
+  else if (!strcmp(name, "inflate_fast")) c->inflate_fast = value != 0;
+  else return fail(ZS_STREAM_ERROR, "unknown option %s", name);
+  return ZS_OK;
+}
 double zs_last_batch_ms(zs_ctx* c) { return c->total_ms; }
 double zs_last_phase_ms(zs_ctx* c, const char* phase) {
   double t = -1;
@@ -528,10 +537,18 @@ static const char* kInflateMsgs[ZS_MSG_COUNT] = {
 
 extern "C" const char* zs_inflate_message(int32_t i) { return (i >= 0 && i < ZS_MSG_COUNT) ? kInflateMsgs[i] : ""; }
 
-__global__ void zs_k_inflate_finish(const zs_inflate_result* r, int32_t* status, int32_t* phase, int32_t* msg,
-                                    uint32_t* out_len, uint32_t* consumed, int n) {
+__global__ void zs_k_inflate_finish(const zs_inflate_result* r, const zs_lane_res* lane, int32_t* status,
+                                    int32_t* phase, int32_t* msg, uint32_t* out_len, uint32_t* consumed, int n) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
+  if (lane && lane[s].bail == 0) {  // clean member from the lane path
+    status[s] = ZS_Z_STREAM_END;
+    phase[s] = ZS_PHASE_NONE_;
+    msg[s] = ZS_MSG_NONE;
+    out_len[s] = lane[s].out_len;
+    consumed[s] = lane[s].consumed;
+    return;
+  }
   status[s] = r[s].status;
   phase[s] = r[s].phase;
   msg[s] = r[s].msg;
@@ -564,13 +581,33 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
   uint8_t* dm = c->meta.as<uint8_t>();
   const size_t smem = zs_inflate_smem_bytes(wbits);
   HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+  const uint64_t* d_ioff = (const uint64_t*)(dm + ml.in_off);
+  const uint32_t* d_ilen = (const uint32_t*)(dm + ml.in_len);
+  const uint64_t* d_ooff = (const uint64_t*)(dm + ml.out_off);
+  const uint32_t* d_ocap = (const uint32_t*)(dm + ml.out_cap);
+  zs_lane_res* lres = nullptr;
   mark(c, st, "start");
-  zs_k_inflate<<<n, 64, smem, st>>>(d_in, (const uint64_t*)(dm + ml.in_off), (const uint32_t*)(dm + ml.in_len), d_out,
-                                    (const uint64_t*)(dm + ml.out_off), (const uint32_t*)(dm + ml.out_cap), wbits,
-                                    c->istate.as<zs_inflate_result>());
+  if (c->inflate_fast && wbits != -16) {
+    // lane-per-member fast path; anything but a clean end of stream goes to the exact kernel
+    HIPCHK(c->ltabs.ensure(zs_inflate_lane_scratch_bytes() * (size_t)n));
+    HIPCHK(c->lres.ensure(sizeof(zs_lane_res) * (size_t)n));
+    HIPCHK(c->llen.ensure(8ull * n));
+    lres = c->lres.as<zs_lane_res>();
+    zs_k_inflate_lane<<<(n + 63) / 64, 64, 0, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
+                                                    (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>());
+    mark(c, st, "inflate_lane");
+    if (wbits > 0) {  // trailer checks over the decoded bytes: adler32 (zlib) / crc32 (gzip)
+      uint32_t* chk = c->llen.as<uint32_t>() + n;
+      zs_k_checksum<<<n, 64, 0, st>>>(d_out, d_ooff, c->llen.as<uint32_t>(), chk, wbits == 31 ? 2 : 1);
+      zs_k_inflate_lane_verify<<<(n + 255) / 256, 256, 0, st>>>(lres, chk, n);
+      mark(c, st, "inflate_check");
+    }
+  }
+  zs_k_inflate<<<n, 64, smem, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
+                                    c->istate.as<zs_inflate_result>(), lres);
   mark(c, st, "inflate");
-  zs_k_inflate_finish<<<(n + 255) / 256, 256, 0, st>>>(c->istate.as<zs_inflate_result>(), d_status, d_phase, d_msg,
-                                                       d_out_len, d_consumed, (int)n);
+  zs_k_inflate_finish<<<(n + 255) / 256, 256, 0, st>>>(c->istate.as<zs_inflate_result>(), lres, d_status, d_phase,
+                                                       d_msg, d_out_len, d_consumed, (int)n);
   mark(c, st, "finish");
   HIPCHK(hipGetLastError());
   collect_marks(c);

@@ -858,9 +858,11 @@ __global__ __launch_bounds__(64) void zs_k_inflate(const uint8_t* __restrict__ i
                                                    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                    const uint64_t* __restrict__ out_off,
                                                    const uint32_t* __restrict__ out_cap, int wbits,
-                                                   zs_inflate_result* __restrict__ res) {
+                                                   zs_inflate_result* __restrict__ res,
+                                                   const zs_lane_res* __restrict__ only) {
   zs_lds& L = *reinterpret_cast<zs_lds*>(zs_inflate_smem);
   const int s = blockIdx.x;
+  if (only && only[s].bail == 0) return;  // decoded cleanly by the lane path
   zs_ist S;
   S.src = in + in_off[s];
   S.n = in_len[s];
@@ -941,4 +943,236 @@ __global__ __launch_bounds__(64) void zs_k_inflate(const uint8_t* __restrict__ i
 size_t zs_inflate_smem_bytes(int wbits) {
   const size_t ring = wbits == -16 ? 2 * 65536 : 2 * 32768;
   return sizeof(zs_lds) + ring;
+}
+
+// ===================================================================== fast path
+// One LANE per member.  The exact kernel above spends a whole wave on one
+// stream because it re-enacts the stream layer's call boundaries; but for a
+// member that decodes cleanly those boundaries change nothing in the output
+// (the inffast window-wrap defect aside, which this engine does not reproduce),
+// so a lane can decode it straight through: zlib's own tables (inflate_table
+// above, so invalid codes are recognised exactly as the reference does), a
+// 64-bit bit buffer, output written to HBM and match history read back from it.
+// A member takes the exact path instead (zs_k_inflate over the bailed members)
+// on ANY condition that is not a clean end of stream -- a data error, truncated
+// input, a dictionary request, gzip header fields, deflate64, a checksum or
+// length mismatch, or output capacity -- so statuses, phases and messages
+// always come from the exact state machine.
+struct zs_lane_tabs {
+  zcode codes[ENOUGH_LENS + ENOUGH_DISTS_9];
+  uint16_t lens[320];
+  uint16_t work[288];
+};
+
+struct zs_lane_reader {
+  const uint8_t* src;
+  uint32_t n, pos;  // next input byte
+  uint64_t hold;
+  uint32_t bits;
+};
+
+static __device__ __forceinline__ void zs_lr_fill(zs_lane_reader& R) {
+  while (R.bits <= 56) {
+    if (R.pos < R.n) R.hold |= (uint64_t)R.src[R.pos] << R.bits;  // zero bits past the end
+    R.pos++;
+    R.bits += 8;
+  }
+}
+// bits consumed so far
+static __device__ __forceinline__ uint64_t zs_lr_bitpos(const zs_lane_reader& R) {
+  return (uint64_t)R.pos * 8u - R.bits;
+}
+// consumed bits beyond the input: a truncated stream (the exact path reports it)
+static __device__ __forceinline__ bool zs_lr_over(const zs_lane_reader& R) {
+  return zs_lr_bitpos(R) > (uint64_t)R.n * 8u;
+}
+static __device__ __forceinline__ uint32_t zs_lr_take(zs_lane_reader& R, uint32_t k) {  // k <= 32
+  if (R.bits < k) zs_lr_fill(R);
+  const uint32_t v = (uint32_t)R.hold & (k == 32 ? 0xffffffffu : ((1u << k) - 1));
+  R.hold >>= k;
+  R.bits -= k;
+  return v;
+}
+static __device__ __forceinline__ void zs_lr_align(zs_lane_reader& R) {
+  const uint32_t d = R.bits & 7u;
+  R.hold >>= d;
+  R.bits -= d;
+}
+
+// decode one Huffman symbol with a zlib table (root `rbits`); returns the final entry
+static __device__ __forceinline__ zcode zs_lane_decode(zs_lane_reader& R, const zcode* t, uint32_t rbits) {
+  if (R.bits < 32) zs_lr_fill(R);
+  zcode here = t[(uint32_t)R.hold & ((1u << rbits) - 1)];
+  if (C_OP(here) && (C_OP(here) & 0xf0) == 0) {  // second-level table
+    const uint32_t rb = C_BITS(here);
+    const zcode last = here;
+    here = t[C_VAL(last) + (((uint32_t)R.hold & ((1u << (rb + C_OP(last))) - 1)) >> rb)];
+    R.hold >>= rb;
+    R.bits -= rb;
+  }
+  R.hold >>= C_BITS(here);
+  R.bits -= C_BITS(here);
+  return here;
+}
+
+__global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off,
+                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_off,
+                                                        const uint32_t* __restrict__ out_cap, int wbits, uint32_t n_members,
+                                                        zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
+                                                        uint32_t* __restrict__ lens_out) {
+  const uint32_t s = blockIdx.x * 64u + threadIdx.x;
+  if (s >= n_members) return;
+  zs_lane_tabs& T = tabs[s];
+  zs_lane_reader R;
+  R.src = in + in_off[s];
+  R.n = in_len[s];
+  R.pos = 0;
+  R.hold = 0;
+  R.bits = 0;
+  uint8_t* dst = out + out_off[s];
+  const uint32_t cap = out_cap[s];
+  uint32_t total = 0;
+  zs_lane_res r = {1u, 0u, 0u, 0u};
+  const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
+  bool bail = wbits == -16;                          // deflate64: exact path
+  // ---- wrapper header (inflate.ts:377-580): plain zlib / gzip headers only
+  if (!bail && wrap) {
+    const uint32_t b0 = zs_lr_take(R, 8), b1 = zs_lr_take(R, 8);
+    if ((wrap & 2) && b0 == 0x1f && b1 == 0x8b) {
+      const uint32_t cm = zs_lr_take(R, 8), flg = zs_lr_take(R, 8);
+      zs_lr_take(R, 32);  // MTIME
+      zs_lr_take(R, 16);  // XFL, OS
+      if (cm != 8 || flg != 0) bail = true;  // FEXTRA / FNAME / FCOMMENT / FHCRC / reserved: exact path
+    } else if (wrap & 1) {
+      if (((b0 << 8) | b1) % 31 || (b0 & 15) != 8 || (b0 >> 4) + 8 > 15 || (b1 & 0x20)) bail = true;
+    } else {
+      bail = true;  // "incorrect header check"
+    }
+  }
+  // ---- blocks
+  bool last = false;
+  while (!bail && !last) {
+    last = zs_lr_take(R, 1) != 0;
+    const uint32_t type = zs_lr_take(R, 2);
+    const zcode* lt;
+    const zcode* dt;
+    uint32_t lbits, dbits;
+    if (type == 0) {  // stored (inflate.ts:615-660)
+      zs_lr_align(R);
+      const uint32_t len = zs_lr_take(R, 16), nlen = zs_lr_take(R, 16);
+      if (len != (nlen ^ 0xffffu) || zs_lr_over(R) || total + len > cap) { bail = true; break; }
+      for (uint32_t i = 0; i < len; i++) dst[total + i] = (uint8_t)zs_lr_take(R, 8);
+      total += len;
+      if (zs_lr_over(R)) { bail = true; break; }
+      continue;
+    }
+    if (type == 1) {  // fixed tables (inflate.ts:218-280)
+      uint32_t sym, used;
+      for (sym = 0; sym < 144; sym++) T.lens[sym] = 8;
+      for (; sym < 256; sym++) T.lens[sym] = 9;
+      for (; sym < 280; sym++) T.lens[sym] = 7;
+      for (; sym < 288; sym++) T.lens[sym] = 8;
+      lbits = 9;
+      zs_inflate_table(LENS, T.lens, 288, T.codes, &lbits, T.work, false, &used);
+      for (sym = 0; sym < 32; sym++) T.lens[sym] = 5;
+      dbits = 5;
+      zs_inflate_table(DISTS, T.lens, 32, T.codes + used, &dbits, T.work, false, &sym);
+      lt = T.codes;
+      dt = T.codes + used;
+    } else if (type == 2) {  // dynamic (inflate.ts:662-836)
+      const uint32_t nlen = zs_lr_take(R, 5) + 257, ndist = zs_lr_take(R, 5) + 1, ncode = zs_lr_take(R, 4) + 4;
+      if (nlen > 286 || ndist > 30) { bail = true; break; }
+      uint32_t i;
+      for (i = 0; i < ncode; i++) T.lens[ZS_BL_ORDER[i]] = (uint16_t)zs_lr_take(R, 3);
+      for (; i < 19; i++) T.lens[ZS_BL_ORDER[i]] = 0;
+      uint32_t cbits = 7, used;
+      if (zs_inflate_table(CODES, T.lens, 19, T.codes, &cbits, T.work, false, &used)) { bail = true; break; }
+      i = 0;
+      while (i < nlen + ndist) {
+        const zcode here = zs_lane_decode(R, T.codes, cbits);
+        const uint32_t v = C_VAL(here);
+        if (v < 16) { T.lens[i++] = (uint16_t)v; continue; }
+        uint32_t rep, val = 0;
+        if (v == 16) {
+          if (i == 0) { bail = true; break; }
+          val = T.lens[i - 1];
+          rep = 3 + zs_lr_take(R, 2);
+        } else if (v == 17) {
+          rep = 3 + zs_lr_take(R, 3);
+        } else {
+          rep = 11 + zs_lr_take(R, 7);
+        }
+        if (i + rep > nlen + ndist) { bail = true; break; }
+        while (rep--) T.lens[i++] = (uint16_t)val;
+      }
+      if (bail || zs_lr_over(R) || T.lens[256] == 0) { bail = true; break; }
+      lbits = 9;
+      uint32_t lused, dused;
+      if (zs_inflate_table(LENS, T.lens, nlen, T.codes, &lbits, T.work, false, &lused)) { bail = true; break; }
+      dbits = 6;
+      if (zs_inflate_table(DISTS, T.lens + nlen, ndist, T.codes + lused, &dbits, T.work, false, &dused)) {
+        bail = true;
+        break;
+      }
+      lt = T.codes;
+      dt = T.codes + lused;
+    } else {
+      bail = true;  // "invalid block type"
+      break;
+    }
+    // symbols (inffast.ts:5-228 semantics, without the call boundaries)
+    for (;;) {
+      zcode here = zs_lane_decode(R, lt, lbits);
+      uint32_t op = C_OP(here);
+      if (op == 0) {
+        if (total >= cap) { bail = true; break; }
+        dst[total++] = (uint8_t)C_VAL(here);
+        continue;
+      }
+      if (op & 32) break;                   // end of block
+      if (!(op & 16)) { bail = true; break; }  // "invalid literal/length code"
+      uint32_t len = C_VAL(here) + zs_lr_take(R, op & 15u);
+      here = zs_lane_decode(R, dt, dbits);
+      op = C_OP(here);
+      if (!(op & 16)) { bail = true; break; }  // "invalid distance code"
+      const uint32_t dist = C_VAL(here) + zs_lr_take(R, op & 15u);
+      if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
+      const uint8_t* from = dst + total - dist;
+      uint8_t* to = dst + total;
+      for (uint32_t i = 0; i < len; i++) to[i] = from[i];
+      total += len;
+    }
+    if (zs_lr_over(R)) bail = true;
+  }
+  // ---- trailer (inflate.ts:1006-1036)
+  if (!bail && wrap) {
+    zs_lr_align(R);
+    const uint32_t a = zs_lr_take(R, 32);
+    if (wrap & 2 && !(wrap & 1)) {  // gzip: crc32 LE, then ISIZE LE
+      r.want = a;
+      const uint32_t isize = zs_lr_take(R, 32);
+      if (isize != total) bail = true;
+    } else {
+      r.want = __builtin_bswap32(a);  // zlib: adler32 big-endian
+    }
+    if (zs_lr_over(R)) bail = true;
+  }
+  if (!bail) {
+    r.bail = 0;
+    r.out_len = total;
+    r.consumed = (uint32_t)((zs_lr_bitpos(R) + 7u) >> 3);
+  }
+  res[s] = r;
+  lens_out[s] = r.out_len;  // for the checksum pass over the decoded bytes
+}
+
+size_t zs_inflate_lane_scratch_bytes() { return sizeof(zs_lane_tabs); }
+
+// checksum of the decoded output against the trailer: a mismatch sends the member to the exact path
+__global__ void zs_k_inflate_lane_verify(zs_lane_res* __restrict__ res, const uint32_t* __restrict__ check,
+                                         uint32_t n) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n && res[s].bail == 0 && res[s].want != check[s]) res[s].bail = 1;
 }

@@ -104,6 +104,7 @@ def lib():
     L.zs_set_timing.argtypes = [_P, ctypes.c_int]
     L.zs_corpus.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P, ctypes.c_int]
     L.zs_selftest.argtypes = [_P, _U64P]
+    L.zs_set_option.argtypes = [_P, ctypes.c_char_p, ctypes.c_int]
     _lib = L
     return L
 
@@ -156,6 +157,11 @@ class Engine:
     @property
     def handle(self):
         return self._ctx
+
+    def set_option(self, name: str, value: int):
+        """zs_set_option: "timing", "inflate_fast" (see zs_gpu.h)."""
+        if self._L.zs_set_option(self._ctx, name.encode(), int(value)) != 0:
+            raise ZsError(self._L.zs_last_error().decode())
 
     def set_timing(self, on: bool):
         self._L.zs_set_timing(self._ctx, 1 if on else 0)
