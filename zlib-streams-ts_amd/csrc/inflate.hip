@@ -1141,7 +1141,18 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
       const uint8_t* from = dst + total - dist;
       uint8_t* to = dst + total;
-      for (uint32_t i = 0; i < len; i++) to[i] = from[i];
+      if (dist >= 8) {  // 8 independent loads, then 8 stores: one memory round trip per 8 bytes
+        for (uint32_t i = 0; i < len; i += 8) {
+          uint8_t b[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) b[k] = i + k < len ? from[i + k] : 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            if (i + k < len) to[i + k] = b[k];
+        }
+      } else {  // overlapping copy: the source is being written
+        for (uint32_t i = 0; i < len; i++) to[i] = from[i];
+      }
       total += len;
     }
     if (zs_lr_over(R)) bail = true;
