@@ -1015,6 +1015,54 @@ static __device__ __forceinline__ zcode zs_lane_decode(zs_lane_reader& R, const 
   return here;
 }
 
+// LDS root tables of one lane: 8-bit lit/len and 6-bit distance roots, u16
+// entries (code length << 12 | symbol), 0 = code longer than the root (the lane
+// then decodes with its zlib table in HBM).  640 B per lane: four 64-lane
+// workgroups fill a CU's 160 KB.
+#define ZS_LROOT 8u
+#define ZS_DROOT 6u
+struct zs_lane_lds {
+  uint16_t lit[1u << ZS_LROOT];
+  uint16_t dist[1u << ZS_DROOT];
+};
+
+static __device__ void zs_lane_root(uint16_t* tab, uint32_t rbits, const uint16_t* lens, uint32_t n) {
+  uint32_t count[16], next[16];
+  for (uint32_t l = 0; l < 16; l++) count[l] = 0;
+  for (uint32_t i = 0; i < n; i++) count[lens[i]]++;
+  count[0] = 0;
+  uint32_t code = 0;
+  for (uint32_t l = 1; l < 16; l++) {  // canonical first codes (RFC 1951 3.2.2)
+    code = (code + count[l - 1]) << 1;
+    next[l] = code;
+  }
+  for (uint32_t k = 0; k < (1u << rbits); k++) tab[k] = 0;
+  for (uint32_t sym = 0; sym < n; sym++) {
+    const uint32_t l = lens[sym];
+    if (l == 0) continue;
+    const uint32_t c = next[l]++;
+    if (l > rbits) continue;
+    const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);  // the stream sends codes MSB first
+    for (uint32_t k = r; k < (1u << rbits); k += 1u << l) tab[k] = (uint16_t)((l << 12) | sym);
+  }
+}
+
+// a root-table symbol as the zlib table entry the decoder consumes
+static __device__ __forceinline__ zcode zs_lit_entry(uint32_t sym) {
+  if (sym < 256) return zpack(0, 0, sym);
+  if (sym == 256) return zpack(32 + 64, 0, 0);
+  const uint32_t c = sym - 257;  // length codes: base / extra bits (inflate/constants.ts:8-23)
+  if (c < 8) return zpack(16, 0, c + 3);
+  if (c == 28) return zpack(16, 0, 258);
+  const uint32_t x = (c >> 2) - 1;
+  return zpack(16 + x, 0, ((4u | (c & 3u)) << x) + 3u);
+}
+static __device__ __forceinline__ zcode zs_dist_entry(uint32_t d) {
+  if (d < 4) return zpack(16, 0, d + 1);
+  const uint32_t x = (d >> 1) - 1;
+  return zpack(16 + x, 0, ((2u | (d & 1u)) << x) + 1u);
+}
+
 __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off,
                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -1022,9 +1070,11 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
                                                         const uint32_t* __restrict__ out_cap, int wbits, uint32_t n_members,
                                                         zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
                                                         uint32_t* __restrict__ lens_out) {
+  __shared__ zs_lane_lds LL[64];
   const uint32_t s = blockIdx.x * 64u + threadIdx.x;
   if (s >= n_members) return;
   zs_lane_tabs& T = tabs[s];
+  zs_lane_lds& F = LL[threadIdx.x];
   zs_lane_reader R;
   R.src = in + in_off[s];
   R.n = in_len[s];
@@ -1081,6 +1131,10 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       zs_inflate_table(DISTS, T.lens, 32, T.codes + used, &dbits, T.work, false, &sym);
       lt = T.codes;
       dt = T.codes + used;
+      for (sym = 0; sym < 288; sym++) T.lens[sym] = sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8;
+      zs_lane_root(F.lit, ZS_LROOT, T.lens, 286);  // 286/287 stay out of the root: invalid codes decode via T
+      for (sym = 0; sym < 30; sym++) T.lens[sym] = 5;
+      zs_lane_root(F.dist, ZS_DROOT, T.lens, 30);    // 30/31 likewise
     } else if (type == 2) {  // dynamic (inflate.ts:662-836)
       const uint32_t nlen = zs_lr_take(R, 5) + 257, ndist = zs_lr_take(R, 5) + 1, ncode = zs_lr_take(R, 4) + 4;
       if (nlen > 286 || ndist > 30) { bail = true; break; }
@@ -1118,13 +1172,24 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       }
       lt = T.codes;
       dt = T.codes + lused;
+      zs_lane_root(F.lit, ZS_LROOT, T.lens, nlen);
+      zs_lane_root(F.dist, ZS_DROOT, T.lens + nlen, ndist);
     } else {
       bail = true;  // "invalid block type"
       break;
     }
     // symbols (inffast.ts:5-228 semantics, without the call boundaries)
     for (;;) {
-      zcode here = zs_lane_decode(R, lt, lbits);
+      if (R.bits < 32) zs_lr_fill(R);
+      zcode here;
+      const uint32_t fe = F.lit[(uint32_t)R.hold & ((1u << ZS_LROOT) - 1)];
+      if (fe >> 12) {
+        R.hold >>= fe >> 12;
+        R.bits -= fe >> 12;
+        here = zs_lit_entry(fe & 0x1ffu);
+      } else {
+        here = zs_lane_decode(R, lt, lbits);
+      }
       uint32_t op = C_OP(here);
       if (op == 0) {
         if (total >= cap) { bail = true; break; }
@@ -1134,7 +1199,15 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (op & 32) break;                   // end of block
       if (!(op & 16)) { bail = true; break; }  // "invalid literal/length code"
       uint32_t len = C_VAL(here) + zs_lr_take(R, op & 15u);
-      here = zs_lane_decode(R, dt, dbits);
+      if (R.bits < 32) zs_lr_fill(R);
+      const uint32_t de = F.dist[(uint32_t)R.hold & ((1u << ZS_DROOT) - 1)];
+      if (de >> 12) {
+        R.hold >>= de >> 12;
+        R.bits -= de >> 12;
+        here = zs_dist_entry(de & 0x1fu);
+      } else {
+        here = zs_lane_decode(R, dt, dbits);
+      }
       op = C_OP(here);
       if (!(op & 16)) { bail = true; break; }  // "invalid distance code"
       const uint32_t dist = C_VAL(here) + zs_lr_take(R, op & 15u);
