@@ -966,17 +966,26 @@ struct zs_lane_tabs {
 
 struct zs_lane_reader {
   const uint8_t* src;
-  uint32_t n, pos;  // next input byte
+  uint32_t n, pos;  // bytes moved into hold so far
   uint64_t hold;
   uint32_t bits;
+  uint32_t pf;      // input bytes [pos, pos + 4), loaded one refill ahead (zero past the end)
 };
 
+static __device__ __forceinline__ uint32_t zs_lr_load4(const zs_lane_reader& R, uint32_t at) {
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++)
+    if (at + k < R.n) v |= (uint32_t)R.src[at + k] << (8 * k);
+  return v;
+}
+// bits < 32 -> bits >= 32: the prefetched word enters hold and the next one is
+// requested, so its latency overlaps the decoding of the bits just added
 static __device__ __forceinline__ void zs_lr_fill(zs_lane_reader& R) {
-  while (R.bits <= 56) {
-    if (R.pos < R.n) R.hold |= (uint64_t)R.src[R.pos] << R.bits;  // zero bits past the end
-    R.pos++;
-    R.bits += 8;
-  }
+  R.hold |= (uint64_t)R.pf << R.bits;
+  R.bits += 32;
+  R.pos += 4;
+  R.pf = zs_lr_load4(R, R.pos);
 }
 // bits consumed so far
 static __device__ __forceinline__ uint64_t zs_lr_bitpos(const zs_lane_reader& R) {
@@ -1081,6 +1090,7 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   R.pos = 0;
   R.hold = 0;
   R.bits = 0;
+  R.pf = zs_lr_load4(R, 0);
   uint8_t* dst = out + out_off[s];
   const uint32_t cap = out_cap[s];
   uint32_t total = 0;
