@@ -243,13 +243,17 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       const uint32_t limit = p > ZS_MAX_DIST ? p - ZS_MAX_DIST : 0;         // deflate.ts:1060
       const uint32_t sp = p - w0;
       const uint32_t s0 = win_word(wb, sp), s1 = win_word(wb, sp + 4);
-      uint32_t best = 2, bq = 0, cnt = 0, best_s = 0, bq_s = 0;
+      // best = (len << 16) | (0x7fff - distance): its maximum is the first
+      // candidate among the longest -- "first strictly longer wins"
+      // (deflate.ts:1100-1105); starts at MIN_MATCH - 1 = 2
+      uint32_t best = (2u << 16) | 0x7fffu, best_s = 0;
       bool small_set = false;
       uint32_t cur = q0;
-      for (;;) {
+      // every candidate a lane evaluates is one chain step, and a lane leaves the
+      // loop at a nice match: the reference's chain counter is the step count
+      for (uint32_t step = 1;; step++) {
         const uint32_t cp = cur - w0;
-        // the chain link and the first 8 bytes (three aligned LDS words) are read
-        // together: one LDS round trip per candidate; longer matches fall to the loop
+        // the chain link and the first 8 bytes (three aligned LDS words) are read together
         const uint32_t d = pv[cp];
         const uint32_t wi = cp >> 2, sh = cp & 3u;
         const uint32_t a0 = wb[wi], a1 = wb[wi + 1], a2 = wb[wi + 2];
@@ -257,32 +261,31 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
         const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, sh) ^ s1;
         const uint64_t x = ((uint64_t)x1 << 32) | x0;
         uint32_t k = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
-        if (k == 8u) {
+        if (__builtin_expect(k == 8u, 0)) {  // longer than 8 bytes: finish the compare
           while (k < maxc) {
-            const uint32_t x = win_word(wb, cp + k) ^ win_word(wb, sp + k);
-            if (x) { k += (uint32_t)(__builtin_ctz(x) >> 3); break; }
+            const uint32_t y = win_word(wb, cp + k) ^ win_word(wb, sp + k);
+            if (y) { k += (uint32_t)(__builtin_ctz(y) >> 3); break; }
             k += 4;
           }
         }
         const uint32_t len = k < maxc ? k : maxc;
-        const bool improve = len > best;  // the first strictly longer match wins (deflate.ts:1100-1105)
-        best = improve ? len : best;
-        bq = improve ? cur : bq;
-        const bool nice_stop = improve && len >= nice;
-        cnt += nice_stop ? 0u : 1u;
-        const bool snap = !small_set && cnt == budget_small;
-        best_s = snap ? best : best_s;
-        bq_s = snap ? bq : bq_s;
-        small_set = small_set || snap;
+        best = max(best, (len << 16) | (0x7fffu - (p - cur)));
+        // while walking, best < nice: a candidate reaching nice ends the walk (deflate.ts:1103)
+        const bool nice_stop = len >= nice;
+        if (step == budget_small && !nice_stop) {  // chain >> 2 budget (deflate.ts:1075-1077)
+          best_s = best;
+          small_set = true;
+        }
         const uint32_t nxt = cur - d;
         // chain ends: nice match, budget spent, no link, or cur <= limit (deflate.ts:1109)
-        if (nice_stop || cnt >= budget || d == 0 || nxt <= limit) break;
+        if (nice_stop || step >= budget || d == 0 || nxt <= limit) break;
         cur = nxt;
       }
-      if (!small_set) { best_s = best; bq_s = bq; }
+      if (!small_set) best_s = best;
       const uint32_t flag = d0 == ZS_MAX_DIST ? 0x8000u : 0u;  // SURVEY A3 slide-NIL corner, resolved in parse
-      r.x = (best << 16) | (best > 2 ? p - bq : 0u) | flag;
-      r.y = (best_s << 16) | (best_s > 2 ? p - bq_s : 0u);
+      const uint32_t bl = best >> 16, bsl = best_s >> 16;
+      r.x = (bl << 16) | (bl > 2 ? 0x7fffu - (best & 0x7fffu) : 0u) | flag;
+      r.y = (bsl << 16) | (bsl > 2 ? 0x7fffu - (best_s & 0x7fffu) : 0u);
     }
     out[p] = r;
   }
