@@ -106,31 +106,40 @@ __global__ __launch_bounds__(64) void zs_k_depth(const uint32_t* __restrict__ in
   const uint16_t* pd = prevd + pos_base[s];
   uint8_t* dp = depth + pos_base[s];
   const int lane = (int)threadIdx.x;
-  for (uint32_t g0 = 0; g0 < n; g0 += 64) {
-    const uint32_t p = g0 + (uint32_t)lane;
-    const uint32_t d = p < n ? pd[p] : 0u;
-    // list ranking: link = lane of the previous position in this step, or -1
-    int link = -1;
-    uint32_t sum = 0;
-    if (d != 0) {
-      const uint32_t q = p - d;
-      if (q >= g0) { link = (int)(q - g0); sum = 1; }
-      else sum = (uint32_t)ring[q & 32767u] + 1u;
+  for (uint32_t b0 = 0; b0 < n; b0 += 256) {
+    uint32_t dd[4];  // four steps' links, loaded together
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t p = b0 + 64 * j + (uint32_t)lane;
+      dd[j] = p < n ? pd[p] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < 6; r++) {
-      const uint32_t ls = __shfl(sum, link < 0 ? lane : link, 64);
-      const int ll = __shfl(link, link < 0 ? lane : link, 64);
-      if (link >= 0) { sum += ls; link = ll; }
+    for (int j = 0; j < 4; j++) {
+      const uint32_t g0 = b0 + 64 * j;
+      const uint32_t p = g0 + (uint32_t)lane;
+      const uint32_t d = dd[j];
+      // list ranking: link = lane of the previous position in this step, or -1
+      int link = -1;
+      uint32_t sum = 0;
+      if (d != 0) {
+        const uint32_t q = p - d;
+        if (q >= g0) { link = (int)(q - g0); sum = 1; }
+        else sum = (uint32_t)ring[q & 32767u] + 1u;
+      }
+      while (__ballot(link >= 0)) {
+        const uint32_t ls = __shfl(sum, link < 0 ? lane : link, 64);
+        const int ll = __shfl(link, link < 0 ? lane : link, 64);
+        if (link >= 0) { sum += ls; link = ll; }
+      }
+      const uint32_t v = sum < 255u ? sum : 255u;
+      __builtin_amdgcn_wave_barrier();
+      if (p < n) {
+        ring[p & 32767u] = (uint8_t)v;
+        dp[p] = (uint8_t)v;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
     }
-    const uint32_t v = sum < 255u ? sum : 255u;
-    __builtin_amdgcn_wave_barrier();
-    if (p < n) {
-      ring[p & 32767u] = (uint8_t)v;
-      dp[p] = (uint8_t)v;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
