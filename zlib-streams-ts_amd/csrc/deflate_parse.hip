@@ -36,6 +36,7 @@
 #define ZS_FIX_SLOTS 1284u
 #define ZS_SEG_WORDS (ZS_SPEC_SLOTS + ZS_SYNC_SLOTS + ZS_FIX_SLOTS)
 #define ZS_NONE 0xffffffffu
+static_assert(ZS_SPEC_SLOTS % 4 == 0 && ZS_SEG_WORDS % 4 == 0, "16-byte aligned scratch regions");
 static_assert(ZS_SEG == ZS_PARSE_SEG && ZS_SEG_WORDS == ZS_PARSE_SEG_WORDS, "scratch layout shared with capi.cpp");
 
 struct zs_seg_info {
@@ -127,13 +128,33 @@ __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in,
       uint32_t* sync = spec + ZS_SPEC_SLOTS;
       zs_pstate st = {a, 0, ZS_MIN_MATCH - 1, 0};
       uint32_t cnt = 0, nsync = 0;
+      // Symbols and sync entries are gathered four at a time and stored as one
+      // 16-byte write: on gfx9 stores share vmcnt with loads, so a store in every
+      // iteration would make each match-table load wait for the previous stores.
+      uint4 sacc = make_uint4(0, 0, 0, 0), yacc = make_uint4(0, 0, 0, 0);
       while (st.p < b) {
         // sync key: (position - a) << 1 | match_available, with the symbol count
-        if (st.ml == ZS_MIN_MATCH - 1) sync[nsync++] = ((st.p - a) << 17) | (st.ma << 16) | cnt;
+        if (st.ml == ZS_MIN_MATCH - 1) {
+          const uint32_t y = ((st.p - a) << 17) | (st.ma << 16) | cnt, m = nsync & 3u;
+          yacc.x = m == 0 ? y : yacc.x;
+          yacc.y = m == 1 ? y : yacc.y;
+          yacc.z = m == 2 ? y : yacc.z;
+          yacc.w = m == 3 ? y : yacc.w;
+          if (++nsync % 4 == 0) *reinterpret_cast<uint4*>(sync + nsync - 4) = yacc;
+        }
         const uint32_t p = st.p;
         const uint32_t v = zs_parse_step(st, M[p], p > 0 ? src[p - 1] : 0u, n, good, lazy);
-        if (v != ZS_NONE) spec[cnt++] = v;
+        if (v != ZS_NONE) {
+          const uint32_t m = cnt & 3u;
+          sacc.x = m == 0 ? v : sacc.x;
+          sacc.y = m == 1 ? v : sacc.y;
+          sacc.z = m == 2 ? v : sacc.z;
+          sacc.w = m == 3 ? v : sacc.w;
+          if (++cnt % 4 == 0) *reinterpret_cast<uint4*>(spec + cnt - 4) = sacc;
+        }
       }
+      for (uint32_t i = nsync & ~3u; i < nsync; i++) sync[i] = (i & 3u) == 0 ? yacc.x : (i & 3u) == 1 ? yacc.y : yacc.z;
+      for (uint32_t i = cnt & ~3u; i < cnt; i++) spec[i] = (i & 3u) == 0 ? sacc.x : (i & 3u) == 1 ? sacc.y : sacc.z;
       sync[nsync] = ZS_NONE;
       if (b == n && st.ma) spec[cnt++] = src[n - 1];  // final deferred literal (deflate.ts:1429-1432)
       seg[lane].end = st.p;
