@@ -173,6 +173,7 @@ __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in,
         const uint32_t* sync = spec + ZS_SPEC_SLOTS;
         uint32_t* fix = scr + (size_t)j * ZS_SEG_WORDS + ZS_SPEC_SLOTS + ZS_SYNC_SLOTS;
         uint32_t nf = 0, from = ZS_NONE, si = 0, sv = sync[0];
+        uint4 facc = make_uint4(0, 0, 0, 0);
         seg[j].start = t.p - t.ma;  // a pending literal in[t.p - 1] opens the run
         while (t.p < b) {
           if (t.ml == ZS_MIN_MATCH - 1) {
@@ -182,8 +183,16 @@ __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in,
           }
           const uint32_t p = t.p;
           const uint32_t v = zs_parse_step(t, M[p], p > 0 ? src[p - 1] : 0u, n, good, lazy);
-          if (v != ZS_NONE) fix[nf++] = v;
+          if (v != ZS_NONE) {  // gathered four at a time (see pass A)
+            const uint32_t m = nf & 3u;
+            facc.x = m == 0 ? v : facc.x;
+            facc.y = m == 1 ? v : facc.y;
+            facc.z = m == 2 ? v : facc.z;
+            facc.w = m == 3 ? v : facc.w;
+            if (++nf % 4 == 0) *reinterpret_cast<uint4*>(fix + nf - 4) = facc;
+          }
         }
+        for (uint32_t i = nf & ~3u; i < nf; i++) fix[i] = (i & 3u) == 0 ? facc.x : (i & 3u) == 1 ? facc.y : facc.z;
         if (from != ZS_NONE) {  // continue from the speculative end state
           t.p = seg[j].end;
           t.ma = seg[j].ma;
@@ -207,17 +216,30 @@ __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in,
     }
     const uint32_t unchecked = final_lit ? total + round_total - 1 : ZS_NONE;  // global index of the final literal
 
-    // ---- pass C: splice and cut blocks
+    // ---- pass C: splice and cut blocks.  A segment's run is its catch-up
+    // symbols followed by its speculative symbols from the sync point; they are
+    // read four 64-symbol chunks at a time before any of them is stored (loads
+    // wait for earlier stores on gfx9).
     for (uint32_t j = 0; j < nr; j++) {
       const zs_seg_info si = seg[j];
       uint32_t pos = si.start;
       const uint32_t* base = scr + (size_t)j * ZS_SEG_WORDS;
-      for (int part = 0; part < 2; part++) {
-        const uint32_t* from = part == 0 ? base + ZS_SPEC_SLOTS + ZS_SYNC_SLOTS : base + si.from;
-        const uint32_t cnt = part == 0 ? si.nfix : (si.from == ZS_NONE ? 0u : si.nspec - si.from);
-        for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+      const uint32_t* fx = base + ZS_SPEC_SLOTS + ZS_SYNC_SLOTS;
+      const uint32_t* sp = base + (si.from == ZS_NONE ? 0u : si.from);
+      const uint32_t cnt = si.nfix + (si.from == ZS_NONE ? 0u : si.nspec - si.from);
+      for (uint32_t g0 = 0; g0 < cnt; g0 += 256) {
+        uint32_t vv[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t i = g0 + 64 * q + lane;
+          vv[q] = i < cnt ? (i < si.nfix ? fx[i] : sp[i - si.nfix]) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t c0 = g0 + 64 * q;
+          if (c0 >= cnt) break;
           const uint32_t i = c0 + lane;
-          const uint32_t v = i < cnt ? from[i] : 0u;
+          const uint32_t v = vv[q];
           const uint32_t len = i < cnt ? ((v & 0x80000000u) ? ((v >> 16) & 0xffu) + ZS_MIN_MATCH : 1u) : 0u;
           uint32_t x = len;  // inclusive scan of symbol lengths
 #pragma unroll
