@@ -86,10 +86,19 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
     __builtin_amdgcn_wave_barrier();
     return hh;
   };
+  // Symbols are held one per lane (lane nsym % 64) and stored 64 at a time: a
+  // store per symbol would make every following load wait for it (on gfx9
+  // stores share vmcnt with loads).
+  uint32_t sbuf = 0;
+  auto drain = [&]() {
+    const uint32_t k = nsym & 63u;
+    if (lane < k) sy[nsym - k + lane] = sbuf;
+  };
   auto emit = [&](uint32_t v) {
-    if (lane == 0) sy[nsym] = v;
+    sbuf = lane == (nsym & 63u) ? v : sbuf;
     nsym++;
     in_blk++;
+    if ((nsym & 63u) == 0) sy[nsym - 64 + lane] = sbuf;
   };
   auto close_block = [&](uint32_t end, uint32_t last) {
     if (lane == 0) {
@@ -169,6 +178,7 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
     if (in_blk == ZS_SYM_END) close_block(p, 0);
   }
   close_block(n, 1);
+  drain();
   if (lane == 0) {
     streams[s].nsym = nsym;
     streams[s].nblk = nflush;
