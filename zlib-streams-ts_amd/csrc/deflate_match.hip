@@ -255,42 +255,43 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       // best = (len << 16) | (0x7fff - distance): its maximum is the first
       // candidate among the longest -- "first strictly longer wins"
       // (deflate.ts:1100-1105); starts at MIN_MATCH - 1 = 2
-      uint32_t best = (2u << 16) | 0x7fffu, best_s = 0;
-      bool small_set = false;
+      uint32_t best = (2u << 16) | 0x7fffu;
       uint32_t cur = q0;
-      // every candidate a lane evaluates is one chain step, and a lane leaves the
-      // loop at a nice match: the reference's chain counter is the step count
-      for (uint32_t step = 1;; step++) {
-        const uint32_t cp = cur - w0;
-        // the chain link and the first 8 bytes (three aligned LDS words) are read together
-        const uint32_t d = pv[cp];
-        const uint32_t wi = cp >> 2, sh = cp & 3u;
-        const uint32_t a0 = wb[wi], a1 = wb[wi + 1], a2 = wb[wi + 2];
-        const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, sh) ^ s0;
-        const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, sh) ^ s1;
-        const uint64_t x = ((uint64_t)x1 << 32) | x0;
-        uint32_t k = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
-        if (__builtin_expect(k == 8u, 0)) {  // longer than 8 bytes: finish the compare
-          while (k < maxc) {
-            const uint32_t y = win_word(wb, cp + k) ^ win_word(wb, sp + k);
-            if (y) { k += (uint32_t)(__builtin_ctz(y) >> 3); break; }
-            k += 4;
+      // Every candidate a lane evaluates is one chain step, and a lane leaves at
+      // a nice match or the chain's end: the reference's chain counter is the
+      // step count.  The walk runs in two phases so that the chain >> 2 result
+      // (deflate.ts:1075-1077) is a snapshot between them, not a per-step test.
+      bool live = true;
+      auto walk = [&](uint32_t step, uint32_t bound) -> uint32_t {
+        for (;; step++) {
+          const uint32_t cp = cur - w0;
+          // the chain link and the first 8 bytes (three aligned LDS words) are read together
+          const uint32_t d = pv[cp];
+          const uint32_t wi = cp >> 2, sh = cp & 3u;
+          const uint32_t a0 = wb[wi], a1 = wb[wi + 1], a2 = wb[wi + 2];
+          const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, sh) ^ s0;
+          const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, sh) ^ s1;
+          const uint64_t x = ((uint64_t)x1 << 32) | x0;
+          uint32_t k = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
+          if (__builtin_expect(k == 8u, 0)) {  // longer than 8 bytes: finish the compare
+            while (k < maxc) {
+              const uint32_t y = win_word(wb, cp + k) ^ win_word(wb, sp + k);
+              if (y) { k += (uint32_t)(__builtin_ctz(y) >> 3); break; }
+              k += 4;
+            }
           }
+          const uint32_t len = k < maxc ? k : maxc;
+          best = max(best, (len << 16) | (0x7fffu - (p - cur)));
+          const uint32_t nxt = cur - d;
+          // ends: nice match (while walking best < nice, deflate.ts:1103), no link, or cur <= limit (deflate.ts:1109)
+          if (len >= nice || d == 0 || nxt <= limit) { live = false; return step; }
+          cur = nxt;
+          if (step >= bound) return step;  // budget reached: uniform across the live lanes
         }
-        const uint32_t len = k < maxc ? k : maxc;
-        best = max(best, (len << 16) | (0x7fffu - (p - cur)));
-        // while walking, best < nice: a candidate reaching nice ends the walk (deflate.ts:1103)
-        const bool nice_stop = len >= nice;
-        if (step == budget_small && !nice_stop) {  // chain >> 2 budget (deflate.ts:1075-1077)
-          best_s = best;
-          small_set = true;
-        }
-        const uint32_t nxt = cur - d;
-        // chain ends: nice match, budget spent, no link, or cur <= limit (deflate.ts:1109)
-        if (nice_stop || step >= budget || d == 0 || nxt <= limit) break;
-        cur = nxt;
-      }
-      if (!small_set) best_s = best;
+      };
+      uint32_t step = walk(1, budget_small);
+      const uint32_t best_s = best;  // lanes still walking: after chain >> 2 candidates; others: final
+      if (live && step < budget) walk(step + 1, budget);
       const uint32_t flag = d0 == ZS_MAX_DIST ? 0x8000u : 0u;  // SURVEY A3 slide-NIL corner, resolved in parse
       const uint32_t bl = best >> 16, bsl = best_s >> 16;
       r.x = (bl << 16) | (bl > 2 ? 0x7fffu - (best & 0x7fffu) : 0u) | flag;
