@@ -199,7 +199,12 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       wb[i] = v;
     }
   }
-  for (uint32_t i = threadIdx.x; i < t1 - w0; i += blockDim.x) pv[i] = pd[w0 + i];
+  // a missing link (0) is staged as 0xffff: the walk's `cur - d <= limit` test
+  // (signed) then also ends the chain, and a head distance > MAX_DIST is invalid
+  for (uint32_t i = threadIdx.x; i < t1 - w0; i += blockDim.x) {
+    const uint32_t d = pd[w0 + i];
+    pv[i] = (uint16_t)(d ? d : 0xffffu);
+  }
   // Deal positions to lanes by decreasing chain depth (a counting sort): the
   // 64 chains a wave walks in lock-step then have similar lengths, instead of
   // every wave waiting for its longest chain.
@@ -242,14 +247,15 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
   for (uint32_t oi = threadIdx.x; oi < t1 - t0; oi += blockDim.x) {
     const uint32_t p = t0 + order[oi];
     uint2 r = make_uint2(0, 0);
-    const uint32_t d0 = p + 2 < n ? pv[p - w0] : 0;
+    const uint32_t d0 = p + 2 < n ? pv[p - w0] : 0xffffu;
     const uint32_t q0 = p - d0;
     // head candidate: non-NIL, distance <= MAX_DIST (deflate.ts:1376)
-    if (d0 != 0 && q0 != 0 && d0 <= ZS_MAX_DIST) {
+    if (q0 != 0 && d0 <= ZS_MAX_DIST) {
       const uint32_t look = n - p;
       const uint32_t maxc = look < ZS_MAX_MATCH ? look : ZS_MAX_MATCH;       // deflate.ts:1068
       const uint32_t nice = look < (uint32_t)nice_cfg ? look : (uint32_t)nice_cfg;  // deflate.ts:1078-1080
-      const uint32_t limit = p > ZS_MAX_DIST ? p - ZS_MAX_DIST : 0;         // deflate.ts:1060
+      const int limit = p > ZS_MAX_DIST ? (int)(p - ZS_MAX_DIST) : 0;       // deflate.ts:1060
+      const uint32_t kbase = 0x7fffu - p;  // best key low half: 0x7fff - distance = cur + kbase
       const uint32_t sp = p - w0;
       const uint32_t s0 = win_word(wb, sp), s1 = win_word(wb, sp + 4);
       // best = (len << 16) | (0x7fff - distance): its maximum is the first
@@ -281,11 +287,11 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
             }
           }
           const uint32_t len = k < maxc ? k : maxc;
-          best = max(best, (len << 16) | (0x7fffu - (p - cur)));
-          const uint32_t nxt = cur - d;
-          // ends: nice match (while walking best < nice, deflate.ts:1103), no link, or cur <= limit (deflate.ts:1109)
-          if (len >= nice || d == 0 || nxt <= limit) { live = false; return step; }
-          cur = nxt;
+          best = max(best, (len << 16) | (cur + kbase));
+          const int nxt = (int)cur - (int)d;
+          // ends: nice match (while walking best < nice, deflate.ts:1103), or no link / cur <= limit (deflate.ts:1109)
+          if (len >= nice || nxt <= limit) { live = false; return step; }
+          cur = (uint32_t)nxt;
           if (step >= bound) return step;  // budget reached: uniform across the live lanes
         }
       };
