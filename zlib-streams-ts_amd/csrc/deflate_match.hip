@@ -254,15 +254,16 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       const uint32_t look = n - p;
       const uint32_t maxc = look < ZS_MAX_MATCH ? look : ZS_MAX_MATCH;       // deflate.ts:1068
       const uint32_t nice = look < (uint32_t)nice_cfg ? look : (uint32_t)nice_cfg;  // deflate.ts:1078-1080
-      const int limit = p > ZS_MAX_DIST ? (int)(p - ZS_MAX_DIST) : 0;       // deflate.ts:1060
-      const uint32_t kbase = 0x7fffu - p;  // best key low half: 0x7fff - distance = cur + kbase
+      // the walk runs in window coordinates (cr = cur - w0)
+      const int limit = (p > ZS_MAX_DIST ? (int)(p - ZS_MAX_DIST) : 0) - (int)w0;  // deflate.ts:1060
+      const uint32_t kbase = 0x7fffu - p + w0;  // best key low half: 0x7fff - distance = cr + kbase
       const uint32_t sp = p - w0;
       const uint32_t s0 = win_word(wb, sp), s1 = win_word(wb, sp + 4);
       // best = (len << 16) | (0x7fff - distance): its maximum is the first
       // candidate among the longest -- "first strictly longer wins"
       // (deflate.ts:1100-1105); starts at MIN_MATCH - 1 = 2
       uint32_t best = (2u << 16) | 0x7fffu;
-      uint32_t cur = q0;
+      uint32_t cr = q0 - w0;
       // Every candidate a lane evaluates is one chain step, and a lane leaves at
       // a nice match or the chain's end: the reference's chain counter is the
       // step count.  The walk runs in two phases so that the chain >> 2 result
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       bool live = true;
       auto walk = [&](uint32_t step, uint32_t bound) -> uint32_t {
         for (;; step++) {
-          const uint32_t cp = cur - w0;
+          const uint32_t cp = cr;
           // the chain link and the first 8 bytes (three aligned LDS words) are read together
           const uint32_t d = pv[cp];
           const uint32_t wi = cp >> 2, sh = cp & 3u;
@@ -287,11 +288,11 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
             }
           }
           const uint32_t len = k < maxc ? k : maxc;
-          best = max(best, (len << 16) | (cur + kbase));
-          const int nxt = (int)cur - (int)d;
+          best = max(best, (len << 16) | (cr + kbase));
+          const int nxt = (int)cr - (int)d;
           // ends: nice match (while walking best < nice, deflate.ts:1103), or no link / cur <= limit (deflate.ts:1109)
           if (len >= nice || nxt <= limit) { live = false; return step; }
-          cur = (uint32_t)nxt;
+          cr = (uint32_t)nxt;
           if (step >= bound) return step;  // budget reached: uniform across the live lanes
         }
       };
