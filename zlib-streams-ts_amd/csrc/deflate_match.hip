@@ -268,7 +268,7 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       // a nice match or the chain's end: the reference's chain counter is the
       // step count.  The walk runs in two phases so that the chain >> 2 result
       // (deflate.ts:1075-1077) is a snapshot between them, not a per-step test.
-      bool live = true;
+      uint32_t alive = 1;  // a 32-bit value, not a bool: keeps the loop's live-out state in a VGPR
       auto walk = [&](uint32_t step, uint32_t bound) -> uint32_t {
         for (;; step++) {
           const uint32_t cp = cr;
@@ -291,14 +291,14 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
           best = max(best, (len << 16) | (cr + kbase));
           const int nxt = (int)cr - (int)d;
           // ends: nice match (while walking best < nice, deflate.ts:1103), or no link / cur <= limit (deflate.ts:1109)
-          if (len >= nice || nxt <= limit) { live = false; return step; }
+          alive = (len < nice && nxt > limit) ? 1u : 0u;
           cr = (uint32_t)nxt;
-          if (step >= bound) return step;  // budget reached: uniform across the live lanes
+          if (!alive || step >= bound) return step;
         }
       };
       uint32_t step = walk(1, budget_small);
       const uint32_t best_s = best;  // lanes still walking: after chain >> 2 candidates; others: final
-      if (live && step < budget) walk(step + 1, budget);
+      if (alive && step < budget) walk(step + 1, budget);
       const uint32_t flag = d0 == ZS_MAX_DIST ? 0x8000u : 0u;  // SURVEY A3 slide-NIL corner, resolved in parse
       const uint32_t bl = best >> 16, bsl = best_s >> 16;
       r.x = (bl << 16) | (bl > 2 ? 0x7fffu - (best & 0x7fffu) : 0u) | flag;
