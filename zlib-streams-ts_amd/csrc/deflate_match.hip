@@ -268,9 +268,11 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       // a nice match or the chain's end: the reference's chain counter is the
       // step count.  The walk runs in two phases so that the chain >> 2 result
       // (deflate.ts:1075-1077) is a snapshot between them, not a per-step test.
-      uint32_t alive = 1;  // a 32-bit value, not a bool: keeps the loop's live-out state in a VGPR
-      auto walk = [&](uint32_t step, uint32_t bound) -> uint32_t {
-        for (;; step++) {
+      auto walk = [&](uint32_t rem) {
+        // the step budget is counted down in a VGPR (the asm hides that it is
+        // uniform): its test then joins the per-lane exit mask in one v_cmp
+        asm volatile("v_mov_b32 %0, %1" : "=v"(rem) : "s"(rem));
+        for (;;) {
           const uint32_t cp = cr;
           // the chain link and the first 8 bytes (three aligned LDS words) are read together
           const uint32_t d = pv[cp];
@@ -291,14 +293,18 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
           best = max(best, (len << 16) | (cr + kbase));
           const int nxt = (int)cr - (int)d;
           // ends: nice match (while walking best < nice, deflate.ts:1103), or no link / cur <= limit (deflate.ts:1109)
-          alive = (len < nice && nxt > limit) ? 1u : 0u;
           cr = (uint32_t)nxt;
-          if (!alive || step >= bound) return step;
+          if ((len >= nice) | (nxt <= limit) | (--rem == 0)) return;
         }
       };
-      uint32_t step = walk(1, budget_small);
+      // A lane leaving the first phase early has ended its chain; the others all
+      // stand at step chain >> 2, so the second phase starts at a uniform step and
+      // whether a lane goes on is recomputed from (cr, best) -- no loop live-out
+      // state beyond them.
+      walk(budget_small);
       const uint32_t best_s = best;  // lanes still walking: after chain >> 2 candidates; others: final
-      if (alive && step < budget) walk(step + 1, budget);
+      asm volatile("" : "+v"(cr));  // recompute the chain-end test below instead of keeping a mask live
+      if (budget_small < budget && (int)cr > limit && (best >> 16) < nice) walk(budget - budget_small);
       const uint32_t flag = d0 == ZS_MAX_DIST ? 0x8000u : 0u;  // SURVEY A3 slide-NIL corner, resolved in parse
       const uint32_t bl = best >> 16, bsl = best_s >> 16;
       r.x = (bl << 16) | (bl > 2 ? 0x7fffu - (best & 0x7fffu) : 0u) | flag;
