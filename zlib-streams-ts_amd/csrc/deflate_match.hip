@@ -164,6 +164,7 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
   __shared__ uint16_t pv[ZS_LOOKBACK + ZS_TILE];
   __shared__ uint16_t order[ZS_TILE];  // tile positions, longest expected chains first
   __shared__ uint32_t bins[256];
+  __shared__ uint32_t next;  // work queue over order[]: the next unclaimed group of 64
   const int s = blockIdx.y;
   const uint32_t n = in_len[s];
   const uint32_t t0 = blockIdx.x * ZS_TILE;
@@ -211,6 +212,7 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
   const uint32_t cap = (uint32_t)chain < 255u ? (uint32_t)chain : 255u;
   const uint8_t* dp = depth + pos_base[s];
   if (threadIdx.x < 256) bins[threadIdx.x] = 0;
+  if (threadIdx.x == 0) next = 0;
   __syncthreads();
   uint32_t key[ZS_TILE / 1024];
 #pragma unroll
@@ -244,7 +246,18 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
 
   const uint32_t budget = (uint32_t)chain, budget_small = (uint32_t)chain >> 2;
   uint2* out = mres + pos_base[s];
-  for (uint32_t oi = threadIdx.x; oi < t1 - t0; oi += blockDim.x) {
+  // Waves claim groups of 64 sorted positions from a queue, longest chains
+  // first: a wave that drew short chains takes more groups, so the 16 waves end
+  // together (a static deal leaves the CU idle while the wave holding the
+  // longest chains of every round finishes).
+  const uint32_t lane = threadIdx.x & 63u;
+  for (;;) {
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(&next, 64u);
+    g = __builtin_amdgcn_readfirstlane(g);
+    if (g >= t1 - t0) break;
+    const uint32_t oi = g + lane;
+    if (oi >= t1 - t0) break;
     const uint32_t p = t0 + order[oi];
     uint2 r = make_uint2(0, 0);
     const uint32_t d0 = p + 2 < n ? pv[p - w0] : 0xffffu;
