@@ -64,7 +64,7 @@ struct zs_ctx {
   hipStream_t stream = nullptr;
   bool timing = false;
   // workspace
-  Buf meta, prevd, depth, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
+  Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
   bool inflate_fast = true;
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res;
@@ -160,7 +160,7 @@ void zs_ctx_destroy(zs_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (Buf* b : {&c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->depth, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
+  for (Buf* b : {&c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
                  &c->istate, &c->d_in, &c->d_out, &c->d_res})
     if (b->p) (void)hipFree(b->p);
   (void)hipStreamDestroy(c->stream);
@@ -261,7 +261,6 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   }
   HIPCHK(c->meta.ensure(ml.bytes));
   HIPCHK(c->prevd.ensure(2 * P + 64));
-  if (level >= 4) HIPCHK(c->depth.ensure(P + 64));
   HIPCHK(c->mres.ensure(8 * P + 64));
   HIPCHK(c->syms.ensure(4 * (P + n) + 64));
   if (level >= 4) HIPCHK(c->pscr.ensure(4ull * ZS_PARSE_SEG_WORDS * (P / ZS_PARSE_SEG + n + 1)));
@@ -292,11 +291,9 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   if (level >= 4) {
     zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
     mark(c, st, "prev");
-    zs_k_depth<<<n, 64, 0, st>>>(d_in_len, d_pos, c->prevd.as<uint16_t>(), c->depth.as<uint8_t>());
-    mark(c, st, "depth");
     dim3 g((max_len + 8191) / 8192, n);
     if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
-                                                 c->depth.as<uint8_t>(), c->mres.as<uint2>(), cfg.chain, cfg.nice);
+                                                 c->mres.as<uint2>(), cfg.chain, cfg.nice);
     mark(c, st, "match");
     zs_k_parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), c->syms.as<uint32_t>(),
                                  d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);

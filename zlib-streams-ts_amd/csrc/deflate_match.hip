@@ -91,58 +91,6 @@ __global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, 
   }
 }
 
-// --------------------------------------------------------------- zs_k_depth
-// Chain depth of every position: the number of links of its chain of
-// prevd[] links (capped at 255), depth(p) = depth(p - prevd[p]) + 1.  It only
-// orders the work of zs_k_match (positions with similar chain lengths share a
-// wave), never its results.  One wave per stream, 64 positions per step; links
-// inside the step are resolved by pointer jumping, earlier ones from an LDS ring.
-__global__ __launch_bounds__(64) void zs_k_depth(const uint32_t* __restrict__ in_len,
-                                                 const uint64_t* __restrict__ pos_base,
-                                                 const uint16_t* __restrict__ prevd, uint8_t* __restrict__ depth) {
-  __shared__ uint8_t ring[32768];
-  const int s = blockIdx.x;
-  const uint32_t n = in_len[s];
-  const uint16_t* pd = prevd + pos_base[s];
-  uint8_t* dp = depth + pos_base[s];
-  const int lane = (int)threadIdx.x;
-  for (uint32_t b0 = 0; b0 < n; b0 += 256) {
-    uint32_t dd[4];  // four steps' links, loaded together
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t p = b0 + 64 * j + (uint32_t)lane;
-      dd[j] = p < n ? pd[p] : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t g0 = b0 + 64 * j;
-      const uint32_t p = g0 + (uint32_t)lane;
-      const uint32_t d = dd[j];
-      // list ranking: link = lane of the previous position in this step, or -1
-      int link = -1;
-      uint32_t sum = 0;
-      if (d != 0) {
-        const uint32_t q = p - d;
-        if (q >= g0) { link = (int)(q - g0); sum = 1; }
-        else sum = (uint32_t)ring[q & 32767u] + 1u;
-      }
-      while (__ballot(link >= 0)) {
-        const uint32_t ls = __shfl(sum, link < 0 ? lane : link, 64);
-        const int ll = __shfl(link, link < 0 ? lane : link, 64);
-        if (link >= 0) { sum += ls; link = ll; }
-      }
-      const uint32_t v = sum < 255u ? sum : 255u;
-      __builtin_amdgcn_wave_barrier();
-      if (p < n) {
-        ring[p & 32767u] = (uint8_t)v;
-        dp[p] = (uint8_t)v;
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-}
-
 // --------------------------------------------------------------- zs_k_match
 #define ZS_TILE 8192u
 #define ZS_LOOKBACK 32768u
@@ -157,11 +105,13 @@ static __device__ __forceinline__ uint32_t win_word(const uint32_t* wb, uint32_t
 __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                    const uint32_t* __restrict__ in_len,
                                                    const uint64_t* __restrict__ pos_base,
-                                                   const uint16_t* __restrict__ prevd,
-                                                   const uint8_t* __restrict__ depth, uint2* __restrict__ mres,
+                                                   const uint16_t* __restrict__ prevd, uint2* __restrict__ mres,
                                                    int chain, int nice_cfg) {
   __shared__ uint32_t wb[ZS_WIN_WORDS + 2];
-  __shared__ uint16_t pv[ZS_LOOKBACK + ZS_TILE];
+  // chain links of [w0, t1); before they are staged the same LDS holds a
+  // 32768-bucket u16 histogram of the window's hashes (the ordering key below)
+  __shared__ uint32_t pvw[(ZS_LOOKBACK + ZS_TILE) / 2];
+  uint16_t* const pv = (uint16_t*)pvw;
   __shared__ uint16_t order[ZS_TILE];  // tile positions, longest expected chains first
   __shared__ uint32_t bins[256];
   __shared__ uint32_t next;  // work queue over order[]: the next unclaimed group of 64
@@ -200,25 +150,36 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       wb[i] = v;
     }
   }
-  // a missing link (0) is staged as 0xffff: the walk's `cur - d <= limit` test
-  // (signed) then also ends the chain, and a head distance > MAX_DIST is invalid
-  for (uint32_t i = threadIdx.x; i < t1 - w0; i += blockDim.x) {
-    const uint32_t d = pd[w0 + i];
-    pv[i] = (uint16_t)(d ? d : 0xffffu);
-  }
-  // Deal positions to lanes by decreasing chain depth (a counting sort): the
-  // 64 chains a wave walks in lock-step then have similar lengths, instead of
-  // every wave waiting for its longest chain.
-  const uint32_t cap = (uint32_t)chain < 255u ? (uint32_t)chain : 255u;
-  const uint8_t* dp = depth + pos_base[s];
+  // Deal positions to lanes by decreasing expected chain length (a counting
+  // sort): the 64 chains a wave walks in lock-step then have similar lengths,
+  // instead of every wave waiting for its longest chain.  A chain holds the
+  // earlier positions with the same hash, so the key is how often the
+  // position's hash occurs in the window [w0, t1) -- a u16 histogram built in
+  // the LDS the links are staged into afterwards.  The key only orders the
+  // work, never changes a result.
+  for (uint32_t i = threadIdx.x; i < (ZS_LOOKBACK + ZS_TILE) / 2; i += blockDim.x) pvw[i] = 0;
   if (threadIdx.x < 256) bins[threadIdx.x] = 0;
   if (threadIdx.x == 0) next = 0;
   __syncthreads();
+  const uint32_t hend = min(t1, n > 2 ? n - 2 : 0u);  // positions <= n-3 are inserted (deflate.ts:1367-1370)
+  for (uint32_t q = w0 + threadIdx.x; q < hend; q += blockDim.x) {
+    const uint32_t w = win_word(wb, q - w0);
+    const uint32_t h = (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
+    atomicAdd(&pvw[h >> 1], 1u << (16 * (h & 1u)));
+  }
+  __syncthreads();
+  const uint32_t cap = (uint32_t)chain < 255u ? (uint32_t)chain : 255u;
   uint32_t key[ZS_TILE / 1024];
 #pragma unroll
   for (uint32_t i = 0; i < ZS_TILE / 1024; i++) {
     const uint32_t p = t0 + threadIdx.x + 1024 * i;
-    key[i] = p < t1 ? 255u - min((uint32_t)dp[p], cap) : 0u;
+    uint32_t c = 0;
+    if (p < hend) {
+      const uint32_t w = win_word(wb, p - w0);
+      const uint32_t h = (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
+      c = (pvw[h >> 1] >> (16 * (h & 1u))) & 0xffffu;
+    }
+    key[i] = p < t1 ? 255u - min(c, cap) : 0u;
     if (p < t1) atomicAdd(&bins[key[i]], 1u);
   }
   __syncthreads();
@@ -241,6 +202,12 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
   for (uint32_t i = 0; i < ZS_TILE / 1024; i++) {
     const uint32_t o = threadIdx.x + 1024 * i;
     if (t0 + o < t1) order[atomicAdd(&bins[key[i]], 1u)] = (uint16_t)o;
+  }
+  // a missing link (0) is staged as 0xffff: the walk's `cur - d <= limit` test
+  // (signed) then also ends the chain, and a head distance > MAX_DIST is invalid
+  for (uint32_t i = threadIdx.x; i < t1 - w0; i += blockDim.x) {
+    const uint32_t d = pd[w0 + i];
+    pv[i] = (uint16_t)(d ? d : 0xffffu);
   }
   __syncthreads();
 

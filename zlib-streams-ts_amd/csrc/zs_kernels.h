@@ -33,8 +33,7 @@ struct zs_stream {
 __global__ void zs_k_prev(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           uint16_t* prevd);
 __global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                           const uint16_t* prevd, const uint8_t* depth, uint2* mres, int chain, int nice);
-__global__ void zs_k_depth(const uint32_t* in_len, const uint64_t* pos_base, const uint16_t* prevd, uint8_t* depth);
+                           const uint16_t* prevd, uint2* mres, int chain, int nice);
 __global__ void zs_k_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint32_t* blk_base, const uint2* mres, uint32_t* syms, zs_block* blocks,
                            zs_stream* streams, uint32_t* scratch, int good, int lazy);
