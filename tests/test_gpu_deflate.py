@@ -38,7 +38,7 @@ def test_random_inputs_vs_oracle(engine, level):
     rng = random.Random(1000 + level)
     inputs = []
     for k in range(24):
-        n = rng.choice([0, 1, 2, 3, 4, 257, 258, 259, 1000, 4095, 32768, 32769, 65535, 65536, 70001,
+        n = rng.choice([0, 1, 2, 3, 4, 257, 258, 259, 1000, 4095, 32768, 32769, 65535, 65536, 65537, 65538, 70001,
                         rng.randrange(1, 140000)])
         kind = rng.choice(["text", "mixed", "rand", "zeros", "ramp"])
         spec = {"kind": kind, "n": n, "seed": rng.randrange(1 << 32)}

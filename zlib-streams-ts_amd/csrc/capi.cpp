@@ -289,7 +289,9 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
     mark(c, st, "checksum");
   }
   if (level >= 4) {
-    zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+    // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
+    zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+    if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
     mark(c, st, "prev");
     dim3 g((max_len + 8191) / 8192, n);
     if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),

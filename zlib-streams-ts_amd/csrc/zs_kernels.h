@@ -32,6 +32,8 @@ struct zs_stream {
 
 __global__ void zs_k_prev(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           uint16_t* prevd);
+__global__ void zs_k_prev16(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                            uint16_t* prevd);
 __global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint16_t* prevd, uint2* mres, int chain, int nice);
 __global__ void zs_k_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
