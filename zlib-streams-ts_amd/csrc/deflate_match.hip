@@ -176,6 +176,11 @@ __global__ __launch_bounds__(64) void zs_k_prev16(const uint8_t* __restrict__ in
 #define ZS_LOOKBACK 32768u
 #define ZS_WIN_BYTES (ZS_LOOKBACK + ZS_TILE + 272u)  // + MAX_MATCH + slack for 4-byte reads
 #define ZS_WIN_WORDS (ZS_WIN_BYTES / 4)
+#define ZS_M_PV ((ZS_WIN_WORDS + 2 + 3) & ~3u)                 // word offsets in zs_k_match's LDS
+#define ZS_M_ORDER (ZS_M_PV + (ZS_LOOKBACK + ZS_TILE) / 2)
+#define ZS_M_BINS (ZS_M_ORDER + ZS_TILE / 2)
+#define ZS_M_WORDS (ZS_M_BINS + 256 + 4)
+static_assert(4 * ZS_M_PV < 65536, "link base must fit a DS offset");
 
 static __device__ __forceinline__ uint32_t win_word(const uint32_t* wb, uint32_t off) {
   const uint32_t i = off >> 2;
@@ -187,14 +192,20 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
                                                    const uint64_t* __restrict__ pos_base,
                                                    const uint16_t* __restrict__ prevd, uint2* __restrict__ mres,
                                                    int chain, int nice_cfg) {
-  __shared__ uint32_t wb[ZS_WIN_WORDS + 2];
-  // chain links of [w0, t1); before they are staged the same LDS holds a
-  // 32768-bucket u16 histogram of the window's hashes (the ordering key below)
-  __shared__ uint32_t pvw[(ZS_LOOKBACK + ZS_TILE) / 2];
+  // One LDS array, carved by hand so the window sits at address 0 and the
+  // links at a constant below 64 KiB: the walk's LDS reads then need no base
+  // add (the link base rides in the instruction's offset field).
+  //   wb    window bytes [w0, w1), zero padded
+  //   pv    chain links of [w0, t1); before they are staged the same LDS holds
+  //         a 32768-bucket u16 histogram of the window's hashes (ordering key)
+  //   order tile positions, longest expected chains first
+  __shared__ __attribute__((aligned(16))) uint32_t lds[ZS_M_WORDS];
+  uint32_t* const wb = lds;
+  uint32_t* const pvw = lds + ZS_M_PV;
   uint16_t* const pv = (uint16_t*)pvw;
-  __shared__ uint16_t order[ZS_TILE];  // tile positions, longest expected chains first
-  __shared__ uint32_t bins[256];
-  __shared__ uint32_t next;  // work queue over order[]: the next unclaimed group of 64
+  uint16_t* const order = (uint16_t*)(lds + ZS_M_ORDER);
+  uint32_t* const bins = lds + ZS_M_BINS;
+  uint32_t& next = lds[ZS_M_BINS + 256];  // work queue over order[]: the next unclaimed group of 64
   const int s = blockIdx.y;
   const uint32_t n = in_len[s];
   const uint32_t t0 = blockIdx.x * ZS_TILE;
@@ -316,14 +327,18 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
       const uint32_t nice = look < (uint32_t)nice_cfg ? look : (uint32_t)nice_cfg;  // deflate.ts:1078-1080
       // the walk runs in window coordinates (cr = cur - w0)
       const int limit = (p > ZS_MAX_DIST ? (int)(p - ZS_MAX_DIST) : 0) - (int)w0;  // deflate.ts:1060
-      const uint32_t kbase = 0x7fffu - p + w0;  // best key low half: 0x7fff - distance = cr + kbase
       const uint32_t sp = p - w0;
       const uint32_t s0 = win_word(wb, sp), s1 = win_word(wb, sp + 4);
-      // best = (len << 16) | (0x7fff - distance): its maximum is the first
-      // candidate among the longest -- "first strictly longer wins"
-      // (deflate.ts:1100-1105); starts at MIN_MATCH - 1 = 2
-      uint32_t best = (2u << 16) | 0x7fffu;
+      // best = (len << 16) | cr: its maximum is the first candidate among the
+      // longest, as the walk visits cr in decreasing order -- "first strictly
+      // longer wins" (deflate.ts:1100-1105); starts at MIN_MATCH - 1 = 2
+      uint32_t best = (2u << 16) | 0xffffu;
       uint32_t cr = q0 - w0;
+      // The 8-byte compare gives k = min(matched bytes, 8).  Below kx = min(nice,
+      // 8) the candidate is final (k < nice <= maxc, no clamp); at k >= kx it
+      // goes to the rare path that extends the compare, clamps to maxc and tests
+      // nice (nice >= 8 unless the stream ends within 8 bytes).
+      const uint32_t kx = nice < 8u ? nice : 8u;
       // Every candidate a lane evaluates is one chain step, and a lane leaves at
       // a nice match or the chain's end: the reference's chain counter is the
       // step count.  The walk runs in two phases so that the chain >> 2 result
@@ -335,40 +350,46 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
         for (;;) {
           const uint32_t cp = cr;
           // the chain link and the first 8 bytes (three aligned LDS words) are read together
-          const uint32_t d = pv[cp];
-          const uint32_t wi = cp >> 2, sh = cp & 3u;
+          uint32_t d = pv[cp];
+          const uint32_t wi = cp >> 2;
           const uint32_t a0 = wb[wi], a1 = wb[wi + 1], a2 = wb[wi + 2];
-          const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, sh) ^ s0;
-          const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, sh) ^ s1;
-          const uint64_t x = ((uint64_t)x1 << 32) | x0;
-          uint32_t k = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
-          if (__builtin_expect(k == 8u, 0)) {  // longer than 8 bytes: finish the compare
-            while (k < maxc) {
-              const uint32_t y = win_word(wb, cp + k) ^ win_word(wb, sp + k);
-              if (y) { k += (uint32_t)(__builtin_ctz(y) >> 3); break; }
-              k += 4;
+          const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, cp) ^ s0;  // alignbyte uses cp & 3
+          const uint32_t x1 = __builtin_amdgcn_alignbyte(a2, a1, cp) ^ s1;
+          // first differing bit, 64 if none (ffbl(0) = ~0, and the clamped add keeps it there)
+          uint32_t f0, f1;
+          asm("v_ffbl_b32 %0, %1" : "=v"(f0) : "v"(x0));
+          asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e64 %0, %0, 32 clamp" : "=&v"(f1) : "v"(x1));
+          uint32_t k = min(min(f0, f1), 64u) >> 3;
+          if (__builtin_expect(k >= kx, 0)) {
+            if (k == 8u) {  // longer than 8 bytes: finish the compare
+              while (k < maxc) {
+                const uint32_t y = win_word(wb, cp + k) ^ win_word(wb, sp + k);
+                if (y) { k += (uint32_t)(__builtin_ctz(y) >> 3); break; }
+                k += 4;
+              }
             }
+            k = k < maxc ? k : maxc;
+            if (k >= nice) d = 0xffffu;  // nice match (deflate.ts:1103): end the chain like a missing link
           }
-          const uint32_t len = k < maxc ? k : maxc;
-          best = max(best, (len << 16) | (cr + kbase));
+          best = max(best, (k << 16) | cr);
           const int nxt = (int)cr - (int)d;
-          // ends: nice match (while walking best < nice, deflate.ts:1103), or no link / cur <= limit (deflate.ts:1109)
           cr = (uint32_t)nxt;
-          if ((len >= nice) | (nxt <= limit) | (--rem == 0)) return;
+          // ends: no link / cur <= limit (deflate.ts:1109), or the budget
+          if ((nxt <= limit) | (--rem == 0)) return;
         }
       };
       // A lane leaving the first phase early has ended its chain; the others all
       // stand at step chain >> 2, so the second phase starts at a uniform step and
-      // whether a lane goes on is recomputed from (cr, best) -- no loop live-out
-      // state beyond them.
+      // whether a lane goes on is recomputed from cr -- no loop live-out state
+      // beyond it.
       walk(budget_small);
       const uint32_t best_s = best;  // lanes still walking: after chain >> 2 candidates; others: final
       asm volatile("" : "+v"(cr));  // recompute the chain-end test below instead of keeping a mask live
-      if (budget_small < budget && (int)cr > limit && (best >> 16) < nice) walk(budget - budget_small);
+      if (budget_small < budget && (int)cr > limit) walk(budget - budget_small);
       const uint32_t flag = d0 == ZS_MAX_DIST ? 0x8000u : 0u;  // SURVEY A3 slide-NIL corner, resolved in parse
       const uint32_t bl = best >> 16, bsl = best_s >> 16;
-      r.x = (bl << 16) | (bl > 2 ? 0x7fffu - (best & 0x7fffu) : 0u) | flag;
-      r.y = (bsl << 16) | (bsl > 2 ? 0x7fffu - (best_s & 0x7fffu) : 0u);
+      r.x = (bl << 16) | (bl > 2 ? sp - (best & 0xffffu) : 0u) | flag;
+      r.y = (bsl << 16) | (bsl > 2 ? sp - (best_s & 0xffffu) : 0u);
     }
     out[p] = r;
   }
