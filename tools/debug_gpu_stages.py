@@ -17,7 +17,7 @@ for name, d, level in [("zeros", bytes(65536), 6), ("ramp", bytes(j % 251 for j 
                        ("text", corpus.text(corpus.stream_seed(0), 65536), 6)]:
     eng.compress_batch_raw([d], "deflate-raw", level)
     n = len(d)
-    prevd = struct.unpack("<%dH" % n, fetch(0, 0, 2 * n))
+    prevd = [0 if v == 0xffff else v for v in struct.unpack("<%dH" % n, fetch(0, 0, 2 * n))]  # 0xffff = no link
     m = struct.unpack("<%dI" % (2 * n), fetch(1, 0, 8 * n))
     st = fetch(4, 0, 64)
     nsym, nblk = struct.unpack_from("<II", st, 0)

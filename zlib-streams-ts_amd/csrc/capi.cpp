@@ -253,7 +253,7 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
     if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
     pos_base[i] = P;
     blk_base[i] = B;
-    P += in_len[i];
+    P += ((uint64_t)in_len[i] + 7) & ~7ull;  // per-position tables start 8-aligned (16-B link loads in zs_k_match)
     const uint32_t nb = in_len[i] / ZS_SYM_END + 2;
     B += nb;
     max_len = std::max(max_len, in_len[i]);
@@ -473,7 +473,7 @@ extern "C" void zs_corpus(int kind, uint32_t first, uint32_t n_streams, uint32_t
 
 // ------------------------------------------------------------ introspection
 // Copies an intermediate array of stream `s` of the last deflate batch to host
-// memory: what = 0 prevd (u16/position), 1 match table (u32x2/position),
+// memory: what = 0 prevd (u16/position, 0xffff = no link), 1 match table (u32x2/position),
 // 2 symbols (u32 each; count = streams[s].nsym), 3 blocks (zs_block each),
 // 4 stream record (zs_stream).  Returns the number of bytes copied.
 extern "C" uint64_t zs_debug_fetch(zs_ctx* c, int what, uint32_t s, void* dst, uint64_t cap) {

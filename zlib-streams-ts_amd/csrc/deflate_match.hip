@@ -86,7 +86,7 @@ __global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, 
         const uint32_t p = g0 + 64 * j + lane;
         if (p < c1) {
           const uint32_t d = e[j] ? p - (e[j] - 1) : 0u;
-          out[p] = (uint16_t)(valid[j] && d <= 32767u ? d : 0u);
+          out[p] = (uint16_t)(valid[j] && d != 0u && d <= 32767u ? d : 0xffffu);
         }
       }
     }
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(64) void zs_k_prev16(const uint8_t* __restrict__ in
         if (p < c1) {
           const uint32_t q1 = (e[j] >> sh[j]) & 0xffffu;  // previous position + 1, 0 = none
           const uint32_t d = q1 ? p + 1 - q1 : 0u;
-          out[p] = (uint16_t)(m[j] && d <= 32767u ? d : 0u);
+          out[p] = (uint16_t)(m[j] && d != 0u && d <= 32767u ? d : 0xffffu);
         }
       }
     }
@@ -215,21 +215,50 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
   const uint32_t w1 = min(n, t1 + ZS_MAX_MATCH + 4);
   const uint8_t* src = in + in_off[s];
   const uint16_t* pd = prevd + pos_base[s];
-  // stage window bytes [w0, w1) (zero padded) and chain links [w0, t1)
-  const uint32_t nwords = (w1 - w0 + 3) / 4 + 2;
-  if ((((uintptr_t)(src + w0)) & 3u) == 0) {
-    const uint32_t* s32 = (const uint32_t*)(src + w0);
-    const uint32_t full = (w1 - w0) / 4;
-    for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) {
-      uint32_t v = 0;
-      if (i < full) v = s32[i];
+  // Staging.  All global loads are issued up front, 16 B per load: the links
+  // of [w0, t1) (pos_base and w0 are multiples of 8, so 16-B aligned) go to
+  // registers and are written to LDS only after the ordering phase below, which
+  // uses the same LDS; the window bytes [w0, w1) go to LDS now.  (Bytes past w1
+  // are never used by a result: every compare is clamped to maxc <= n - p.)
+  const uint32_t npv = t1 - w0;  // links to stage, <= ZS_LOOKBACK + ZS_TILE
+  uint4 lk[(ZS_LOOKBACK + ZS_TILE) / 8 / 1024];
+  {
+    const uint4* src16 = (const uint4*)(pd + w0);
+#pragma unroll
+    for (uint32_t j = 0; j < (ZS_LOOKBACK + ZS_TILE) / 8 / 1024; j++) {
+      const uint32_t i = threadIdx.x + 1024 * j;  // entries [8i, 8i + 8)
+      if (8 * i + 8 <= npv) lk[j] = src16[i];
       else {
-        for (uint32_t k = 0; k < 4; k++) {
-          const uint32_t b = w0 + 4 * i + k;
-          if (b < w1) v |= (uint32_t)src[b] << (8 * k);
-        }
+        uint32_t v[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+        for (uint32_t k = 0; k < 8; k++)
+          if (8 * i + k < npv) {
+            const uint32_t sh = 16 * (k & 1);
+            v[k >> 1] = (v[k >> 1] & ~(0xffffu << sh)) | ((uint32_t)pd[w0 + 8 * i + k] << sh);
+          }
+        lk[j] = make_uint4(v[0], v[1], v[2], v[3]);
       }
-      wb[i] = v;
+    }
+  }
+  const uint32_t nwords = (w1 - w0 + 3) / 4 + 2;  // window words incl. 8 B of zero slack
+  if ((((uintptr_t)(src + w0)) & 15u) == 0) {
+    constexpr uint32_t J = (ZS_WIN_WORDS + 2 + 4095) / 4096;
+    uint4 wv[J];
+#pragma unroll
+    for (uint32_t j = 0; j < J; j++) {
+      const uint32_t i = threadIdx.x + 1024 * j;  // bytes [w0 + 16i, w0 + 16i + 16)
+      const uint32_t b = w0 + 16 * i;
+      if (b + 16 <= n) wv[j] = ((const uint4*)(src + w0))[i];
+      else {
+        uint32_t v[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < 16; k++)
+          if (b + k < n) v[k >> 2] |= (uint32_t)src[b + k] << (8 * (k & 3));
+        wv[j] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < J; j++) {
+      const uint32_t i = threadIdx.x + 1024 * j;
+      if (4 * i < nwords) *(uint4*)(wb + 4 * i) = wv[j];
     }
   } else {
     for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) {
@@ -248,7 +277,7 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
   // position's hash occurs in the window [w0, t1) -- a u16 histogram built in
   // the LDS the links are staged into afterwards.  The key only orders the
   // work, never changes a result.
-  for (uint32_t i = threadIdx.x; i < (ZS_LOOKBACK + ZS_TILE) / 2; i += blockDim.x) pvw[i] = 0;
+  for (uint32_t i = threadIdx.x; i < 32768 / 8; i += blockDim.x) *(uint4*)(pvw + 4 * i) = make_uint4(0, 0, 0, 0);
   if (threadIdx.x < 256) bins[threadIdx.x] = 0;
   if (threadIdx.x == 0) next = 0;
   __syncthreads();
@@ -294,11 +323,12 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
     const uint32_t o = threadIdx.x + 1024 * i;
     if (t0 + o < t1) order[atomicAdd(&bins[key[i]], 1u)] = (uint16_t)o;
   }
-  // a missing link (0) is staged as 0xffff: the walk's `cur - d <= limit` test
-  // (signed) then also ends the chain, and a head distance > MAX_DIST is invalid
-  for (uint32_t i = threadIdx.x; i < t1 - w0; i += blockDim.x) {
-    const uint32_t d = pd[w0 + i];
-    pv[i] = (uint16_t)(d ? d : 0xffffu);
+  // the links (a missing one is 0xffff: the walk's signed `cur - d <= limit`
+  // test then also ends the chain, and a head distance > MAX_DIST is invalid)
+#pragma unroll
+  for (uint32_t j = 0; j < (ZS_LOOKBACK + ZS_TILE) / 8 / 1024; j++) {
+    const uint32_t i = threadIdx.x + 1024 * j;
+    if (8 * i < npv) *(uint4*)(pvw + 4 * i) = lk[j];
   }
   __syncthreads();
 
