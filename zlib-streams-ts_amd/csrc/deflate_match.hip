@@ -282,10 +282,15 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
   if (threadIdx.x == 0) next = 0;
   __syncthreads();
   const uint32_t hend = min(t1, n > 2 ? n - 2 : 0u);  // positions <= n-3 are inserted (deflate.ts:1367-1370)
-  for (uint32_t q = w0 + threadIdx.x; q < hend; q += blockDim.x) {
-    const uint32_t w = win_word(wb, q - w0);
-    const uint32_t h = (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
-    atomicAdd(&pvw[h >> 1], 1u << (16 * (h & 1u)));
+  // four consecutive positions per thread from two window words
+  for (uint32_t i = threadIdx.x; 4 * i < hend - w0; i += blockDim.x) {
+    const uint32_t lo = wb[i], hi = wb[i + 1];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, k);
+      const uint32_t h = (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
+      if (4 * i + k < hend - w0) atomicAdd(&pvw[h >> 1], 1u << (16 * (h & 1u)));
+    }
   }
   __syncthreads();
   const uint32_t cap = (uint32_t)chain < 255u ? (uint32_t)chain : 255u;
