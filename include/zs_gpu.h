@@ -126,7 +126,9 @@ double zs_last_phase_ms(zs_ctx *ctx, const char *phase);
 void zs_set_timing(zs_ctx *ctx, int on);
 /* Engine options: "timing" (0/1, as zs_set_timing); "inflate_fast" (default 1):
  * decode members lane-per-member and re-run only those that do not end cleanly
- * on the exact stream-layer state machine (0: exact path for every member). */
+ * on the exact stream-layer state machine (0: exact path for every member);
+ * "check_phases" (default 0): synchronise after every kernel phase and fail
+ * with ZS_MEM_ERROR naming the phase whose launch or execution failed. */
 int zs_set_option(zs_ctx *ctx, const char *name, int value);
 
 /* Introspection for tests: copy an intermediate array of stream s of the last

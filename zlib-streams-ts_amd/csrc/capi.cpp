@@ -63,6 +63,7 @@ struct zs_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool timing = false;
+  bool check_phases = false;  // synchronise after every phase and name the one that failed
   // workspace
   Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
   bool inflate_fast = true;
@@ -76,13 +77,29 @@ struct zs_ctx {
   double total_ms = -1;
 };
 
-static void mark(zs_ctx* c, hipStream_t st, const char* name) {
-  if (!c->timing) return;
+// Phase boundary: records a timing event and, with check_phases, waits for the
+// phase and reports a launch or execution error under the phase's name.
+static int mark(zs_ctx* c, hipStream_t st, const char* name) {
+  if (c->check_phases) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      const std::string msg = std::string(name) + ": " + hipGetErrorString(e);
+      return fail(ZS_MEM_ERROR, "%s", msg.c_str());
+    }
+  }
+  if (!c->timing) return ZS_OK;
   hipEvent_t e;
-  if (hipEventCreate(&e) != hipSuccess) return;
+  if (hipEventCreate(&e) != hipSuccess) return ZS_OK;
   (void)hipEventRecord(e, st);
   c->marks.emplace_back(name, e);
+  return ZS_OK;
 }
+#define MARK(name)                              \
+  do {                                          \
+    const int r_ = mark(c, st, name);           \
+    if (r_ != ZS_OK) return r_;                 \
+  } while (0)
 
 static void collect_marks(zs_ctx* c) {
   c->phase_ms.clear();
@@ -173,6 +190,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   if (!c || !name) return fail(ZS_STREAM_ERROR, "invalid arguments");
   if (!strcmp(name, "timing")) c->timing = value != 0;
   else if (!strcmp(name, "inflate_fast")) c->inflate_fast = value != 0;
+  else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else return fail(ZS_STREAM_ERROR, "unknown option %s", name);
   return ZS_OK;
 }
@@ -282,42 +300,42 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   const zs_level_cfg cfg = kLevels[level];
   const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
 
-  mark(c, st, "start");
+  MARK("start");
   if (wrap) {
     zs_k_checksum<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, c->check.as<uint32_t>(), wrap == 1 ? 1 : 2);
     zs_k_copy_check<<<nblocks_s, nthreads_s, 0, st>>>(c->check.as<uint32_t>(), d_st, (int)n);
-    mark(c, st, "checksum");
+    MARK("checksum");
   }
   if (level >= 4) {
     // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
     zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
     if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
-    mark(c, st, "prev");
+    MARK("prev");
     dim3 g((max_len + 8191) / 8192, n);
     if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
                                                  c->mres.as<uint2>(), cfg.chain, cfg.nice);
-    mark(c, st, "match");
+    MARK("match");
     zs_k_parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), c->syms.as<uint32_t>(),
                                  d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
-    mark(c, st, "parse");
+    MARK("parse");
   } else {
     const int fast_smem = 2 * 32768 * 2;  // head[] + prev[] (u16 x 32 K each)
     HIPCHK(hipFuncSetAttribute((const void*)zs_k_fast, hipFuncAttributeMaxDynamicSharedMemorySize, fast_smem));
     zs_k_fast<<<n, 64, fast_smem, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
                                         cfg.chain, cfg.lazy, cfg.nice);
-    mark(c, st, "parse");
+    MARK("parse");
   }
   zs_k_trees<<<dim3(max_blk, n), 64, 0, st>>>(d_in, d_in_off, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
                                               c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), (int)n);
-  mark(c, st, "trees");
+  MARK("trees");
   zs_k_layout<<<nblocks_s, nthreads_s, 0, st>>>(d_blk, d_bk, d_st, d_out_cap, d_out, d_out_off, wrap, (int)n);
-  mark(c, st, "layout");
+  MARK("layout");
   zs_k_emit<<<dim3(max_blk, n), 256, 0, st>>>(d_in, d_in_off, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
                                               c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), d_out, d_out_off, wrap);
-  mark(c, st, "emit");
+  MARK("emit");
   if (wrap) zs_k_wrap<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_out, d_out_off, d_in_len, wrap, level, (int)n);
   zs_k_finish<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_status, d_out_len, (int)n);
-  mark(c, st, "finish");
+  MARK("finish");
   HIPCHK(hipGetLastError());
   collect_marks(c);
   return ZS_OK;
@@ -384,10 +402,10 @@ static int checksum_batch(zs_ctx* c, int kind, uint32_t n, const uint8_t* d_in, 
   memcpy(c->hmeta.data() + ml.in_len, in_len, 4ull * n);
   HIPCHK(c->meta.ensure(ml.bytes));
   HIPCHK(hipMemcpyAsync(c->meta.p, c->hmeta.data(), ml.bytes, hipMemcpyHostToDevice, st));
-  mark(c, st, "start");
+  MARK("start");
   zs_k_checksum<<<n, 64, 0, st>>>(d_in, (const uint64_t*)(c->meta.as<uint8_t>() + ml.in_off),
                                   (const uint32_t*)(c->meta.as<uint8_t>() + ml.in_len), d_check, kind);
-  mark(c, st, "checksum");
+  MARK("checksum");
   HIPCHK(hipGetLastError());
   collect_marks(c);
   return ZS_OK;
@@ -585,7 +603,7 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
   const uint64_t* d_ooff = (const uint64_t*)(dm + ml.out_off);
   const uint32_t* d_ocap = (const uint32_t*)(dm + ml.out_cap);
   zs_lane_res* lres = nullptr;
-  mark(c, st, "start");
+  MARK("start");
   if (c->inflate_fast && wbits != -16) {
     // lane-per-member fast path; anything but a clean end of stream goes to the exact kernel
     HIPCHK(c->ltabs.ensure(zs_inflate_lane_scratch_bytes() * (size_t)n));
@@ -594,20 +612,20 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
     lres = c->lres.as<zs_lane_res>();
     zs_k_inflate_lane<<<(n + 63) / 64, 64, 0, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
                                                     (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>());
-    mark(c, st, "inflate_lane");
+    MARK("inflate_lane");
     if (wbits > 0) {  // trailer checks over the decoded bytes: adler32 (zlib) / crc32 (gzip)
       uint32_t* chk = c->llen.as<uint32_t>() + n;
       zs_k_checksum<<<n, 64, 0, st>>>(d_out, d_ooff, c->llen.as<uint32_t>(), chk, wbits == 31 ? 2 : 1);
       zs_k_inflate_lane_verify<<<(n + 255) / 256, 256, 0, st>>>(lres, chk, n);
-      mark(c, st, "inflate_check");
+      MARK("inflate_check");
     }
   }
   zs_k_inflate<<<n, 64, smem, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
                                     c->istate.as<zs_inflate_result>(), lres);
-  mark(c, st, "inflate");
+  MARK("inflate");
   zs_k_inflate_finish<<<(n + 255) / 256, 256, 0, st>>>(c->istate.as<zs_inflate_result>(), lres, d_status, d_phase,
                                                        d_msg, d_out_len, d_consumed, (int)n);
-  mark(c, st, "finish");
+  MARK("finish");
   HIPCHK(hipGetLastError());
   collect_marks(c);
   return ZS_OK;
