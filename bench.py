@@ -1,18 +1,32 @@
 #!/usr/bin/env python3
-"""Headline benchmark: uncompressed MB/s, deflate-raw level 6, 4096 x 64 KiB
-synthetic T-corpus streams per GPU (BASELINE.json configs[1]).
+"""Headline benchmark: uncompressed MB/s, deflate-raw L6, one 4096 x 64 KiB
+synthetic T-corpus batch (BASELINE.json configs[1]) at 1/2/4/8 GPUs.
 
 One process per GPU (torch.distributed.run for N > 1).  A "step" is one batch
-compression of the rank's 4096 streams, input already resident in HBM, output
-written to HBM; rank r compresses stream indices [r*4096, (r+1)*4096) so the
-per-GPU work is fixed (weak scaling).  For N > 1 the per-stream compressed
-sizes are all-gathered over RCCL at the end of every step (the "final size
-gather" of the north star: it gives every rank the global output layout).
+compression, inputs already resident in HBM, outputs written to HBM.
+
+* Strong scaling (default, the north star's "batch partitioned across the
+  GPUs"): the ONE global batch of --streams streams is split into contiguous
+  shards, rank r compressing streams shard_range(S, N, r) (zsamd/shard.py).
+  value = global input bytes / max-over-ranks step time.
+* --scaling weak: every rank compresses its own --streams streams.
+* For N > 1 every step ends with the final per-stream size all-gather over
+  RCCL (the only collective: it gives every rank the global output layout).
+
+After the timed region, outside it: every output stream is checked against
+the committed reference golden of the workload (tests/golden/batch_*.bin,
+made by the reference bundle) -- a mismatch fails the run; --no-verify skips
+it (profiling runs only).  On rank 0 at N=1 the line also carries the shard
+sweep (the step time of the 512 / 1024 / 2048-stream shards a rank gets at
+8 / 4 / 2 GPUs), the end-to-end host->host rate through zs_deflate_batch, and
+the CPU baselines.  --mode inflate decodes members (C3; with --format gzip the
+C5-i gunzip; with --format deflate64-raw the C5-ii deflate64 decode).
 
 Prints ONE JSON line on rank 0.  See DESIGN.md "Measurement".
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import sys
@@ -20,230 +34,415 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "zlib-streams-ts_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+# SURVEY.md section 6 (measured in the survey container: Intel Xeon 8 vCPU,
+# Node v12.22.9, the reference's own dist/ bundle, median of 3 after warm-up).
+# The reference tree does not exist on the GPU box, so it cannot be re-timed there.
+REFERENCE_TS = {
+    "deflate": {"value": 2.57, "cores": 1, "value_8_cores": 20.2},
+    "deflate-l1-256k": {"value": 4.82, "cores": 1},
+    "deflate-l9-256k": {"value": 2.10, "cores": 1},
+    "inflate": {"value": 84.2, "cores": 1},
+    "gunzip": {"value": 80.3, "cores": 1},
+    "deflate64": {"value": 17.9, "cores": 1},
+}
+GOLDENS = {("text", 65536, 6, "deflate-raw"): "t64_l6_raw", ("text", 65536, 6, "gzip"): "t64_l6_gzip",
+           ("text", 262144, 1, "deflate-raw"): "t256_l1_raw", ("text", 262144, 9, "deflate-raw"): "t256_l9_raw",
+           ("mixed", 65536, 6, "deflate-raw"): "m64_l6_raw"}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--streams", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=4096, help="global batch (strong) or per-GPU batch (weak)")
     ap.add_argument("--stream-bytes", type=int, default=65536)
     ap.add_argument("--level", type=int, default=6)
     ap.add_argument("--format", default="deflate-raw")
-    ap.add_argument("--corpus", default="text")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--corpus", default=None,
+                    help="text | mixed | rand (default: text; mixed for the C3 deflate-raw inflate mode)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU-baseline sample (per variant)")
+    ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", action="store_true", help="check every output against the batch golden")
+    ap.add_argument("--no-verify", action="store_true", help="skip the golden check (profiling runs only)")
+    ap.add_argument("--no-shard-sweep", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--mode", default="deflate", choices=["deflate", "inflate"],
-                    help="deflate: the headline (configs[1]); inflate: C3 decode of pre-built members (configs[2])")
+                    help="deflate: the headline (configs[1]); inflate: decode of pre-built members (configs[2], C5)")
     ap.add_argument("--replicas", type=int, default=16, help="inflate: members = streams x replicas (C3: 4096 x 16)")
     return ap.parse_args()
 
 
-def profiled_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary (FETCH_SIZE / WRITE_SIZE passes, gfx950 read correction applied by
-    tools/summarize_profile.py), or (None, None)."""
+class Dist:
+    """torch.distributed plumbing: one process per GPU (RCCL), or a single process."""
+
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+
+    def barrier(self):
+        self.torch.cuda.synchronize()
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def max(self, x):
+        t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.dev)
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        t = self.torch.tensor([int(x)], dtype=self.torch.int64, device=self.dev)
+        if self.world > 1:
+            self.dist.all_reduce(t)
+        return int(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def profiled_traffic(kernel, kernel_ms):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
+    summary (profiles/*/summary*.json: FETCH_SIZE / WRITE_SIZE passes, gfx950
+    read correction by tools/summarize_profile.py) -- used only when that
+    profile's average kernel duration agrees with this run's HIP-event time
+    within 10 % (i.e. it profiled this build); otherwise (None, reason)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")), key=os.path.getmtime)
     for f in reversed(files):
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
             continue
-        if e and "hbm_bytes_corrected" in e:
-            return int(e["hbm_bytes_corrected"]), os.path.relpath(f, ROOT)
-    return None, None
+        if not e or "hbm_bytes_corrected" not in e:
+            continue
+        prof_ms = e["avg_ns"] / 1e6
+        src = os.path.relpath(f, ROOT)
+        if abs(prof_ms - kernel_ms) > 0.1 * kernel_ms:
+            return None, "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
+        return int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms)
+    return None, "no committed profile for %s" % kernel
 
 
-def cpu_baseline(args):
-    """The C oracle (a single-threaded restatement of the reference algorithm),
-    timed on a bounded sample of the same workload on this host."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+def timed_port(fn, items, seconds, threads):
+    """Runs fn(item) over items until `seconds` of wall time pass; returns
+    (items done, wall seconds).  The oracle is a ctypes C library, so threads
+    run in parallel (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    done, t0 = 0, time.perf_counter()
+    if threads == 1:
+        for it in items:
+            fn(it)
+            done += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        return done, time.perf_counter() - t0
+    with ThreadPoolExecutor(threads) as ex:
+        k = 0
+        while k < len(items) and time.perf_counter() - t0 < seconds:
+            batch = items[k:k + 4 * threads]
+            list(ex.map(fn, batch))
+            done += len(batch)
+            k += len(batch)
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(args, kind, make_item, fn, unit_bytes, n_items, ref_key):
+    """The C oracle (oracle/, a restatement of the reference algorithm; kind
+    "port") on a bounded sample of the same workload on this host, 1 thread and
+    --cpu-threads threads; the reference TS figure is quoted with provenance."""
     import oracle
-    import zsamd
 
     oracle.lib()
-    n = args.stream_bytes
-    done, t_total, i = 0, 0.0, 0
-    while t_total < args.cpu_seconds and i < args.streams:
-        data = bytes(zsamd.corpus(args.corpus, i, 1, n, 1))
-        t0 = time.perf_counter()
-        st, out, _ = oracle.compress(data, args.level, args.format)
-        t_total += time.perf_counter() - t0
-        done += n
-        i += 1
-    return {"value": round(done / t_total / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
-            "sample": "%d of the %d x %d B %s streams, oracle/ C restatement, 1 thread" % (i, args.streams, n, args.corpus)}
+    items = [make_item(i) for i in range(min(n_items, 4096))]
+    fn(items[0])  # warm
+    k1, t1 = timed_port(fn, items, args.cpu_seconds, 1)
+    kp, tp = timed_port(fn, items, args.cpu_seconds, args.cpu_threads)
+    ref = REFERENCE_TS.get(ref_key)
+    out = {"value": round(k1 * unit_bytes / t1 / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+           "sample": "%d %s units of %d B (of the workload's %d), oracle/ C restatement, 1 thread, %.1f s"
+                     % (k1, kind, unit_bytes, n_items, t1),
+           "port_parallel": {"value": round(kp * unit_bytes / tp / 1e6, 3), "cores": args.cpu_threads,
+                             "sample": "%d units, %.1f s" % (kp, tp)}}
+    if ref:
+        out["reference_ts"] = dict(ref, unit="MB/s", kind="reference",
+                                   provenance="SURVEY.md section 6: the reference's dist/ bundle under Node v12.22.9 on "
+                                              "the survey container's Intel Xeon (8 vCPU), median of 3 after warm-up; "
+                                              "/root/reference does not exist on the GPU box, so it is quoted, not re-timed")
+    return out
+
+
+def layout(S, L, cap):
+    in_off = (ctypes.c_uint64 * max(1, S))(*[i * L for i in range(S)])
+    in_len = (ctypes.c_uint32 * max(1, S))(*([L] * S))
+    out_off = (ctypes.c_uint64 * max(1, S))(*[i * cap for i in range(S)])
+    out_cap = (ctypes.c_uint32 * max(1, S))(*([cap] * S))
+    return in_off, in_len, out_off, out_cap
 
 
 def main():
     args = parse()
+    if args.corpus is None:
+        args.corpus = "mixed" if (args.mode == "inflate" and args.format == "deflate-raw") else "text"
     if args.mode == "inflate":
         return main_inflate(args)
-    import torch
-    import torch.distributed as dist
     import zsamd
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    S, L = args.streams, args.stream_bytes
-    first = rank * S
-    host = zsamd.corpus(args.corpus, first, S, L, threads=8)
-    d_in = torch.frombuffer(host, dtype=torch.uint8).to(dev)
-    cap = zsamd.deflate_capacity(L, args.format)
-    d_out = torch.zeros(S * cap, dtype=torch.uint8, device=dev)
-    d_status = torch.zeros(S, dtype=torch.int32, device=dev)
-    d_len = torch.zeros(S, dtype=torch.int32, device=dev)
-    in_off = (ctypes.c_uint64 * S)(*[i * L for i in range(S)])
-    in_len = (ctypes.c_uint32 * S)(*([L] * S))
-    out_off = (ctypes.c_uint64 * S)(*[i * cap for i in range(S)])
-    out_cap = (ctypes.c_uint32 * S)(*([cap] * S))
-    eng = zsamd.Engine(local)
-    stream = torch.cuda.current_stream(dev)
     import zsamd.shard as shard
 
-    def step():
-        eng.compress_device(args.level, args.format, S, d_in.data_ptr(), in_off, in_len, d_out.data_ptr(), out_off,
+    D = Dist()
+    torch = D.torch
+    S_glob = args.streams * (D.world if args.scaling == "weak" else 1)
+    lo, hi = shard.shard_range(S_glob, D.world, D.rank)
+    S, L = hi - lo, args.stream_bytes
+    host = zsamd.corpus(args.corpus, lo, S, L, threads=8)
+    d_in = torch.frombuffer(host, dtype=torch.uint8).to(D.dev)
+    cap = zsamd.deflate_capacity(L, args.format)
+    d_out = torch.zeros(S * cap, dtype=torch.uint8, device=D.dev)
+    d_status = torch.zeros(S, dtype=torch.int32, device=D.dev)
+    d_len = torch.zeros(S, dtype=torch.int32, device=D.dev)
+    in_off, in_len, out_off, out_cap = layout(S, L, cap)
+    eng = zsamd.Engine(D.local)
+    stream = torch.cuda.current_stream(D.dev)
+
+    def run(n):
+        eng.compress_device(args.level, args.format, n, d_in.data_ptr(), in_off, in_len, d_out.data_ptr(), out_off,
                             out_cap, d_status.data_ptr(), d_len.data_ptr(), stream.cuda_stream)
-        if world > 1:
+
+    def step():
+        run(S)
+        if D.world > 1:
             # the final size gather (RCCL all_gather over xGMI): global output layout on every rank
-            sizes = shard.gather_sizes(d_len, world * S)
+            sizes = shard.gather_sizes(d_len, S_glob)
             shard.global_offsets(sizes)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    D.barrier()
     eng.set_timing(True)
     phases = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        for ph in ("checksum", "prev", "depth", "match", "parse", "trees", "layout", "emit", "finish"):
+        for ph in ("checksum", "prev", "match", "parse", "trees", "layout", "emit", "finish"):
             v = eng.last_ms(ph)
             if v >= 0:
                 phases[ph] = phases.get(ph, 0.0) + v
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    D.barrier()
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = D.max(elapsed)
 
     status = d_status.cpu()
     lens = d_len.cpu()
     assert int((status != 1).sum()) == 0, "some streams failed: %s" % status.unique()
-    out_total = int(lens.sum())
-    in_total = S * L
-    if args.verify:
-        import hashlib
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import golden_io
-        recs = golden_io.batch("t64_l6_raw")
-        ob = d_out.cpu().numpy()
-        for i in range(S):
-            o = ob[i * cap: i * cap + int(lens[i])].tobytes()
-            assert (len(o), hashlib.sha256(o).digest()[:16]) == recs[first + i], "stream %d differs" % (first + i)
+    out_local = int(lens.sum())
+    out_total = D.sum(out_local)
+    in_total = S_glob * L
 
-    if rank == 0:
+    # parity: every stream against the reference golden (outside the timed region)
+    verify = {"golden": None, "checked": 0, "mismatches": 0}
+    gname = GOLDENS.get((args.corpus, L, args.level, args.format))
+    if not args.no_verify and gname:
+        import golden_io
+        recs = golden_io.batch(gname)
+        ob = d_out.cpu().numpy()
+        bad = checked = 0
+        for i in range(S):
+            if lo + i >= len(recs):
+                break
+            o = ob[i * cap: i * cap + int(lens[i])].tobytes()
+            checked += 1
+            bad += (len(o), hashlib.sha256(o).digest()[:16]) != recs[lo + i]
+        verify = {"golden": "tests/golden/batch_%s.bin" % gname, "checked": D.sum(checked),
+                  "mismatches": D.sum(bad)}
+        assert verify["mismatches"] == 0, "outputs differ from the reference golden: %s" % verify
+    elif args.no_verify:
+        verify["golden"] = "skipped (--no-verify)"
+
+    extra = {}
+    if D.world == 1 and D.rank == 0:
+        if not args.no_shard_sweep and args.scaling == "strong":
+            # what each rank computes at 8 / 4 / 2 GPUs (same streams, one GPU)
+            sweep = {}
+            for m in (512, 1024, 2048):
+                if m >= S:
+                    continue
+                run(m)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(args.steps):
+                    run(m)
+                torch.cuda.synchronize()
+                sweep[str(m)] = round((time.perf_counter() - t1) / args.steps * 1e3, 4)
+            sweep[str(S)] = round(elapsed / args.steps * 1e3, 4)
+            extra["shard_sweep_ms"] = sweep
+            if "512" in sweep:
+                extra["implied_1_to_8_speedup"] = round(sweep[str(S)] / sweep["512"], 3)
+        if not args.no_e2e:
+            # end-to-end: caller-owned host buffers -> host buffers through zs_deflate_batch
+            import numpy as np
+            hout = np.zeros(S * cap, dtype=np.uint8)
+            st = (ctypes.c_int32 * S)()
+            ol = (ctypes.c_uint32 * S)()
+            hin_ptr = ctypes.addressof((ctypes.c_char * len(host)).from_buffer(host))
+
+            def e2e():
+                eng.compress_host(args.level, args.format, S, hin_ptr, in_off, in_len, hout.ctypes.data, out_off,
+                                  out_cap, st, ol)
+            e2e()
+            t1 = time.perf_counter()
+            reps = max(1, min(args.steps, 5))
+            for _ in range(reps):
+                e2e()
+            te = (time.perf_counter() - t1) / reps
+            ok = sum(ol) == out_local and all(st[i] == 1 for i in range(S))
+            extra["end_to_end"] = {"value": round(in_total / te / 1e6, 2), "unit": "MB/s", "ms": round(te * 1e3, 3),
+                                   "path": "host buffers -> zs_deflate_batch (pinned staging, 1 DMA each way, device "
+                                           "compaction) -> host buffers", "matches_device_path": bool(ok)}
+
+    if D.rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
-        value = world * in_total / (elapsed / args.steps) / 1e6
+        value = in_total / (elapsed / args.steps) / 1e6
         phase_avg = {k: round(v / args.steps, 4) for k, v in phases.items()}
         dom = max(phase_avg, key=phase_avg.get) if phase_avg else None
         roof = None
         if dom:
-            alg = in_total + out_total  # SURVEY.md 8(d): bytes_in + bytes_out per stream, x streams per launch
+            # SURVEY.md 8(d): bytes_in + bytes_out per stream x streams per launch (this rank's shard)
+            alg = S * L + out_local
             achieved = alg / (phase_avg[dom] / 1e3) / 1e9
-            traffic, tsrc = profiled_traffic("zs_k_" + dom)
-            roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": tsrc,
-                    "algorithmic_bytes": alg, "kernel_ms": phase_avg[dom], "phase_ms": phase_avg,
-                    "pipeline_ms": round(sum(phase_avg.values()), 4)}
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+            traffic, tsrc = profiled_traffic("zs_k_" + dom, phase_avg[dom])
+            roof = {"bound": "hbm", "kernel": "zs_k_" + dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "traffic_source": tsrc, "algorithmic_bytes": alg, "kernel_ms": phase_avg[dom],
+                    "phase_ms": phase_avg, "pipeline_ms": round(sum(phase_avg.values()), 4)}
+        cpu = None
+        if not (args.no_cpu_baseline or D.world > 1):
+            import oracle
+            key = "deflate" if L == 65536 else "deflate-l%d-256k" % args.level
+            cpu = cpu_baseline(args, "stream", lambda i: bytes(host[i * L:(i + 1) * L]),
+                               lambda d: oracle.compress(d, args.level, args.format), L, S, key)
         line = {
-            "metric": "uncompressed MB/s, deflate-raw L6, 4096x64KiB batch at 1/2/4/8 GPUs",
-            "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "%d x %d B %s-corpus streams per GPU, %s level %d" % (S, L, args.corpus, args.format,
-                                                                                          args.level),
-                       "streams_per_gpu": S, "stream_bytes": L, "level": args.level, "format": args.format,
-                       "compressed_bytes_per_gpu": out_total, "ratio": round(in_total / max(1, out_total), 4),
-                       "parallelism": "dp%d" % world},
-            "roofline": roof, "cpu_baseline": cpu,
+            "metric": "uncompressed MB/s, deflate-raw L6, 4096x64KiB batch at 1/2/4/8 GPUs"
+            if (args.format, args.level, L, args.corpus) == ("deflate-raw", 6, 65536, "text")
+            else "uncompressed MB/s, %s L%d, %dx%dB %s batch" % (args.format, args.level, S_glob, L, args.corpus),
+            "value": round(value, 2), "unit": "MB/s", "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": args.scaling,
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "%d x %d B %s-corpus streams%s, %s level %d" % (
+                S_glob, L, args.corpus, " split across the GPUs" if args.scaling == "strong" else " (per GPU x N)",
+                args.format, args.level),
+                "global_streams": S_glob, "streams_per_gpu": S, "stream_bytes": L, "level": args.level,
+                "format": args.format, "compressed_bytes": out_total, "ratio": round(in_total / max(1, out_total), 4),
+                "parallelism": "dp%d" % D.world},
+            "verify": verify, "roofline": roof, "cpu_baseline": cpu,
         }
+        line.update(extra)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    D.close()
+
+
+def d64_fixtures():
+    """The reference's test/data deflate64 fixtures (tests/golden/d64) with their
+    decoded sizes / digests from inflate_small.json."""
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "inflate_small.json")))
+    out = []
+    for c in g["cases"]:
+        if c["name"].startswith("d64_") and c.get("ok"):
+            out.append((open(os.path.join(ROOT, "tests", "golden", "d64", c["name"][4:]), "rb").read(),
+                        c["out_len"], c["out_sha256"]))
+    return out
 
 
 def main_inflate(args):
-    """C3: 4096 unique M-corpus 64 KiB buffers compressed at
-    deflate-raw L6 (by this engine, bit-exact to the reference; the batch golden
-    is checked), replicated x16 = 65,536 members, decoded on one GPU.  Metric:
-    uncompressed (output) MB/s.  Weak scaling: rank r decodes its own copy."""
-    import torch
-    import torch.distributed as dist
+    """Decode of pre-built members, strong scaling over the global member list.
+    C3: 4096 unique M-corpus 64 KiB buffers compressed at
+    deflate-raw L6 by this engine (checked against the reference batch golden),
+    x16 = 65,536 members.  --format gzip: C5-i gunzip (CRC-32 trailer checked).
+    --format deflate64-raw: C5-ii, the T-corpus raw-L6 streams decoded as
+    deflate64 (valid deflate64: no length-258 match) with the
+    reference's deflate64 fixtures interleaved.  Metric: output MB/s."""
     import zsamd
+    import zsamd.shard as shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    D = Dist()
+    torch = D.torch
     S, L, R = args.streams, args.stream_bytes, args.replicas
-    eng = zsamd.Engine(local)
-    host = zsamd.corpus("mixed", 0, S, L, threads=8)
-    comp = eng.compress_batch([bytes(host[i * L:(i + 1) * L]) for i in range(S)], "deflate-raw", 6)
-    members = comp * R
+    dec_fmt = args.format
+    enc_fmt = "deflate-raw" if dec_fmt == "deflate64-raw" else dec_fmt
+    eng = zsamd.Engine(D.local)
+    N_glob = S * R
+    lo, hi = shard.shard_range(N_glob, D.world, D.rank)
+    uniq = sorted({i % S for i in range(lo, hi)})
+    umap = {u: k for k, u in enumerate(uniq)}
+    host = bytearray()
+    for u in uniq:
+        host += zsamd.corpus(args.corpus, u, 1, L, threads=1)
+    comp = eng.compress_batch([bytes(host[k * L:(k + 1) * L]) for k in range(len(uniq))], enc_fmt, 6)
+    gname = GOLDENS.get((args.corpus, L, 6, enc_fmt))
+    members_checked = 0
+    if gname and not args.no_verify:
+        import golden_io
+        recs = golden_io.batch(gname)
+        for k, u in enumerate(uniq):
+            if u < len(recs):
+                assert (len(comp[k]), hashlib.sha256(comp[k]).digest()[:16]) == recs[u], "member source %d" % u
+                members_checked += 1
+    members = [comp[umap[i % S]] for i in range(lo, hi)]
+    expect = [("u", umap[i % S]) for i in range(lo, hi)]
+    if dec_fmt == "deflate64-raw":
+        # interleave the reference's deflate64 fixtures (distances > 32 KiB, codes 30/31)
+        fx = d64_fixtures()
+        step_k = max(1, len(members) // max(1, len(fx)))
+        for j, (blob, olen, osha) in enumerate(fx):
+            at = min(len(members), j * step_k + step_k // 2)
+            members.insert(at, blob)
+            expect.insert(at, ("f", olen, osha))
     N = len(members)
+    caps = [L if e[0] == "u" else ((e[1] + 3) & ~3) for e in expect]
     blob = b"".join(members)
-    d_in = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    d_in = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(D.dev)
     offs, o = [], 0
     for m in members:
         offs.append(o)
         o += len(m)
+    oo, ooffs = 0, []
+    for c in caps:
+        ooffs.append(oo)
+        oo += c
     in_off = (ctypes.c_uint64 * N)(*offs)
     in_len = (ctypes.c_uint32 * N)(*[len(m) for m in members])
-    cap = L
-    d_out = torch.zeros(N * cap, dtype=torch.uint8, device=dev)
-    out_off = (ctypes.c_uint64 * N)(*[i * cap for i in range(N)])
-    out_cap = (ctypes.c_uint32 * N)(*([cap] * N))
-    i32 = lambda: torch.zeros(N, dtype=torch.int32, device=dev)
+    d_out = torch.zeros(oo, dtype=torch.uint8, device=D.dev)
+    out_off = (ctypes.c_uint64 * N)(*ooffs)
+    out_cap = (ctypes.c_uint32 * N)(*caps)
+    i32 = lambda: torch.zeros(N, dtype=torch.int32, device=D.dev)
     d_status, d_phase, d_msg, d_len, d_cons = i32(), i32(), i32(), i32(), i32()
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.current_stream(D.dev)
 
     def step():
-        eng.decompress_device("deflate-raw", N, d_in.data_ptr(), in_off, in_len, d_out.data_ptr(), out_off, out_cap,
+        eng.decompress_device(dec_fmt, N, d_in.data_ptr(), in_off, in_len, d_out.data_ptr(), out_off, out_cap,
                               d_status.data_ptr(), d_phase.data_ptr(), d_msg.data_ptr(), d_len.data_ptr(),
                               d_cons.data_ptr(), stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    D.barrier()
     eng.set_timing(True)
     phases = {}
     t0 = time.perf_counter()
@@ -253,58 +452,63 @@ def main_inflate(args):
             v = eng.last_ms(ph)
             if v >= 0:
                 phases[ph] = phases.get(ph, 0.0) + v
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
     eng.set_timing(False)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
     assert int((d_status != 1).sum()) == 0, "some members failed"
-    assert int(d_len.sum()) == N * L
-    if args.verify:
-        ob = d_out.cpu().numpy()
-        for i in range(S):
-            assert ob[i * cap:(i + 1) * cap].tobytes() == bytes(host[i * L:(i + 1) * L]), "member %d differs" % i
-    if rank == 0:
-        out_total, in_total = N * L, len(blob)
+    out_local = int(d_len.to(torch.int64).sum())
+    out_total = D.sum(out_local)
+    in_local = len(blob)
+    in_total = D.sum(in_local)
+    # parity: every member's output against its source bytes / fixture digest (on the GPU)
+    checked = bad = 0
+    if not args.no_verify:
+        src = torch.frombuffer(host, dtype=torch.uint8).to(D.dev).view(-1, L)
+        lens = d_len.cpu().tolist()
+        for i, e in enumerate(expect):
+            if e[0] == "u":
+                ok = lens[i] == L and bool(torch.equal(d_out[ooffs[i]:ooffs[i] + L], src[e[1]]))
+            else:
+                got = d_out[ooffs[i]:ooffs[i] + lens[i]].cpu().numpy().tobytes()
+                ok = lens[i] == e[1] and hashlib.sha256(got).hexdigest() == e[2]
+            checked += 1
+            bad += not ok
+        checked, bad = D.sum(checked), D.sum(bad)
+        assert bad == 0, "%d of %d members decode wrong" % (bad, checked)
+    if D.rank == 0:
         phase_avg = {k: round(v / args.steps, 4) for k, v in phases.items()}
         dom = max(phase_avg, key=phase_avg.get)
         k_ms = phase_avg[dom]
-        alg = in_total + out_total  # compressed_in + uncompressed_out per member
+        alg = in_local + out_local  # compressed_in + uncompressed_out per member
         achieved = alg / (k_ms / 1e3) / 1e9
+        traffic, tsrc = profiled_traffic("zs_k_" + dom, k_ms)
         cpu = None
-        if not (args.no_cpu_baseline or world > 1):
-            sys.path.insert(0, os.path.join(ROOT, "tests"))
+        if not (args.no_cpu_baseline or D.world > 1):
             import oracle
-            done, tt, i = 0, 0.0, 0
-            while tt < args.cpu_seconds and i < S:
-                t1 = time.perf_counter()
-                oracle.decompress(comp[i], "deflate-raw", cap=L)
-                tt += time.perf_counter() - t1
-                done += L
-                i += 1
-            cpu = {"value": round(done / tt / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
-                   "sample": "%d of the %d unique members, oracle/ C restatement, 1 thread" % (i, S)}
+            key = {"deflate64-raw": "deflate64", "gzip": "gunzip"}.get(dec_fmt, "inflate")
+            cpu = cpu_baseline(args, "member", lambda i: comp[i % len(comp)],
+                               lambda m: oracle.decompress(m, dec_fmt, cap=L), L, N, key)
+        name = {"deflate64-raw": "deflate64-raw decode (C5-ii)", "gzip": "gunzip + crc32 (C5-i)"}.get(
+            dec_fmt, "inflate %s L6 members (C3)" % dec_fmt)
         line = {
-            "metric": "uncompressed MB/s, inflate deflate-raw L6 members (C3)",
-            "value": round(world * out_total / (elapsed / args.steps) / 1e6, 2), "unit": "MB/s", "n_gpus": world,
+            "metric": "uncompressed MB/s, %s" % name,
+            "value": round(out_total / (elapsed / args.steps) / 1e6, 2), "unit": "MB/s", "n_gpus": D.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "%d members (%d unique M-corpus %d B buffers x %d), deflate-raw L6, decode" % (N, S, L, R),
-                       "members_per_gpu": N, "compressed_bytes_per_gpu": in_total, "parallelism": "dp%d" % world},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": profiled_traffic("zs_k_" + dom)[0], "traffic_source": profiled_traffic("zs_k_" + dom)[1],
-                         "algorithmic_bytes": alg, "kernel_ms": round(k_ms, 4), "phase_ms": phase_avg},
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "%d members (%d unique %s-corpus %d B buffers x %d%s), %s decode" % (
+                N_glob, S, args.corpus, L, R, " + the 9 reference deflate64 fixtures per rank" if dec_fmt ==
+                "deflate64-raw" else "", dec_fmt), "members_per_gpu": N, "compressed_bytes": in_total,
+                "parallelism": "dp%d" % D.world},
+            "verify": {"members_checked": checked, "mismatches": bad, "sources_vs_golden": members_checked,
+                       "golden": "tests/golden/batch_%s.bin" % gname if gname else None},
+            "roofline": {"bound": "hbm", "kernel": "zs_k_" + dom, "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg,
+                         "kernel_ms": round(k_ms, 4), "phase_ms": phase_avg},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    D.close()
 
 
 if __name__ == "__main__":

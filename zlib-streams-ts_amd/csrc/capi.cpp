@@ -53,6 +53,24 @@ struct Buf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// pinned host staging (grows on demand, reused across calls)
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
 const zs_level_cfg kLevels[10] = {{0, 0, 0, 0},     {4, 4, 8, 4},     {4, 5, 16, 8},     {4, 6, 32, 32},
                                   {4, 4, 16, 16},   {8, 16, 32, 32},  {8, 16, 128, 128}, {8, 32, 128, 256},
                                   {32, 128, 258, 1024}, {32, 258, 258, 4096}};  // deflate.ts:86-103
@@ -68,7 +86,8 @@ struct zs_ctx {
   Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
   bool inflate_fast = true;
   // host staging for the host-buffer entry points
-  Buf d_in, d_out, d_res;
+  Buf d_in, d_out, d_res, d_pack;
+  HostBuf h_in, h_out;
   std::vector<uint8_t> hmeta;
   size_t last_n = 0;
   // timing
@@ -178,8 +197,10 @@ void zs_ctx_destroy(zs_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (Buf* b : {&c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
-                 &c->istate, &c->d_in, &c->d_out, &c->d_res})
+                 &c->istate, &c->d_in, &c->d_out, &c->d_res, &c->d_pack})
     if (b->p) (void)hipFree(b->p);
+  for (HostBuf* b : {&c->h_in, &c->h_out})
+    if (b->p) (void)hipHostFree(b->p);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -341,15 +362,69 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   return ZS_OK;
 }
 
-// host-buffer wrapper shared by deflate / inflate
+// ---------------------------------------------------------- host buffers
+// The host-buffer entry points move data in ONE DMA each way: the caller's
+// streams are packed (in parallel) into a pinned staging buffer and copied to
+// HBM in one hipMemcpyAsync; after the batch the outputs are compacted on the
+// device (4-aligned, in stream order) and come back in one copy of exactly
+// the produced bytes, which the host then scatters to the caller's offsets.
+static void par_copy(uint32_t n, uint8_t* dst, const uint64_t* dst_off, const uint8_t* src, const uint64_t* src_off,
+                     const uint32_t* len, uint64_t total) {
+  const int T = total >= (32u << 20) ? 8 : (total >= (4u << 20) ? 4 : 1);
+  auto part = [&](int t) {
+    for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)T)
+      if (len[i]) memcpy(dst + dst_off[i], src + src_off[i], len[i]);
+  };
+  if (T == 1) { part(0); return; }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++) th.emplace_back(part, t);
+  for (auto& x : th) x.join();
+}
+
 static int stage_in(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                     std::vector<uint64_t>& doff, uint64_t& total) {
   total = 0;
   doff.resize(n);
   for (uint32_t i = 0; i < n; i++) { doff[i] = total; total += in_len[i]; }
   HIPCHK(c->d_in.ensure(total + 16));
-  for (uint32_t i = 0; i < n; i++)
-    if (in_len[i]) HIPCHK(hipMemcpyAsync(c->d_in.as<uint8_t>() + doff[i], in + in_off[i], in_len[i], hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c->h_in.ensure(total + 16));
+  par_copy(n, c->h_in.as<uint8_t>(), doff.data(), in, in_off, in_len, total);
+  if (total) HIPCHK(hipMemcpyAsync(c->d_in.p, c->h_in.p, total, hipMemcpyHostToDevice, c->stream));
+  return ZS_OK;
+}
+
+// dst[poff[s] ...] = src[soff[s] ...], len[s] bytes (all offsets multiples of 4)
+__global__ void zs_k_compact(const uint8_t* __restrict__ src, const uint64_t* __restrict__ offs,
+                             const uint32_t* __restrict__ len, uint8_t* __restrict__ dst, uint32_t n) {
+  const uint32_t s = blockIdx.x;
+  if (s >= n) return;
+  const uint32_t words = (len[s] + 3) / 4;
+  const uint32_t* a = (const uint32_t*)(src + offs[s]);
+  uint32_t* b = (uint32_t*)(dst + offs[n + s]);
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) b[i] = a[i];
+}
+
+// Compacts the produced outputs (len[] already on the host) and copies them
+// into the caller's buffer at out_off[].
+static int fetch_out(zs_ctx* c, uint32_t n, const uint64_t* soff, const uint32_t* d_len, const uint32_t* len,
+                     uint8_t* out, const uint64_t* out_off) {
+  std::vector<uint64_t> offs(2ull * n), poff(n);
+  uint64_t P = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    offs[i] = soff[i];
+    offs[n + i] = poff[i] = P;
+    P += ((uint64_t)len[i] + 3) & ~3ull;
+  }
+  if (!P) return ZS_OK;
+  HIPCHK(c->d_pack.ensure(P + 16 + 16ull * n));
+  uint64_t* d_offs = (uint64_t*)(c->d_pack.as<uint8_t>() + ((P + 15) & ~15ull));
+  HIPCHK(hipMemcpyAsync(d_offs, offs.data(), 16ull * n, hipMemcpyHostToDevice, c->stream));
+  zs_k_compact<<<n, 256, 0, c->stream>>>(c->d_out.as<uint8_t>(), d_offs, d_len, c->d_pack.as<uint8_t>(), n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(c->h_out.ensure(P + 16));
+  HIPCHK(hipMemcpyAsync(c->h_out.p, c->d_pack.p, P, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  par_copy(n, out, out_off, c->h_out.as<uint8_t>(), poff.data(), len, P);
   return ZS_OK;
 }
 
@@ -378,11 +453,7 @@ extern "C" int zs_deflate_batch(zs_ctx* c, int level, int wbits, uint32_t n, con
   HIPCHK(hipMemcpyAsync(status, d_status, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(out_len, d_len, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  for (uint32_t i = 0; i < n; i++)
-    if (status[i] == ZS_STREAM_END && out_len[i])
-      HIPCHK(hipMemcpyAsync(out + out_off[i], c->d_out.as<uint8_t>() + ooff[i], out_len[i], hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return ZS_OK;
+  return fetch_out(c, n, ooff.data(), d_len, out_len, out, out_off);  // out_len is 0 for failed streams
 }
 
 extern "C" int zs_crc32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
@@ -640,7 +711,8 @@ extern "C" int zs_inflate_batch(zs_ctx* c, int wbits, uint32_t n, const uint8_t*
   uint64_t total = 0, ototal = 0;
   int r = stage_in(c, n, in, in_off, in_len, doff, total);
   if (r != ZS_OK) return r;
-  for (uint32_t i = 0; i < n; i++) { ooff[i] = ototal; ototal += out_cap[i]; }
+  std::vector<uint32_t> ocap(n);
+  for (uint32_t i = 0; i < n; i++) { ooff[i] = ototal; ocap[i] = out_cap[i]; ototal += ((uint64_t)out_cap[i] + 3) & ~3ull; }
   HIPCHK(c->d_out.ensure(ototal + 16));
   HIPCHK(c->d_res.ensure(20ull * n + 16));
   int32_t* d_status = c->d_res.as<int32_t>();
@@ -649,7 +721,7 @@ extern "C" int zs_inflate_batch(zs_ctx* c, int wbits, uint32_t n, const uint8_t*
   uint32_t* d_len = (uint32_t*)(d_msg + n);
   uint32_t* d_cons = d_len + n;
   r = zs_inflate_batch_device(c, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len, c->d_out.as<uint8_t>(),
-                              ooff.data(), out_cap, d_status, d_phase, d_msg, d_len, d_cons, c->stream);
+                              ooff.data(), ocap.data(), d_status, d_phase, d_msg, d_len, d_cons, c->stream);
   if (r != ZS_OK) return r;
   HIPCHK(hipMemcpyAsync(status, d_status, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(phase, d_phase, 4ull * n, hipMemcpyDeviceToHost, c->stream));
@@ -657,9 +729,5 @@ extern "C" int zs_inflate_batch(zs_ctx* c, int wbits, uint32_t n, const uint8_t*
   HIPCHK(hipMemcpyAsync(out_len, d_len, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(consumed, d_cons, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  for (uint32_t i = 0; i < n; i++)
-    if (out_len[i])
-      HIPCHK(hipMemcpyAsync(out + out_off[i], c->d_out.as<uint8_t>() + ooff[i], out_len[i], hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return ZS_OK;
+  return fetch_out(c, n, ooff.data(), d_len, out_len, out, out_off);
 }

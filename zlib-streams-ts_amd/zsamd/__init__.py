@@ -275,6 +275,14 @@ class Engine:
                                             _P(d_consumed), _P(hip_stream) if hip_stream else None)
         self._check(r, "zs_inflate_batch_device")
 
+    def compress_host(self, level: int, fmt: str, n: int, h_in: int, in_off, in_len, h_out: int, out_off, out_cap,
+                      status, out_len):
+        """zs_deflate_batch on caller-owned host memory (pointers as ints,
+        layout/result arrays as ctypes arrays): the end-to-end host->host path."""
+        r = self._L.zs_deflate_batch(self._ctx, level, compress_wbits(fmt), n, ctypes.cast(h_in, ctypes.c_char_p),
+                                     in_off, in_len, _P(h_out), out_off, out_cap, status, out_len)
+        self._check(r, "zs_deflate_batch")
+
     def checksum_device(self, kind: str, n: int, d_in: int, in_off, in_len, d_check: int, hip_stream: int = 0):
         fn = self._L.zs_crc32_batch_device if kind == "crc32" else self._L.zs_adler32_batch_device
         r = fn(self._ctx, n, _P(d_in), in_off, in_len, _P(d_check), _P(hip_stream) if hip_stream else None)
