@@ -62,6 +62,34 @@ def test_block_boundaries_and_stored_blocks(engine):
             assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1], (len(d), level)
 
 
+@pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
+def test_sweep_match_table_equals_chain_walk(engine, level):
+    """zs_k_bucket + zs_k_sweep (deflate_sweep.hip) and zs_k_prev16 + zs_k_match
+    (deflate_match.hip) compute the same longest_match table -- both budgets and
+    the slide-NIL flag -- at every position, and the same output bytes."""
+    rng = random.Random(500 + level)
+    inputs = []
+    for k in range(20):
+        n = rng.choice([0, 1, 2, 3, 4, 5, 9, 10, 11, 258, 259, 300, 4097, 32506, 32507, 32769, 65535, 65536, 65537,
+                        rng.randrange(1, 65538)])
+        kind = rng.choice(["text", "mixed", "rand", "zeros", "ramp"])
+        inputs.append(corpus.make({"kind": kind, "n": n, "seed": rng.randrange(1 << 32)}))
+    b = bytearray(corpus.rand(77, 65536))  # a candidate at exactly MAX_DIST (SURVEY A3)
+    b[40000:40020] = b[40000 - 32506:40000 - 32506 + 20]
+    inputs.append(bytes(b))
+    tables, outs = [], []
+    try:
+        for sweep in (1, 0):
+            engine.set_option("match_sweep", sweep)
+            outs.append(engine.compress_batch_raw(inputs, "deflate-raw", level))
+            tables.append([engine.debug_fetch(1, i, 8 * len(d)) for i, d in enumerate(inputs)])
+    finally:
+        engine.set_option("match_sweep", 1)
+    for i, d in enumerate(inputs):
+        assert tables[0][i] == tables[1][i], (i, len(d))
+        assert outs[0][i] == outs[1][i] and outs[0][i][1] == oracle.compress(d, level, "deflate-raw")[1], (i, len(d))
+
+
 def test_output_capacity_too_small_reports_buf_error(engine):
     import ctypes
     import zsamd

@@ -1,0 +1,179 @@
+// emu_bucket_sweep.c -- CPU model of the L4..L9 match finder for streams of
+// at most 65,537 bytes (zs_k_bucket + zs_k_sweep, deflate_sweep.hip), checked
+// position by position against a direct longest_match (deflate.ts:1053-1115)
+// for both budgets the lazy parse asks for (chain, chain >> 2 when
+// prev_length >= good_match, deflate.ts:1075-1077) and for the slide-NIL flag.
+//
+// The model follows the kernels' data flow:
+//   * members: the positions p <= n-3 (every one is inserted),
+//     sorted by (15-bit hash, position) -- a counting sort whose scatter keeps
+//     position order inside a bucket.  Member k's chain (deflate.ts:1109) is
+//     then members k-1, k-2, ... of its own bucket: the t-th predecessor is
+//     the t-th chain step, no links are followed.
+//   * the sweep: for t = 1, 2, ... every lane compares its position with the
+//     t-th predecessor's 8-byte signature; a candidate is alive while
+//     key = hash << 16 | pos passes the head test (t = 1: non-NIL, distance
+//     <= MAX_DIST, deflate.ts:1376) or the chain test (t >= 2: pos > limit,
+//     deflate.ts:1109) and t <= budget; liveness is monotone in t.
+//   * a candidate whose 8 signature bytes all match (and maxc > 8) is "long":
+//     up to 4 are recorded (t, pos) and extended afterwards in chain order
+//     with the nice cut-off (deflate.ts:1100-1105); a fifth ends the lane's
+//     sweep and the lane re-walks its chain from the first long candidate.
+//   * short candidates keep the first max of (len, -t) (first strictly longer
+//     wins), clamped to maxc (deflate.ts:1068); when any long candidate is
+//     within the budget the result comes from the long ones only.
+// Test infrastructure (tests/test_emu_sweep.py); it checks the algorithm off
+// the GPU, not the kernel binary (tests/test_gpu_deflate.py does that).
+//
+// usage: emu_bucket_sweep FILE CHAIN NICE; FILE = u32 count, u32 sizes[count], bytes
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#define MAXD 32506u
+#define NLONG 4
+
+static uint8_t buf[65536 + 300];
+static int32_t head[32768], prev[65536];
+static uint32_t cnt[32768], off[32768];
+static uint16_t mem[65536];
+
+static uint32_t hash3(uint32_t p) { return ((buf[p] << 10) ^ (buf[p + 1] << 5) ^ buf[p + 2]) & 0x7fff; }
+
+// direct reference: longest_match with a chain budget; returns len << 16 | dist
+// (dist only when len > 2), 0 when the reference does not call it (no head)
+static uint32_t ref_lm(uint32_t n, uint32_t p, uint32_t budget, uint32_t nice_cfg) {
+  int32_t cur = prev[p];
+  if (p + 2 >= n || cur <= 0 || p - (uint32_t)cur > MAXD) return 0;
+  uint32_t look = n - p, maxc = look < 258 ? look : 258, nice = look < nice_cfg ? look : nice_cfg;
+  int limit = p > MAXD ? (int)(p - MAXD) : 0;
+  uint32_t bl = 2, bd = 0, st = 0;
+  for (;;) {
+    st++;
+    uint32_t k = 0;
+    while (k < maxc && buf[cur + k] == buf[p + k]) k++;
+    if (k > bl) { bl = k; bd = p - cur; if (k >= nice) break; }
+    if (st >= budget) break;
+    int32_t nx = prev[cur];
+    if (nx <= limit) break;
+    cur = nx;
+  }
+  return (bl << 16) | (bl > 2 ? bd : 0);
+}
+
+static uint32_t lcp8(uint32_t a, uint32_t b) {
+  uint32_t k = 0;
+  while (k < 8 && buf[a + k] == buf[b + k]) k++;
+  return k;
+}
+
+// exact length of a long candidate (>= 8 equal bytes), clamped to maxc
+static uint32_t extend(uint32_t p, uint32_t q, uint32_t maxc) {
+  uint32_t k = 8;
+  while (k < maxc && buf[q + k] == buf[p + k]) k++;
+  return k < maxc ? k : maxc;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) { fprintf(stderr, "usage: %s FILE CHAIN NICE\n", argv[0]); return 2; }
+  FILE* f = fopen(argv[1], "rb");
+  const uint32_t chain = atoi(argv[2]), nice_cfg = atoi(argv[3]), chain_s = chain >> 2;
+  if (!f) return 2;
+  uint32_t ns = 0, sizes[4096];
+  if (fread(&ns, 4, 1, f) != 1 || ns > 4096 || fread(sizes, 4, ns, f) != ns) return 2;
+  long bad = 0, checked = 0, overflow = 0, longs = 0, steps = 0;
+  for (uint32_t si = 0; si < ns; si++) {
+    const uint32_t n = sizes[si];
+    if (n > 65537) return 2;
+    memset(buf, 0, sizeof buf);
+    if (fread(buf, 1, n, f) != n) return 2;
+    // reference chains (for ref_lm)
+    for (int i = 0; i < 32768; i++) head[i] = -1;
+    for (uint32_t p = 0; p < n; p++) {
+      prev[p] = 0;
+      if (p + 2 >= n) continue;
+      const uint32_t h = hash3(p);
+      if (head[h] > 0) prev[p] = head[h];
+      head[h] = (int32_t)p;
+    }
+    // zs_k_bucket: counting sort of the inserted positions by hash (stable)
+    const uint32_t m = n > 2 ? n - 2 : 0;
+    memset(cnt, 0, sizeof cnt);
+    for (uint32_t p = 0; p < m; p++) cnt[hash3(p)]++;
+    uint32_t run = 0;
+    for (int h = 0; h < 32768; h++) { off[h] = run; run += cnt[h]; }
+    for (uint32_t p = 0; p < m; p++) mem[off[hash3(p)]++] = (uint16_t)p;
+    // zs_k_sweep, one lane per member
+    for (uint32_t k = 0; k < m; k++) {
+      const uint32_t p = mem[k], h = hash3(p);
+      const uint32_t look = n - p, maxc = look < 258 ? look : 258, nice = look < nice_cfg ? look : nice_cfg;
+      const uint32_t kcap = maxc < 8 ? maxc : 8, long_thr = maxc > 8 ? 8 : 9;
+      const uint32_t limit = p > MAXD ? p - MAXD : 0;
+      const uint32_t khead = (h << 16) | (limit > 1 ? limit : 1), klim = (h << 16) | limit;
+      uint32_t best = 2u << 16, best_s = best, nl = 0, lt[NLONG], lq[NLONG], flag = 0, t_end = 0;
+      int ovf = 0, headok = 0;
+      for (uint32_t t = 1; t <= chain && t <= k; t++) {
+        const uint32_t q = mem[k - t], key = (hash3(q) << 16) | q;
+        if (t == 1 ? key < khead : key <= klim) break;
+        if (t == 1) { headok = 1; flag = (p - q == MAXD) ? 0x8000u : 0u; }
+        steps++;
+        t_end = t;
+        uint32_t kk = lcp8(p, q);
+        kk = kk < kcap ? kk : kcap;
+        if (kk >= long_thr) {
+          if (nl == NLONG) { ovf = 1; break; }
+          lt[nl] = t; lq[nl] = q; nl++;
+        }
+        const uint32_t score = (kk << 16) | (0xffffu - t);
+        if (score > best) best = score;
+        if (t == chain_s) best_s = best;
+      }
+      if (t_end < chain_s) best_s = best;
+      uint32_t rx = 0, ry = 0;
+      if (headok) {
+        uint32_t bl = best >> 16, bd = bl > 2 ? p - mem[k - (0xffffu - (best & 0xffffu))] : 0;
+        uint32_t bsl = best_s >> 16, bsd = bsl > 2 ? p - mem[k - (0xffffu - (best_s & 0xffffu))] : 0;
+        if (nl) {
+          longs += nl;
+          uint32_t lb = 0, ld = 0, lbs = 0, lds = 0;
+          if (ovf) {  // a fifth long candidate: re-walk the chain from the first long one
+            overflow++;
+            for (uint32_t t = lt[0]; t <= chain && t <= k; t++) {
+              const uint32_t q = mem[k - t], key = (hash3(q) << 16) | q;
+              if (t == 1 ? key < khead : key <= klim) break;
+              if (lcp8(p, q) < long_thr) continue;
+              const uint32_t L = extend(p, q, maxc);
+              if (L > lb) { lb = L; ld = p - q; }
+              if (t <= chain_s && L > lbs) { lbs = L; lds = p - q; }
+              if (L >= nice) break;
+            }
+          } else {
+            for (uint32_t i = 0; i < nl; i++) {
+              const uint32_t L = extend(p, lq[i], maxc);
+              if (L > lb) { lb = L; ld = p - lq[i]; }
+              if (lt[i] <= chain_s && L > lbs) { lbs = L; lds = p - lq[i]; }
+              if (L >= nice) break;
+            }
+          }
+          bl = lb; bd = ld;
+          if (lbs) { bsl = lbs; bsd = lds; }
+        }
+        rx = (bl << 16) | bd | flag;
+        ry = (bsl << 16) | bsd;
+      }
+      // reference
+      const uint32_t ex = ref_lm(n, p, chain, nice_cfg);
+      const uint32_t ey = ref_lm(n, p, chain_s ? chain_s : 1, nice_cfg);
+      const uint32_t ef = (ex && prev[p] > 0 && p - (uint32_t)prev[p] == MAXD) ? 0x8000u : 0u;
+      checked++;
+      if (rx != (ex | ef) || (ex && ry != ey)) {
+        if (bad < 10)
+          printf("stream %u pos %u: got %08x/%08x want %08x/%08x\n", si, p, rx, ry, ex | ef, ey);
+        bad++;
+      }
+    }
+  }
+  printf("checked %ld positions, mismatches %ld, sweep steps %ld, long candidates %ld, overflow lanes %ld\n",
+         checked, bad, steps, longs, overflow);
+  return bad != 0;
+}

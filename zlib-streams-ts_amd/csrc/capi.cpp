@@ -85,6 +85,7 @@ struct zs_ctx {
   // workspace
   Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
   bool inflate_fast = true;
+  bool match_sweep = true;  // L4..9 streams <= 65537 B: bucket sort + sweep (0: chain links + walk)
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res, d_pack;
   HostBuf h_in, h_out;
@@ -212,6 +213,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   if (!strcmp(name, "timing")) c->timing = value != 0;
   else if (!strcmp(name, "inflate_fast")) c->inflate_fast = value != 0;
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
+  else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else return fail(ZS_STREAM_ERROR, "unknown option %s", name);
   return ZS_OK;
 }
@@ -328,14 +330,28 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
     MARK("checksum");
   }
   if (level >= 4) {
-    // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
-    zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
-    if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
-    MARK("prev");
-    dim3 g((max_len + 8191) / 8192, n);
-    if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
-                                                 c->mres.as<uint2>(), cfg.chain, cfg.nice);
-    MARK("match");
+    const dim3 g((max_len + 8191) / 8192, n);
+    if (c->match_sweep) {
+      // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
+      // longer ones: chain links + per-tile chain walk (deflate_match.hip)
+      zs_k_bucket<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
+      if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+      MARK("prev");
+      zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
+                                     cfg.chain, cfg.nice);
+      if (max_len > 65537u)
+        zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
+                                       cfg.chain, cfg.nice, 65537u);
+      MARK("match");
+    } else {
+      // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
+      zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+      if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+      MARK("prev");
+      if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
+                                                   c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
+      MARK("match");
+    }
     zs_k_parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), c->syms.as<uint32_t>(),
                                  d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
     MARK("parse");

@@ -191,7 +191,7 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
                                                    const uint32_t* __restrict__ in_len,
                                                    const uint64_t* __restrict__ pos_base,
                                                    const uint16_t* __restrict__ prevd, uint2* __restrict__ mres,
-                                                   int chain, int nice_cfg) {
+                                                   int chain, int nice_cfg, uint32_t min_len) {
   // One LDS array, carved by hand so the window sits at address 0 and the
   // links at a constant below 64 KiB: the walk's LDS reads then need no base
   // add (the link base rides in the instruction's offset field).
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(1024) void zs_k_match(const uint8_t* __restrict__ i
   const int s = blockIdx.y;
   const uint32_t n = in_len[s];
   const uint32_t t0 = blockIdx.x * ZS_TILE;
-  if (t0 >= n) return;
+  if (t0 >= n || n <= min_len) return;  // n <= min_len: zs_k_sweep's stream
   const uint32_t t1 = min(n, t0 + ZS_TILE);
   const uint32_t w0 = t0 > ZS_LOOKBACK ? t0 - ZS_LOOKBACK : 0;  // multiple of 4
   const uint32_t w1 = min(n, t1 + ZS_MAX_MATCH + 4);

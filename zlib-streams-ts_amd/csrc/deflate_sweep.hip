@@ -1,0 +1,440 @@
+// deflate_sweep.hip -- LZ77 match finding for deflate levels 4..9 on gfx950,
+// streams of at most 65,537 bytes (the batch workloads' 64 KiB streams).
+//
+// What it computes is what zs_k_match (deflate_match.hip) computes: for EVERY
+// position p, the (length, distance) the reference's longest_match
+// (deflate.ts:1053-1115) returns at p for the full chain budget and for the
+// budget >> 2 used when prev_length >= good_match (deflate.ts:1075-1077).  At
+// levels 4..9 every position <= n-3 is inserted into its hash chain exactly
+// once and in order, so p's chain is "every earlier inserted
+// position with the same 15-bit hash, most recent first", cut at
+// limit = p - MAX_DIST (deflate.ts:1060,1109) and by the budget.
+//
+// How is different.  Instead of following prev[] links (a dependent LDS
+// round trip per chain step), the positions are counting-sorted by (hash,
+// position) into a "member" array (zs_k_bucket).  Member k's chain is then
+// simply members k-1, k-2, ... of its bucket, and the t-th predecessor is the
+// t-th chain step.  zs_k_sweep gives each lane one member and sweeps t = 1,
+// 2, ... for all 64 lanes at once: lane i reads the record of member
+// k0 + i - t from a per-wave LDS ring (consecutive lanes, consecutive 16-byte
+// records: conflict-free, and no load depends on the previous step), compares
+// the 8-byte signatures with xor + ffbl, and keeps the first maximum.
+//
+// Exactness (checked off the GPU by tools/emu/emu_bucket_sweep.c against a
+// direct longest_match, and on the GPU by tests/test_gpu_deflate.py):
+//   * liveness: record key = hash << 16 | pos; the head (t = 1) needs
+//     key >= hash << 16 | max(limit, 1) (non-NIL, distance <= MAX_DIST,
+//     deflate.ts:1376), the chain (t >= 2) key > hash << 16 | limit
+//     (deflate.ts:1109); a member of another bucket fails both.  Liveness is
+//     monotone in t, so a lane leaves at its first dead step.
+//   * first strictly longer match wins (deflate.ts:1100-1105): the best is the
+//     maximum of (len << 16) | (0xffff - t).  Lengths are clamped to maxc =
+//     min(258, lookahead) (deflate.ts:1068) through the min3 below.
+//   * a candidate whose 12 signature bytes all match (maxc > 12) is "long":
+//     its exact length needs the window.  Up to four are recorded in chain
+//     order and extended after the sweep, with the nice cut-off (nice >= 16 at
+//     levels 4..9, so no short candidate reaches it unless the stream ends
+//     first, where maxc clamps it); when one exists within the budget the
+//     result is among them (every short one is <= 12).
+//     A fifth long candidate ends the lane's sweep, and the lane re-walks its
+//     chain from the first long one (repetitive data: the first is usually a
+//     nice match).
+#include <hip/hip_runtime.h>
+#include "zs_common.h"
+#include "zs_kernels.h"
+
+#define ZS_SWEEP_MAX 65537u  // position + 1 <= 65535 for every inserted position: u16 members and offsets
+#define ZS_BK_STAGE 4096u
+#define ZS_SW_WIN_WORDS ((ZS_SWEEP_MAX + 20u + 3u) / 4u + 2u)
+#define ZS_SW_RING 128u  // records per wave (two blocks of 64 members), stored twice (mirror)
+
+typedef __attribute__((address_space(3))) uint32_t zs_sw_lds_u32;
+static __device__ __forceinline__ uint32_t sw_lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const zs_sw_lds_u32*)p;
+}
+
+static __device__ __forceinline__ uint32_t sw_hash(uint32_t w) {  // SURVEY A1, bytes 0..2 of w
+  return (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
+}
+
+// Stages input bytes [c0, c0 + ZS_BK_STAGE + 8) of one stream into stg (one wave).
+static __device__ __forceinline__ void sw_stage(uint32_t* stg, const uint8_t* src, uint32_t n, uint32_t c0,
+                                                bool aligned, uint32_t lane) {
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = lane; i < ZS_BK_STAGE / 4 + 2; i += 64) {
+    const uint32_t at = c0 + 4 * i;
+    uint32_t v = 0;
+    if (aligned && at + 4 <= n) {
+      v = *(const uint32_t*)(src + at);
+    } else {
+      for (uint32_t k = 0; k < 4; k++)
+        if (at + k < n) v |= (uint32_t)src[at + k] << (8 * k);
+    }
+    stg[i] = v;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// -------------------------------------------------------------- zs_k_bucket
+// One wave per stream: a counting sort of the inserted positions p <= n-3 by
+// their hash, stable in position, into members[] (u16, the stream's range of
+// the per-position workspace).  Pass 1 counts (32768 u16 buckets, two per LDS
+// word), an exclusive scan turns the counts into offsets, pass 2 walks the
+// positions in order, 64 per instruction, and claims slots with ONE
+// ds_add_rtn_u32 per lane: gfx950 applies same-address LDS atomics of one wave
+// instruction in increasing lane order (zs_selftest checks it, including the
+// 16-bit half form used here), so equal hashes get slots in position order.
+// Results of the positions that are not inserted (the last two) are zeroed.
+__global__ __launch_bounds__(64) void zs_k_bucket(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                  const uint32_t* __restrict__ in_len,
+                                                  const uint64_t* __restrict__ pos_base, uint16_t* __restrict__ members,
+                                                  uint2* __restrict__ mres) {
+  __shared__ uint32_t cnt[16384];
+  __shared__ uint32_t stg[ZS_BK_STAGE / 4 + 2];
+  const int s = blockIdx.x;
+  const uint32_t n = in_len[s];
+  if (n > ZS_SWEEP_MAX) return;  // zs_k_prev / zs_k_match's stream
+  const uint32_t lane = threadIdx.x;
+  const uint8_t* src = in + in_off[s];
+  uint16_t* mem = members + pos_base[s];
+  uint2* out = mres + pos_base[s];
+  const uint32_t m = n > 2 ? n - 2 : 0u;  // inserted positions (deflate.ts:1367-1370)
+  for (uint32_t p = m + lane; p < n; p += 64) out[p] = make_uint2(0, 0);
+  if (m == 0) return;
+  for (uint32_t i = lane; i < 16384; i += 64) cnt[i] = 0;
+  const bool aligned = ((uintptr_t)src & 3u) == 0;
+  // pass 1: bucket sizes
+  for (uint32_t c0 = 0; c0 < m; c0 += ZS_BK_STAGE) {
+    sw_stage(stg, src, n, c0, aligned, lane);
+    const uint32_t c1 = min(m, c0 + ZS_BK_STAGE);
+    for (uint32_t p = c0 + lane; p < c1; p += 64) {
+      const uint32_t o = p - c0;
+      const uint32_t h = sw_hash(__builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u));
+      atomicAdd(&cnt[h >> 1], 1u << (16u * (h & 1u)));
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  // exclusive scan: lane i owns words [256i, 256i + 256) (buckets 512i ...)
+  {
+    uint32_t sum = 0;
+    for (uint32_t j = 0; j < 256; j++) {
+      const uint32_t w = cnt[256 * lane + ((j + lane) & 255u)];  // rotated: lanes hit different banks
+      sum += (w & 0xffffu) + (w >> 16);
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    uint32_t run = x - sum;
+    for (uint32_t j = 0; j < 256; j++) {
+      const uint32_t w = cnt[256 * lane + j];
+      const uint32_t lo = w & 0xffffu;
+      cnt[256 * lane + j] = run | ((run + lo) << 16);
+      run += lo + (w >> 16);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  // pass 2: ordered scatter, four instructions (256 positions) per wait
+  for (uint32_t c0 = 0; c0 < m; c0 += ZS_BK_STAGE) {
+    sw_stage(stg, src, n, c0, aligned, lane);
+    const uint32_t c1 = min(m, c0 + ZS_BK_STAGE);
+    for (uint32_t g0 = c0; g0 < c1; g0 += 256) {
+      uint32_t a[4], v[4], sh[4], e[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t p = g0 + 64 * j + lane;
+        const uint32_t o = p - c0;
+        const uint32_t h = sw_hash(__builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u));
+        sh[j] = 16u * (h & 1u);
+        a[j] = sw_lds_addr(&cnt[h >> 1]);
+        v[j] = p < c1 ? 1u << sh[j] : 0u;  // a lane past the chunk adds nothing
+      }
+      // in order: group j's adds land after group j-1's (LDS executes a wave's ops in order)
+      asm volatile(
+          "ds_add_rtn_u32 %0, %4, %8\n\t"
+          "ds_add_rtn_u32 %1, %5, %9\n\t"
+          "ds_add_rtn_u32 %2, %6, %10\n\t"
+          "ds_add_rtn_u32 %3, %7, %11\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(e[0]), "=&v"(e[1]), "=&v"(e[2]), "=&v"(e[3])
+          : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3])
+          : "memory");
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t p = g0 + 64 * j + lane;
+        if (p < c1) mem[(e[j] >> sh[j]) & 0xffffu] = (uint16_t)p;
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------- zs_k_sweep
+static __device__ __forceinline__ uint32_t sw_word(const uint32_t* win, uint32_t off) {
+  const uint32_t i = off >> 2;
+  return __builtin_amdgcn_alignbyte(win[i + 1], win[i], off & 3u);
+}
+
+// exact length of a candidate whose first 12 bytes match, clamped to maxc
+static __device__ __forceinline__ uint32_t sw_extend(const uint32_t* win, uint32_t p, uint32_t q, uint32_t maxc) {
+  uint32_t k = 12;
+  while (k < maxc) {
+    const uint32_t y = sw_word(win, q + k) ^ sw_word(win, p + k);
+    if (y) { k += (uint32_t)(__builtin_ctz(y) >> 3); break; }
+    k += 4;
+  }
+  return k < maxc ? k : maxc;
+}
+
+// matched bytes (0..12) of two 12-byte signatures, capped at kcap / 8
+static __device__ __forceinline__ uint32_t sw_lcp(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t b0, uint32_t b1,
+                                                  uint32_t b2, uint32_t kcap) {
+  uint32_t f0, f1, f2;
+  asm("v_ffbl_b32 %0, %1" : "=v"(f0) : "v"(a0 ^ b0));
+  asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e64 %0, %0, 32 clamp" : "=&v"(f1) : "v"(a1 ^ b1));
+  asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e64 %0, %0, 64 clamp" : "=&v"(f2) : "v"(a2 ^ b2));
+  // ffbl(0) = ~0 and the clamped adds keep "no difference" at ~0: the cap wins
+  return min(min(f0, f1), min(f2, kcap)) >> 3;
+}
+
+struct SwRec {
+  uint32_t w0, w1, w2, key;  // bytes [q, q + 12) and hash << 16 | q
+};
+
+__global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                   const uint32_t* __restrict__ in_len,
+                                                   const uint64_t* __restrict__ pos_base,
+                                                   const uint16_t* __restrict__ members, uint2* __restrict__ mres,
+                                                   int chain, int nice_cfg) {
+  __shared__ __attribute__((aligned(16))) SwRec ring[16][2 * ZS_SW_RING];
+  __shared__ __attribute__((aligned(16))) uint32_t win[ZS_SW_WIN_WORDS];
+  __shared__ uint32_t next;
+  const int s = blockIdx.x;
+  const uint32_t n = in_len[s];
+  if (n > ZS_SWEEP_MAX || n < 3) return;
+  const uint32_t m = n - 2;
+  const uint8_t* src = in + in_off[s];
+  const uint16_t* mem = members + pos_base[s];
+  uint2* out = mres + pos_base[s];
+  // the whole stream in LDS, zero padded (reads run up to 16 bytes past n)
+  if ((((uintptr_t)src) & 15u) == 0) {
+    for (uint32_t i = threadIdx.x; 4 * i < ZS_SW_WIN_WORDS; i += 1024) {
+      const uint32_t b = 16 * i;
+      uint4 v;
+      if (b + 16 <= n) v = ((const uint4*)src)[i];
+      else {
+        uint32_t t[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < 16; k++)
+          if (b + k < n) t[k >> 2] |= (uint32_t)src[b + k] << (8 * (k & 3));
+        v = make_uint4(t[0], t[1], t[2], t[3]);
+      }
+      if (4 * i + 3 < ZS_SW_WIN_WORDS) *(uint4*)(win + 4 * i) = v;
+      else for (uint32_t k = 0; 4 * i + k < ZS_SW_WIN_WORDS; k++) win[4 * i + k] = (&v.x)[k];
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < ZS_SW_WIN_WORDS; i += 1024) {
+      uint32_t v = 0;
+      for (uint32_t k = 0; k < 4; k++)
+        if (4 * i + k < n) v |= (uint32_t)src[4 * i + k] << (8 * k);
+      win[i] = v;
+    }
+  }
+  if (threadIdx.x == 0) next = 0;
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63u;
+  SwRec* const R = ring[threadIdx.x >> 6];
+  const uint32_t budget = (uint32_t)chain, budget_s = (uint32_t)chain >> 2;
+  const uint32_t nchunks = (m + 63) / 64;
+  // Member j's record lives in ring slot j mod 128 and again 128 slots later,
+  // so that a block's 64 steps read slots base .. base + 63 without wrapping.
+  auto put_rec = [&](int j, SwRec r) {
+    const uint32_t i = (uint32_t)j & (ZS_SW_RING - 1);
+    R[i] = r;
+    R[i + ZS_SW_RING] = r;
+  };
+  auto load_rec = [&](int j) {  // key 0 = no member: fails every liveness test
+    SwRec r = {0, 0, 0, 0};
+    if (j >= 0 && (uint32_t)j < m) {
+      const uint32_t q = mem[j];
+      r.w0 = sw_word(win, q);
+      r.w1 = sw_word(win, q + 4);
+      r.w2 = sw_word(win, q + 8);
+      r.key = (sw_hash(r.w0) << 16) | q;
+    }
+    put_rec(j, r);
+  };
+  for (;;) {
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&next, 1u);
+    c = __builtin_amdgcn_readfirstlane(c);
+    if (c >= nchunks) break;
+    const int k0 = (int)(64 * c);
+    const int k = k0 + (int)lane;
+    const bool own = (uint32_t)k < m;
+    const uint32_t p = own ? mem[k] : 0u;
+    const uint32_t s0 = sw_word(win, p), s1 = sw_word(win, p + 4), s2 = sw_word(win, p + 8);
+    const uint32_t h = sw_hash(s0);
+    const uint32_t look = n - p;
+    const uint32_t maxc = look < ZS_MAX_MATCH ? look : ZS_MAX_MATCH;                 // deflate.ts:1068
+    const uint32_t nice = look < (uint32_t)nice_cfg ? look : (uint32_t)nice_cfg;      // deflate.ts:1078-1080
+    const uint32_t kcap = 8u * (maxc < 12u ? maxc : 12u);
+    const uint32_t long_thr = maxc > 12u ? 12u : 13u;
+    const uint32_t limit = p > ZS_MAX_DIST ? p - ZS_MAX_DIST : 0u;                   // deflate.ts:1060
+    const uint32_t khead = (h << 16) | (limit > 1u ? limit : 1u);
+    const uint32_t klim = (h << 16) | limit;
+    // ring: this chunk's block and the one before it
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    put_rec(k, own ? SwRec{s0, s1, s2, (h << 16) | p} : SwRec{0, 0, 0, 0});
+    load_rec(k - 64);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+
+    uint32_t best = 2u << 16, best_s = 2u << 16;
+    uint32_t nl = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;  // long candidates: t << 16 | pos, in chain order
+    bool ovf = false, alive = false;
+    uint32_t head = 0;  // bit 0: head candidate valid; 0x8000: at exactly MAX_DIST
+    auto note_long = [&](uint32_t t, uint32_t key) {
+      if (nl == 4) {  // a fifth: the lane stops and re-walks its chain afterwards
+        ovf = true;
+        alive = false;
+      } else {
+        const uint32_t e = (t << 16) | (key & 0xffffu);
+        l0 = nl == 0 ? e : l0;
+        l1 = nl == 1 ? e : l1;
+        l2 = nl == 2 ? e : l2;
+        l3 = nl == 3 ? e : l3;
+        nl++;
+      }
+    };
+    // t = 1: the head candidate (deflate.ts:1376)
+    {
+      const SwRec r = R[(uint32_t)(k - 1) & (ZS_SW_RING - 1)];
+      if (own && r.key >= khead) {
+        alive = true;
+        head = 1u | ((p - (r.key & 0xffffu)) == ZS_MAX_DIST ? 0x8000u : 0u);
+        const uint32_t kk = sw_lcp(r.w0, r.w1, r.w2, s0, s1, s2, kcap);
+        if (kk >= long_thr) note_long(1, r.key);
+        best = max(best, (kk << 16) | (0xffffu - 1u));
+      }
+    }
+    // One chain step for every lane: a dead lane's result simply stops
+    // changing (no per-step exit, no exec-mask bookkeeping).
+    auto step = [&](const uint4 r, uint32_t t, bool& lng) {
+      alive = alive & (r.w > klim);  // the chain ends at the first dead step (deflate.ts:1109)
+      const uint32_t kk = sw_lcp(r.x, r.y, r.z, s0, s1, s2, kcap);
+      const uint32_t sc = max(best, (kk << 16) | (0xffffu - t));
+      best = alive ? sc : best;
+      lng = lng | (alive & (kk >= long_thr));
+    };
+    // Long candidates are rare (~1 % of groups): a group with one is re-run
+    // step by step to record them in chain order.
+    auto relong = [&](const SwRec* Rg, uint32_t t0, uint32_t cnt, bool al) {
+      for (uint32_t u = 0; u < cnt; u++) {
+        const SwRec r = Rg[-(int)u];
+        al = al && r.key > klim;
+        if (al && sw_lcp(r.w0, r.w1, r.w2, s0, s1, s2, kcap) >= long_thr) {
+          note_long(t0 + u, r.key);
+          if (ovf) al = false;
+        }
+      }
+    };
+    // Steps 2..4 (block 0, before the first full group).
+    {
+      const SwRec* const Rg = R + (((uint32_t)(k - 64) & (ZS_SW_RING - 1)) + 64u - 2u);
+      const bool alive0 = alive;
+      bool lng = false;
+      for (uint32_t u = 0; u < 3; u++) step(*(const uint4*)(Rg - (int)u), 2u + u, lng);
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(lng) != 0, 0)) relong(Rg, 2u, 3u, alive0);
+    }
+    // Steps [ta, tb] of block b in groups of four (ta = 1 mod 4, tb = 0 mod 4,
+    // wave-uniform).  Step t reads slot base_b + 64b + 64 - t: one address per
+    // group, immediate offsets inside, all four records loaded up front.
+    auto run = [&](uint32_t b, uint32_t ta, uint32_t tb) {
+      const uint32_t base_b = (uint32_t)(k - 64 * (int)b - 64) & (ZS_SW_RING - 1);
+      const SwRec* const Rb = R + base_b + 64u * b + 64u;
+      for (uint32_t t0 = ta; t0 <= tb; t0 += 4) {
+        const SwRec* const Rg = Rb - t0;  // step t0 + u reads Rg[-u]
+        const uint4 r0 = *(const uint4*)(Rg), r1 = *(const uint4*)(Rg - 1), r2 = *(const uint4*)(Rg - 2),
+                    r3 = *(const uint4*)(Rg - 3);
+        const bool alive0 = alive;
+        bool lng = false;
+        step(r0, t0, lng);
+        step(r1, t0 + 1, lng);
+        step(r2, t0 + 2, lng);
+        step(r3, t0 + 3, lng);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(lng) != 0, 0)) relong(Rg, t0, 4u, alive0);
+        if (!__builtin_amdgcn_ballot_w64(alive)) break;
+      }
+    };
+    bool snapped = false;
+    for (uint32_t b = 0;; b++) {
+      // block b = steps (64b, 64b + 64]: members k0 - 64b - 64 ... k0 - 64b + 62, i.e. the blocks b and b + 1 back
+      if (b >= 1) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        load_rec(k - 64 * (int)(b + 1));
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+      const uint32_t ta = b == 0 ? 5u : 64u * b + 1u;
+      const uint32_t tb = min(64u * b + 64u, budget);
+      if (!snapped && budget_s <= tb) {  // the chain >> 2 result (deflate.ts:1075-1077); budgets are multiples of 4
+        if (budget_s >= ta) run(b, ta, budget_s);
+        best_s = best;
+        snapped = true;
+        if (budget_s + 1u <= tb) run(b, max(ta, budget_s + 1u), tb);
+      } else {
+        run(b, ta, tb);
+      }
+      if (tb >= budget || !__builtin_amdgcn_ballot_w64(alive)) break;
+    }
+    if (!snapped) best_s = best;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    if (own) {
+      uint32_t rx = 0, ry = 0;
+      if (head) {
+        const uint32_t bl = best >> 16, bsl = best_s >> 16;
+        uint32_t bd = bl > 2u ? p - mem[k - (int)(0xffffu - (best & 0xffffu))] : 0u;
+        uint32_t bsd = bsl > 2u ? p - mem[k - (int)(0xffffu - (best_s & 0xffffu))] : 0u;
+        uint32_t L = bl, Ls = bsl;
+        if (nl) {
+          uint32_t lb = 0, ld = 0, lbs = 0, lds = 0;
+          auto take = [&](uint32_t t, uint32_t q) -> bool {
+            const uint32_t len = sw_extend(win, p, q, maxc);
+            if (len > lb) { lb = len; ld = p - q; }
+            if (t <= budget_s && len > lbs) { lbs = len; lds = p - q; }
+            return len >= nice;  // nice match: the walk ends (deflate.ts:1103)
+          };
+          if (ovf) {  // re-walk the chain from the first long candidate
+            for (uint32_t t = l0 >> 16; t <= budget && (int)t <= k; t++) {
+              const uint32_t q = mem[k - (int)t];
+              const uint32_t w0 = sw_word(win, q), w1 = sw_word(win, q + 4), w2 = sw_word(win, q + 8);
+              const uint32_t key = (sw_hash(w0) << 16) | q;
+              if (t == 1u ? key < khead : key <= klim) break;
+              if (sw_lcp(w0, w1, w2, s0, s1, s2, kcap) < long_thr) continue;
+              if (take(t, q)) break;
+            }
+          } else {
+            if (!take(l0 >> 16, l0 & 0xffffu) && nl > 1 && !take(l1 >> 16, l1 & 0xffffu) && nl > 2 &&
+                !take(l2 >> 16, l2 & 0xffffu) && nl > 3)
+              take(l3 >> 16, l3 & 0xffffu);
+          }
+          L = lb;
+          bd = ld;
+          if (lbs) { Ls = lbs; bsd = lds; }
+        }
+        rx = (L << 16) | (L > 2u ? bd : 0u) | (head & 0x8000u);
+        ry = (Ls << 16) | (Ls > 2u ? bsd : 0u);
+      }
+      out[p] = make_uint2(rx, ry);
+    }
+  }
+}

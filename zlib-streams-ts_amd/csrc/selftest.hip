@@ -1,7 +1,7 @@
 // selftest.hip -- run-time check of the one hardware property the chain
 // builder (zs_k_prev, deflate_match.hip) relies on beyond the ISA manual:
 // same-address LDS atomics (ds_wrxchg_rtn_b32, ds_mskor_rtn_b32 on 16-bit
-// halves, and ds_add_rtn_u32) issued by
+// halves, and ds_add_rtn_u32 on whole words and on 16-bit halves) issued by
 // ONE wave instruction are applied in increasing lane order on gfx950.  Probed
 // off-line (tools/probes/lds_atomic_order.hip, lds_atomic_add_order.hip); the
 // context re-checks it at creation so a part that behaves differently fails
@@ -21,10 +21,11 @@ __global__ __launch_bounds__(64) void zs_k_selftest(uint32_t* __restrict__ bad, 
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t keys[64];
   __shared__ uint32_t half[128];  // 256 u16 buckets, two per word (zs_k_prev16)
+  __shared__ uint32_t hcnt[128];  // 256 u16 counters, two per word (zs_k_bucket)
   const uint32_t lane = threadIdx.x;
   const uint32_t mask = (blockIdx.x & 3u) == 0 ? 0u : (blockIdx.x & 3u) == 1 ? 3u : (blockIdx.x & 3u) == 2 ? 15u : 255u;
   for (uint32_t i = lane; i < 256; i += 64) { tab[i] = 0; cnt[i] = 0; }
-  for (uint32_t i = lane; i < 128; i += 64) half[i] = 0;
+  for (uint32_t i = lane; i < 128; i += 64) { half[i] = 0; hcnt[i] = 0; }
   __syncthreads();
   uint32_t errs = 0;
   for (int r = 0; r < rounds; r++) {
@@ -32,11 +33,16 @@ __global__ __launch_bounds__(64) void zs_k_selftest(uint32_t* __restrict__ bad, 
     keys[lane] = k;
     const uint32_t sh = 16u * (k & 1u);
     const uint32_t before_x = tab[k], before_c = cnt[k], before_h = (half[k >> 1] >> sh) & 0xffffu;
+    const uint32_t before_hc = (hcnt[k >> 1] >> sh) & 0xffffu;
     __syncthreads();
     const uint32_t val = 1 + lane + 64u * (uint32_t)r;
     const uint32_t old_x = atomicExch(&tab[k], val);
     const uint32_t old_c = atomicAdd(&cnt[k], 1u);
-    uint32_t old_w;
+    uint32_t old_w, old_hc;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(old_hc)
+                 : "v"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&hcnt[k >> 1]), "v"(1u << sh)
+                 : "memory");
     asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
                  : "=v"(old_w)
                  : "v"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&half[k >> 1]),
@@ -51,6 +57,7 @@ __global__ __launch_bounds__(64) void zs_k_selftest(uint32_t* __restrict__ bad, 
     if (old_x != (lower ? last_lower : before_x)) errs++;
     if (old_c != before_c + lower) errs++;
     if (((old_w >> sh) & 0xffffu) != (lower ? (last_lower & 0xffffu) : before_h)) errs++;
+    if (((old_hc >> sh) & 0xffffu) != ((before_hc + lower) & 0xffffu)) errs++;
     __syncthreads();
   }
   if (errs) atomicAdd(bad, errs);

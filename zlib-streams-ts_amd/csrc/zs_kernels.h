@@ -35,7 +35,12 @@ __global__ void zs_k_prev(const uint8_t* in, const uint64_t* in_off, const uint3
 __global__ void zs_k_prev16(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                             uint16_t* prevd);
 __global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                           const uint16_t* prevd, uint2* mres, int chain, int nice);
+                           const uint16_t* prevd, uint2* mres, int chain, int nice, uint32_t min_len);
+// levels 4..9, streams of at most 65,537 bytes (deflate_sweep.hip)
+__global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                            uint16_t* members, uint2* mres);
+__global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                           const uint16_t* members, uint2* mres, int chain, int nice);
 __global__ void zs_k_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint32_t* blk_base, const uint2* mres, uint32_t* syms, zs_block* blocks,
                            zs_stream* streams, uint32_t* scratch, int good, int lazy);

@@ -105,6 +105,8 @@ def lib():
     L.zs_corpus.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P, ctypes.c_int]
     L.zs_selftest.argtypes = [_P, _U64P]
     L.zs_set_option.argtypes = [_P, ctypes.c_char_p, ctypes.c_int]
+    L.zs_debug_fetch.restype = ctypes.c_uint64
+    L.zs_debug_fetch.argtypes = [_P, ctypes.c_int, ctypes.c_uint32, _P, ctypes.c_uint64]
     _lib = L
     return L
 
@@ -159,9 +161,16 @@ class Engine:
         return self._ctx
 
     def set_option(self, name: str, value: int):
-        """zs_set_option: "timing", "inflate_fast" (see zs_gpu.h)."""
+        """zs_set_option: "timing", "inflate_fast", "check_phases", "match_sweep" (see zs_gpu.h)."""
         if self._L.zs_set_option(self._ctx, name.encode(), int(value)) != 0:
             raise ZsError(self._L.zs_last_error().decode())
+
+    def debug_fetch(self, what: int, stream: int, nbytes: int) -> bytes:
+        """zs_debug_fetch: an intermediate array of `stream` from the last deflate batch
+        (0 links/members u16, 1 match table u32x2 per position, 2 symbols, ...)."""
+        buf = ctypes.create_string_buffer(max(1, nbytes))
+        k = self._L.zs_debug_fetch(self._ctx, what, stream, buf, nbytes)
+        return buf.raw[:k]
 
     def set_timing(self, on: bool):
         self._L.zs_set_timing(self._ctx, 1 if on else 0)
