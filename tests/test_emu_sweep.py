@@ -1,0 +1,56 @@
+"""CPU check of the L4..L9 match finder's algorithm for streams of <= 65,537
+bytes (tools/emu/emu_bucket_sweep.c models zs_k_bucket + zs_k_sweep of
+deflate_sweep.hip): the counting sort by (hash, position), the lock-step
+sweep over bucket predecessors with 12-byte signatures, the liveness keys,
+the chain >> 2 snapshot and the deferred long candidates (with the re-walk
+after a fifth) reproduce a direct longest_match (deflate.ts:1053-1115) at
+every position, for both budgets and the slide-NIL flag, at the level
+configurations of deflate.ts:84-100 (L4..L9).  No GPU needed; the kernels
+themselves are checked against the chain-walk kernel and the oracle by
+tests/test_gpu_deflate.py (test_sweep_match_table_equals_chain_walk)."""
+import os
+import shutil
+import struct
+import subprocess
+
+import pytest
+
+import corpus
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tools", "emu", "emu_bucket_sweep.c")
+
+# (chain, nice) per level, deflate.ts:84-100 configuration_table
+LEVELS = {4: (16, 16), 5: (32, 32), 6: (128, 128), 7: (256, 128), 8: (1024, 258), 9: (4096, 258)}
+
+
+@pytest.fixture(scope="module")
+def emu(tmp_path_factory):
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    exe = str(tmp_path_factory.mktemp("emu") / "emu_bucket_sweep")
+    subprocess.run(["gcc", "-O2", "-o", exe, SRC], check=True)
+    return exe
+
+
+def _streams():
+    specs = [("text", 65536), ("mixed", 65536), ("rand", 40000), ("zeros", 65536), ("ramp", 65536),
+             ("text", 3), ("text", 4), ("text", 13), ("text", 259), ("mixed", 1000), ("text", 32769),
+             ("text", 65535), ("text", 65537), ("zeros", 65537)]
+    out = [corpus.make({"kind": k, "n": n, "seed": 7000 + i}) for i, (k, n) in enumerate(specs)]
+    b = bytearray(corpus.rand(77, 65536))  # a head candidate at exactly MAX_DIST
+    b[40000:40020] = b[40000 - 32506:40000 - 32506 + 20]
+    out.append(bytes(b))
+    return out
+
+
+@pytest.mark.parametrize("level", sorted(LEVELS))
+def test_sweep_model_matches_longest_match(emu, tmp_path, level):
+    streams = _streams()
+    blob = struct.pack("<I", len(streams)) + struct.pack("<%dI" % len(streams), *map(len, streams)) + b"".join(streams)
+    f = tmp_path / "streams.bin"
+    f.write_bytes(blob)
+    chain, nice = LEVELS[level]
+    r = subprocess.run([emu, str(f), str(chain), str(nice)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout, r.stdout
