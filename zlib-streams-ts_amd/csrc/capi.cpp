@@ -334,7 +334,7 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
     if (c->match_sweep) {
       // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
       // longer ones: chain links + per-tile chain walk (deflate_match.hip)
-      zs_k_bucket<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
+      zs_k_bucket<<<n, 256, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
       if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
       MARK("prev");
       zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),

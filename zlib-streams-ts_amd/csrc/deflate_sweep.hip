@@ -44,7 +44,6 @@
 #include "zs_kernels.h"
 
 #define ZS_SWEEP_MAX 65537u  // position + 1 <= 65535 for every inserted position: u16 members and offsets
-#define ZS_BK_STAGE 4096u
 #define ZS_SW_WIN_WORDS ((ZS_SWEEP_MAX + 20u + 3u) / 4u + 2u)
 #define ZS_SW_RING 128u  // records per wave (two blocks of 64 members), stored twice (mirror)
 
@@ -57,97 +56,145 @@ static __device__ __forceinline__ uint32_t sw_hash(uint32_t w) {  // SURVEY A1, 
   return (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
 }
 
-// Stages input bytes [c0, c0 + ZS_BK_STAGE + 8) of one stream into stg (one wave).
-static __device__ __forceinline__ void sw_stage(uint32_t* stg, const uint8_t* src, uint32_t n, uint32_t c0,
-                                                bool aligned, uint32_t lane) {
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  for (uint32_t i = lane; i < ZS_BK_STAGE / 4 + 2; i += 64) {
-    const uint32_t at = c0 + 4 * i;
-    uint32_t v = 0;
-    if (aligned && at + 4 <= n) {
-      v = *(const uint32_t*)(src + at);
-    } else {
-      for (uint32_t k = 0; k < 4; k++)
-        if (at + k < n) v |= (uint32_t)src[at + k] << (8 * k);
-    }
-    stg[i] = v;
+// -------------------------------------------------------------- zs_k_bucket
+// One workgroup (4 waves) per stream: a counting sort of the inserted
+// positions p <= n-3 by their hash, stable in position, into members[] (u16,
+// the stream's range of the per-position workspace).  Pass 1 counts (32768 u16
+// buckets, two per LDS word; all four waves), an exclusive scan turns the
+// counts into offsets, and pass 2 -- one wave -- walks the positions in order,
+// 64 per instruction, claiming slots with ONE ds_add_rtn_u32 per lane: gfx950
+// applies same-address LDS atomics of one wave instruction in increasing lane
+// order (zs_selftest checks it, including the 16-bit half form used here), so
+// equal hashes get slots in position order.  Hashes come straight from global
+// memory (a 4-byte window per lane, two aligned loads).  Results of the
+// positions that are not inserted (the last two) are zeroed.
+#define ZS_BK_THREADS 256u
+#define ZS_BK_INFLIGHT 8  // pass 2: wave instructions (x 64 positions) per wait
+#define ZS_BK_CHUNK 4096u  // pass 2: input bytes staged in LDS at a time
+
+// hash of position p (p + 2 < n); src4 = the stream's bytes as aligned words (a
+// word past n is never used for a valid p: p + 2 < n reads at most word (n-1)/4)
+static __device__ __forceinline__ uint32_t bk_hash_at(const uint8_t* src, uint32_t p, uint32_t n, bool aligned) {
+  uint32_t w;
+  if (aligned) {
+    const uint32_t* s4 = (const uint32_t*)src;
+    const uint32_t i = p >> 2;
+    const uint32_t lo = s4[i];
+    const uint32_t hi = (4 * i + 4 < n) ? s4[i + 1] : 0u;
+    w = __builtin_amdgcn_alignbyte(hi, lo, p & 3u);
+  } else {
+    w = (uint32_t)src[p] | ((uint32_t)src[p + 1] << 8) | ((uint32_t)src[p + 2] << 16);
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
+  return sw_hash(w);
 }
 
-// -------------------------------------------------------------- zs_k_bucket
-// One wave per stream: a counting sort of the inserted positions p <= n-3 by
-// their hash, stable in position, into members[] (u16, the stream's range of
-// the per-position workspace).  Pass 1 counts (32768 u16 buckets, two per LDS
-// word), an exclusive scan turns the counts into offsets, pass 2 walks the
-// positions in order, 64 per instruction, and claims slots with ONE
-// ds_add_rtn_u32 per lane: gfx950 applies same-address LDS atomics of one wave
-// instruction in increasing lane order (zs_selftest checks it, including the
-// 16-bit half form used here), so equal hashes get slots in position order.
-// Results of the positions that are not inserted (the last two) are zeroed.
-__global__ __launch_bounds__(64) void zs_k_bucket(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                  const uint32_t* __restrict__ in_len,
-                                                  const uint64_t* __restrict__ pos_base, uint16_t* __restrict__ members,
-                                                  uint2* __restrict__ mres) {
+__global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __restrict__ in,
+                                                            const uint64_t* __restrict__ in_off,
+                                                            const uint32_t* __restrict__ in_len,
+                                                            const uint64_t* __restrict__ pos_base,
+                                                            uint16_t* __restrict__ members, uint2* __restrict__ mres) {
   __shared__ uint32_t cnt[16384];
-  __shared__ uint32_t stg[ZS_BK_STAGE / 4 + 2];
+  __shared__ uint32_t part[ZS_BK_THREADS];
+  __shared__ uint32_t stg[ZS_BK_CHUNK / 4 + 2];
   const int s = blockIdx.x;
   const uint32_t n = in_len[s];
   if (n > ZS_SWEEP_MAX) return;  // zs_k_prev / zs_k_match's stream
-  const uint32_t lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x;
   const uint8_t* src = in + in_off[s];
   uint16_t* mem = members + pos_base[s];
   uint2* out = mres + pos_base[s];
   const uint32_t m = n > 2 ? n - 2 : 0u;  // inserted positions (deflate.ts:1367-1370)
-  for (uint32_t p = m + lane; p < n; p += 64) out[p] = make_uint2(0, 0);
+  for (uint32_t p = m + tid; p < n; p += ZS_BK_THREADS) out[p] = make_uint2(0, 0);
   if (m == 0) return;
-  for (uint32_t i = lane; i < 16384; i += 64) cnt[i] = 0;
+  for (uint32_t i = tid; i < 16384; i += ZS_BK_THREADS) cnt[i] = 0;
   const bool aligned = ((uintptr_t)src & 3u) == 0;
-  // pass 1: bucket sizes
-  for (uint32_t c0 = 0; c0 < m; c0 += ZS_BK_STAGE) {
-    sw_stage(stg, src, n, c0, aligned, lane);
-    const uint32_t c1 = min(m, c0 + ZS_BK_STAGE);
-    for (uint32_t p = c0 + lane; p < c1; p += 64) {
-      const uint32_t o = p - c0;
-      const uint32_t h = sw_hash(__builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u));
-      atomicAdd(&cnt[h >> 1], 1u << (16u * (h & 1u)));
+  __syncthreads();
+  // pass 1: bucket sizes (unordered adds, all waves)
+  for (uint32_t p0 = 0; p0 < m; p0 += 4 * ZS_BK_THREADS) {
+    uint32_t h[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t p = p0 + ZS_BK_THREADS * j + tid;
+      h[j] = p < m ? bk_hash_at(src, p, n, aligned) : 0xffffffffu;
     }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (h[j] != 0xffffffffu) atomicAdd(&cnt[h[j] >> 1], 1u << (16u * (h[j] & 1u)));
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  // exclusive scan: lane i owns words [256i, 256i + 256) (buckets 512i ...)
+  __syncthreads();
+  // exclusive scan: thread i owns words [64i, 64i + 64) (buckets 128i ...)
   {
     uint32_t sum = 0;
-    for (uint32_t j = 0; j < 256; j++) {
-      const uint32_t w = cnt[256 * lane + ((j + lane) & 255u)];  // rotated: lanes hit different banks
+    for (uint32_t j = 0; j < 64; j++) {
+      const uint32_t w = cnt[64 * tid + ((j + tid) & 63u)];  // rotated: threads hit different banks
       sum += (w & 0xffffu) + (w >> 16);
     }
-    uint32_t x = sum;
+    part[tid] = sum;
+    __syncthreads();
+    if (tid < 64) {  // scan of the 256 partial sums, one wave
+      uint32_t v[4], t = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(x, d, 64);
-      if (lane >= (uint32_t)d) x += y;
+      for (int j = 0; j < 4; j++) { v[j] = part[4 * tid + j]; t += v[j]; }
+      uint32_t x = t;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (tid >= (uint32_t)d) x += y;
+      }
+      uint32_t run = x - t;
+#pragma unroll
+      for (int j = 0; j < 4; j++) { part[4 * tid + j] = run; run += v[j]; }
     }
-    uint32_t run = x - sum;
-    for (uint32_t j = 0; j < 256; j++) {
-      const uint32_t w = cnt[256 * lane + j];
+    __syncthreads();
+    uint32_t run = part[tid];
+    for (uint32_t j = 0; j < 64; j++) {
+      const uint32_t i = 64 * tid + ((j + tid) & 63u);
+      (void)i;
+      const uint32_t w = cnt[64 * tid + j];
       const uint32_t lo = w & 0xffffu;
-      cnt[256 * lane + j] = run | ((run + lo) << 16);
+      cnt[64 * tid + j] = run | ((run + lo) << 16);
       run += lo + (w >> 16);
     }
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  // pass 2: ordered scatter, four instructions (256 positions) per wait
-  for (uint32_t c0 = 0; c0 < m; c0 += ZS_BK_STAGE) {
-    sw_stage(stg, src, n, c0, aligned, lane);
-    const uint32_t c1 = min(m, c0 + ZS_BK_STAGE);
-    for (uint32_t g0 = c0; g0 < c1; g0 += 256) {
-      uint32_t a[4], v[4], sh[4], e[4];
+  __syncthreads();
+  if (tid >= 64) return;
+  // pass 2: ordered scatter by wave 0.  The input goes through LDS 4 KiB at a
+  // time (stg, the pass-1 partial sums' neighbour), the next chunk's loads in
+  // flight in registers while this chunk's positions are claimed,
+  // ZS_BK_INFLIGHT instructions per wait.
+  const uint32_t lane = tid;
+  constexpr uint32_t CW = ZS_BK_CHUNK / 4 / 64;  // words per lane per chunk
+  uint32_t nxt[CW + 1];
+  auto fetch = [&](uint32_t c0) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+    for (uint32_t i = 0; i <= CW; i++) {
+      const uint32_t w = 64 * i + lane;  // word index within the chunk (+ 2 words of overlap)
+      const uint32_t at = c0 + 4 * w;
+      uint32_t v = 0;
+      if (w < ZS_BK_CHUNK / 4 + 2) {
+        if (aligned && at + 4 <= n) v = *(const uint32_t*)(src + at);
+        else
+          for (uint32_t k = 0; k < 4; k++)
+            if (at + k < n) v |= (uint32_t)src[at + k] << (8 * k);
+      }
+      nxt[i] = v;
+    }
+  };
+  fetch(0);
+  for (uint32_t c0 = 0; c0 < m; c0 += ZS_BK_CHUNK) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t i = 0; i <= CW; i++)
+      if (64 * i + lane < ZS_BK_CHUNK / 4 + 2) stg[64 * i + lane] = nxt[i];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    if (c0 + ZS_BK_CHUNK < m) fetch(c0 + ZS_BK_CHUNK);
+    const uint32_t c1 = min(m, c0 + ZS_BK_CHUNK);
+    for (uint32_t g0 = c0; g0 < c1; g0 += 64 * ZS_BK_INFLIGHT) {
+      uint32_t a[ZS_BK_INFLIGHT], v[ZS_BK_INFLIGHT], sh[ZS_BK_INFLIGHT], e[ZS_BK_INFLIGHT];
+#pragma unroll
+      for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
         const uint32_t p = g0 + 64 * j + lane;
         const uint32_t o = p - c0;
         const uint32_t h = sw_hash(__builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u));
@@ -155,18 +202,23 @@ __global__ __launch_bounds__(64) void zs_k_bucket(const uint8_t* __restrict__ in
         a[j] = sw_lds_addr(&cnt[h >> 1]);
         v[j] = p < c1 ? 1u << sh[j] : 0u;  // a lane past the chunk adds nothing
       }
-      // in order: group j's adds land after group j-1's (LDS executes a wave's ops in order)
+      // in order: instruction j's adds land after instruction j-1's (LDS executes a wave's ops in order)
       asm volatile(
-          "ds_add_rtn_u32 %0, %4, %8\n\t"
-          "ds_add_rtn_u32 %1, %5, %9\n\t"
-          "ds_add_rtn_u32 %2, %6, %10\n\t"
-          "ds_add_rtn_u32 %3, %7, %11\n\t"
+          "ds_add_rtn_u32 %0, %8, %16\n\t"
+          "ds_add_rtn_u32 %1, %9, %17\n\t"
+          "ds_add_rtn_u32 %2, %10, %18\n\t"
+          "ds_add_rtn_u32 %3, %11, %19\n\t"
+          "ds_add_rtn_u32 %4, %12, %20\n\t"
+          "ds_add_rtn_u32 %5, %13, %21\n\t"
+          "ds_add_rtn_u32 %6, %14, %22\n\t"
+          "ds_add_rtn_u32 %7, %15, %23\n\t"
           "s_waitcnt lgkmcnt(0)"
-          : "=&v"(e[0]), "=&v"(e[1]), "=&v"(e[2]), "=&v"(e[3])
-          : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3])
+          : "=&v"(e[0]), "=&v"(e[1]), "=&v"(e[2]), "=&v"(e[3]), "=&v"(e[4]), "=&v"(e[5]), "=&v"(e[6]), "=&v"(e[7])
+          : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(v[0]),
+            "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7])
           : "memory");
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+      for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
         const uint32_t p = g0 + 64 * j + lane;
         if (p < c1) mem[(e[j] >> sh[j]) & 0xffffu] = (uint16_t)p;
       }
