@@ -128,7 +128,11 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * decode members lane-per-member and re-run only those that do not end cleanly
  * on the exact stream-layer state machine (0: exact path for every member);
  * "check_phases" (default 0): synchronise after every kernel phase and fail
- * with ZS_MEM_ERROR naming the phase whose launch or execution failed. */
+ * with ZS_MEM_ERROR naming the phase whose launch or execution failed;
+ * "match_sweep" (default 1): levels 4..9, streams <= 65,537 B find matches by
+ * a counting sort by hash + lock-step sweep (0: chain links + per-tile walk);
+ * "parse_split" (default 0): levels 4..9 parse as per-range + per-stream
+ * kernels (0: one wave per stream).  Options never change output bytes. */
 int zs_set_option(zs_ctx *ctx, const char *name, int value);
 
 /* Introspection for tests: copy an intermediate array of stream s of the last

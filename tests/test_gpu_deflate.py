@@ -90,6 +90,38 @@ def test_sweep_match_table_equals_chain_walk(engine, level):
         assert outs[0][i] == outs[1][i] and outs[0][i][1] == oracle.compress(d, level, "deflate-raw")[1], (i, len(d))
 
 
+@pytest.mark.parametrize("level", [4, 6, 9])
+def test_split_parse_equals_one_wave_parse(engine, level):
+    """zs_k_parse_a + zs_k_parse_b (ranges of 4096 positions, lane merges, joins,
+    serial fallbacks) produce the same symbols and output bytes as the one-wave
+    zs_k_parse, including repetitive data (matches longer than a segment or a
+    range) and streams ending inside a match."""
+    rng = random.Random(900 + level)
+    inputs = []
+    for k in range(24):
+        n = rng.choice([0, 1, 2, 3, 63, 64, 65, 4095, 4096, 4097, 8191, 8192, 12000, 65536, 65537, 100000, 262144,
+                        rng.randrange(1, 300000)])
+        kind = rng.choice(["text", "mixed", "rand", "zeros", "ramp", "text"])
+        inputs.append(corpus.make({"kind": kind, "n": n, "seed": rng.randrange(1 << 32)}))
+    # long runs crossing segment and range boundaries inside text
+    t = bytearray(corpus.text(5, 70000))
+    t[4000:4700] = bytes(700)
+    t[8100:8300] = t[100:300]
+    t[20000:20600] = t[20000 - 300:20300] + t[20000 - 300:20300]
+    inputs.append(bytes(t))
+    outs, symtabs = [], []
+    try:
+        for split in (1, 0):
+            engine.set_option("parse_split", split)
+            outs.append(engine.compress_batch_raw(inputs, "deflate-raw", level))
+            symtabs.append([engine.debug_fetch(2, i, 4 * (len(d) + 1)) for i, d in enumerate(inputs)])
+    finally:
+        engine.set_option("parse_split", 0)
+    for i, d in enumerate(inputs):
+        assert symtabs[0][i] == symtabs[1][i], (i, len(d))
+        assert outs[0][i] == outs[1][i] and outs[0][i][1] == oracle.compress(d, level, "deflate-raw")[1], (i, len(d))
+
+
 def test_output_capacity_too_small_reports_buf_error(engine):
     import ctypes
     import zsamd

@@ -85,7 +85,8 @@ struct zs_ctx {
   // workspace
   Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
   bool inflate_fast = true;
-  bool match_sweep = true;  // L4..9 streams <= 65537 B: bucket sort + sweep (0: chain links + walk)
+  bool match_sweep = true;
+  bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)  // L4..9 streams <= 65537 B: bucket sort + sweep (0: chain links + walk)
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res, d_pack;
   HostBuf h_in, h_out;
@@ -214,6 +215,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "inflate_fast")) c->inflate_fast = value != 0;
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
+  else if (!strcmp(name, "parse_split")) c->parse_split = value != 0;
   else return fail(ZS_STREAM_ERROR, "unknown option %s", name);
   return ZS_OK;
 }
@@ -233,9 +235,9 @@ uint64_t zs_deflate_bound(uint64_t n, int wbits) {  // deflate.ts:615-674, memLe
 
 }  // extern "C"
 
-// Device metadata block: in_off | in_len | out_off | out_cap | pos_base | blk_base
+// Device metadata block: in_off | in_len | out_off | out_cap | pos_base | blk_base | range_base
 struct MetaLayout {
-  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, bytes;
+  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, range_base, bytes;
   explicit MetaLayout(uint32_t n) {
     size_t o = 0;
     auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~size_t(255); return r; };
@@ -245,6 +247,7 @@ struct MetaLayout {
     out_cap = take(4ull * n);
     pos_base = take(8ull * n);
     blk_base = take(4ull * n);
+    range_base = take(4ull * n);
     bytes = o;
   }
 };
@@ -288,12 +291,15 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   memcpy(hm + ml.out_cap, out_cap, 4ull * n);
   uint64_t* pos_base = (uint64_t*)(hm + ml.pos_base);
   uint32_t* blk_base = (uint32_t*)(hm + ml.blk_base);
+  uint32_t* range_base = (uint32_t*)(hm + ml.range_base);
   uint64_t P = 0;
-  uint32_t B = 0, max_len = 0, max_blk = 0;
+  uint32_t B = 0, max_len = 0, max_blk = 0, NR = 0;
   for (uint32_t i = 0; i < n; i++) {
     if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
     pos_base[i] = P;
     blk_base[i] = B;
+    range_base[i] = NR;
+    NR += (in_len[i] + ZS_PARSE_RANGE - 1) / ZS_PARSE_RANGE;
     P += ((uint64_t)in_len[i] + 7) & ~7ull;  // per-position tables start 8-aligned (16-B link loads in zs_k_match)
     const uint32_t nb = in_len[i] / ZS_SYM_END + 2;
     B += nb;
@@ -304,7 +310,9 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   HIPCHK(c->prevd.ensure(2 * P + 64));
   HIPCHK(c->mres.ensure(8 * P + 64));
   HIPCHK(c->syms.ensure(4 * (P + n) + 64));
-  if (level >= 4) HIPCHK(c->pscr.ensure(4ull * ZS_PARSE_SEG_WORDS * (P / ZS_PARSE_SEG + n + 1)));
+  if (level >= 4)
+    HIPCHK(c->pscr.ensure(c->parse_split ? 4ull * ZS_PARSE_RANGE_WORDS * (NR + 1)
+                                         : 4ull * ZS_PARSE_SEG_WORDS * (P / ZS_PARSE_SEG + n + 1)));
   HIPCHK(c->blocks.ensure(sizeof(zs_block) * (size_t)B));
   HIPCHK(c->streams.ensure(sizeof(zs_stream) * (size_t)n));
   HIPCHK(c->codes.ensure(4ull * (ZS_L_CODES + ZS_D_CODES) * B));
@@ -318,6 +326,7 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   const uint32_t* d_out_cap = (const uint32_t*)(dm + ml.out_cap);
   const uint64_t* d_pos = (const uint64_t*)(dm + ml.pos_base);
   const uint32_t* d_blk = (const uint32_t*)(dm + ml.blk_base);
+  const uint32_t* d_rng = (const uint32_t*)(dm + ml.range_base);
   zs_stream* d_st = c->streams.as<zs_stream>();
   zs_block* d_bk = c->blocks.as<zs_block>();
   const zs_level_cfg cfg = kLevels[level];
@@ -352,8 +361,17 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
                                                    c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
       MARK("match");
     }
-    zs_k_parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), c->syms.as<uint32_t>(),
-                                 d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
+    if (c->parse_split) {
+      // the lazy parse: per-range speculative parse + merges, then per-stream joins and splice (deflate_parse.hip)
+      if (max_len)
+        zs_k_parse_a<<<dim3((max_len + ZS_PARSE_RANGE - 1) / ZS_PARSE_RANGE, n), 64, 0, st>>>(
+            d_in, d_in_off, d_in_len, d_pos, d_rng, c->mres.as<uint2>(), c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
+      zs_k_parse_b<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, d_rng, c->mres.as<uint2>(),
+                                     c->syms.as<uint32_t>(), d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
+    } else {
+      zs_k_parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(),
+                                   c->syms.as<uint32_t>(), d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
+    }
     MARK("parse");
   } else {
     const int fast_smem = 2 * 32768 * 2;  // head[] + prev[] (u16 x 32 K each)

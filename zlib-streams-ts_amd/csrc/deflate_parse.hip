@@ -29,13 +29,13 @@
 #include <hip/hip_runtime.h>
 #include "zs_common.h"
 #include "zs_kernels.h"
+#include "zs_parse.h"
 
 #define ZS_SEG 1024u                        // positions per speculative segment
 #define ZS_SPEC_SLOTS 1284u                 // >= ZS_SEG + MAX_MATCH - 1 symbols
 #define ZS_SYNC_SLOTS 1028u                 // >= ZS_SEG sync points + sentinel
 #define ZS_FIX_SLOTS 1284u
 #define ZS_SEG_WORDS (ZS_SPEC_SLOTS + ZS_SYNC_SLOTS + ZS_FIX_SLOTS)
-#define ZS_NONE 0xffffffffu
 static_assert(ZS_SPEC_SLOTS % 4 == 0 && ZS_SEG_WORDS % 4 == 0, "16-byte aligned scratch regions");
 static_assert(ZS_SEG == ZS_PARSE_SEG && ZS_SEG_WORDS == ZS_PARSE_SEG_WORDS, "scratch layout shared with capi.cpp");
 
@@ -47,53 +47,6 @@ struct zs_seg_info {
   uint32_t nfix;        // catch-up symbols (true parse) preceding the splice
   uint32_t from;        // first speculative symbol kept (ZS_NONE: none)
 };
-
-struct zs_pstate {
-  uint32_t p, ma, ml, ms;
-};
-
-// One iteration of deflate_slow's loop at position p (deflate.ts:1356-1426),
-// given the match-table entry e of p and the byte in[p-1].  Returns the symbol
-// tallied (ZS_NONE: none).  Symbols: literal = byte, match = 0x80000000 |
-// (len - 3) << 16 | dist.
-static __device__ __forceinline__ uint32_t zs_parse_step(zs_pstate& st, uint2 e, uint32_t lit, uint32_t n, int good,
-                                                         int lazy) {
-  const uint32_t p = st.p, pl = st.ml, pm = st.ms;
-  uint32_t ml = ZS_MIN_MATCH - 1, ms = pm;
-  // head slot emptied by a slide at exactly this position
-  const bool nil =
-      (e.x & 0x8000u) && p >= ZS_SLIDE_AT && ((p - ZS_SLIDE_AT) & 32767u) == 0 && n - p < (uint32_t)ZS_MIN_LOOKAHEAD;
-  if ((e.x >> 16) != 0 && pl < (uint32_t)lazy && !nil) {
-    const uint32_t u = pl >= (uint32_t)good ? e.y : e.x;  // chain >> 2 when prev_length >= good (deflate.ts:1075-1077)
-    const uint32_t L = u >> 16, D = u & 0x7fffu;
-    if (L > pl) {
-      ml = L;
-      ms = p - D;
-      if (L == ZS_MIN_MATCH && D > ZS_TOO_FAR) ml = ZS_MIN_MATCH - 1;  // deflate.ts:1381-1387
-    }
-  }
-  if (pl >= ZS_MIN_MATCH && ml <= pl) {  // emit the previous match (deflate.ts:1389-1411)
-    st.p = p + pl - 1;
-    st.ma = 0;
-    st.ml = ZS_MIN_MATCH - 1;
-    st.ms = ms;
-    return 0x80000000u | ((pl - ZS_MIN_MATCH) << 16) | (p - 1 - pm);
-  }
-  st.ml = ml;
-  st.ms = ms;
-  st.p = p + 1;
-  if (st.ma) return lit;  // deferred literal (deflate.ts:1412-1421)
-  st.ma = 1;
-  return ZS_NONE;
-}
-
-// Number of fill_window slides performed by the time the parse visits v
-// (slide j happens at the first visited position >= T_j with
-// T_j = max(32768 j + 65274, min(n, 32768 j + 65536) - 261), deflate.ts:180-190).
-static __device__ __forceinline__ uint32_t zs_slides(uint32_t v, uint32_t n) {
-  if (n <= v + 261u) return v >= ZS_SLIDE_AT ? (v - ZS_SLIDE_AT) / 32768u + 1u : 0u;
-  return v >= ZS_SLIDE_AT + 1u ? (v - ZS_SLIDE_AT - 1u) / 32768u + 1u : 0u;
-}
 
 __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                  const uint32_t* __restrict__ in_len,

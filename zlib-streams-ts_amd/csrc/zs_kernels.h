@@ -47,6 +47,14 @@ __global__ void zs_k_parse(const uint8_t* in, const uint64_t* in_off, const uint
 // parse scratch words per 1024-position segment (deflate_parse.hip)
 #define ZS_PARSE_SEG 1024u
 #define ZS_PARSE_SEG_WORDS 3596u
+// the two-kernel parse (deflate_parse2.hip): positions per range, scratch words per range
+#define ZS_PARSE_RANGE 2048u
+#define ZS_PARSE_RANGE_WORDS 5376u
+__global__ void zs_k_parse_a(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                             const uint32_t* range_base, const uint2* mres, uint32_t* scratch, int good, int lazy);
+__global__ void zs_k_parse_b(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
+                             const uint32_t* blk_base, const uint32_t* range_base, const uint2* mres, uint32_t* syms,
+                             zs_block* blocks, zs_stream* streams, uint32_t* scratch, int good, int lazy);
 __global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,
                           int lazy, int nice);
