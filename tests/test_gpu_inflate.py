@@ -54,10 +54,19 @@ def test_roundtrip_random_inputs(engine, fmt):
         srcs.append(corpus.make({"kind": rng.choice(["text", "mixed", "rand", "zeros"]), "n": n,
                                  "seed": rng.randrange(1 << 32)}))
     comps = [oracle.compress(s, rng.choice([1, 6, 9]), fmt)[1] for s in srcs]
+    # default: the reference's bytes, including its inflate_fast window-wrap copy (inffast.ts:133-147)
     res = engine.decompress_batch_raw(comps, fmt, out_caps=[len(s) + 64 for s in srcs])
     for s, c, (st, ph, msg, out, cons) in zip(srcs, comps, res):
-        ost, oout, ocons, oph, omsg = oracle.decompress(c, fmt, cap=len(s) + 64, reference_bugs=False)
-        assert st == 1 and out == s and cons == ocons == len(c), (len(s), st, ph, msg)
+        ost, oout, ocons, oph, omsg = oracle.decompress(c, fmt, cap=len(s) + 64)
+        assert (st, ph, msg, out, cons) == (ost, oph, omsg, oout, ocons), (len(s), st, ph, msg)
+    # inflate_ref_wrap = 0: zlib semantics, the source bytes
+    try:
+        engine.set_option("inflate_ref_wrap", 0)
+        res = engine.decompress_batch_raw(comps, fmt, out_caps=[len(s) + 64 for s in srcs])
+    finally:
+        engine.set_option("inflate_ref_wrap", 1)
+    for s, c, (st, ph, msg, out, cons) in zip(srcs, comps, res):
+        assert st == 1 and out == s and cons == len(c), (len(s), st, ph, msg)
 
 
 def test_trailing_garbage_and_second_member_ignored(engine):
@@ -93,12 +102,24 @@ def test_capacity_too_small(engine):
     assert st == -5 and ph == 0 and msg == "output capacity exceeded"
 
 
-def test_inffast_window_wrap_defect_case_decodes_correctly(engine):
+def test_inffast_window_wrap_defect_is_reproduced(engine):
+    """tests/golden/inffast_wrap_defect.json: a 256 KiB M-corpus stream that the
+    reference itself decodes to DIFFERENT bytes than its source (inffast.ts:133-147
+    copies from output[0..] instead of window[0..]).  The engine returns the
+    reference's bytes by default, and the source with inflate_ref_wrap = 0."""
     j = json.load(open(os.path.join(golden_io.GOLDEN, "inffast_wrap_defect.json")))
     src = corpus.make(j["source"])
     comp = oracle.compress(src, 6, "deflate-raw")[1]
+    assert corpus.sha256(comp) == j["compressed_sha256"]
     (st, ph, msg, out, cons), = engine.decompress_batch_raw([comp], "deflate-raw", out_caps=[len(src) + 64])
-    assert st == 1 and out == src  # the reference emits corrupt bytes here (documented divergence)
+    assert st == 1 and len(out) == j["ref_out_len"] and corpus.sha256(out) == j["ref_out_sha256"]
+    assert out != src
+    try:
+        engine.set_option("inflate_ref_wrap", 0)
+        (st, ph, msg, out, cons), = engine.decompress_batch_raw([comp], "deflate-raw", out_caps=[len(src) + 64])
+    finally:
+        engine.set_option("inflate_ref_wrap", 1)
+    assert st == 1 and out == src
 
 
 @pytest.mark.slow

@@ -85,6 +85,7 @@ struct zs_ctx {
   // workspace
   Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
   bool inflate_fast = true;
+  bool inflate_ref_wrap = true;  // reproduce the reference's inflate_fast window-wrap copy (inffast.ts:133-147)
   bool match_sweep = true;
   bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)  // L4..9 streams <= 65537 B: bucket sort + sweep (0: chain links + walk)
   // host staging for the host-buffer entry points
@@ -213,6 +214,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   if (!c || !name) return fail(ZS_STREAM_ERROR, "invalid arguments");
   if (!strcmp(name, "timing")) c->timing = value != 0;
   else if (!strcmp(name, "inflate_fast")) c->inflate_fast = value != 0;
+  else if (!strcmp(name, "inflate_ref_wrap")) c->inflate_ref_wrap = value != 0;
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "parse_split")) c->parse_split = value != 0;
@@ -716,7 +718,8 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
     HIPCHK(c->llen.ensure(8ull * n));
     lres = c->lres.as<zs_lane_res>();
     zs_k_inflate_lane<<<(n + 63) / 64, 64, 0, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
-                                                    (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>());
+                                                    (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
+                                                    c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0);
     MARK("inflate_lane");
     if (wbits > 0) {  // trailer checks over the decoded bytes: adler32 (zlib) / crc32 (gzip)
       uint32_t* chk = c->llen.as<uint32_t>() + n;
@@ -726,7 +729,7 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
     }
   }
   zs_k_inflate<<<n, 64, smem, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
-                                    c->istate.as<zs_inflate_result>(), lres);
+                                    c->istate.as<zs_inflate_result>(), lres, c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0);
   MARK("inflate");
   zs_k_inflate_finish<<<(n + 255) / 256, 256, 0, st>>>(c->istate.as<zs_inflate_result>(), lres, d_status, d_phase,
                                                        d_msg, d_out_len, d_consumed, (int)n);

@@ -18,11 +18,17 @@
 // (w_have) and which stream-layer call reports an error ("process error: N"
 // vs "finalization error: N").
 //
-// Divergence by design: inffast.ts:139-147 reads the output buffer from index 0
-// instead of the window when a window-sourced copy wraps the ring and the rest
-// fits in w_next; the reference then emits bytes that depend on the stream
-// layer's buffer recycling (tests/golden/inffast_wrap_defect.json).  This engine
-// copies the true history (zlib semantics); see DESIGN.md.
+// The reference's window-wrap defect is reproduced (flag ZS_INF_REF_WRAP, the
+// default): when an inflate_fast copy sourced from the window wraps the ring
+// (w_next < op2) and the rest fits in w_next, inffast.ts:133-147 sets
+// from_index = 0 and copies the rest from the caller's OUTPUT buffer at index
+// 0 -- i.e. from where this inflate() call began writing -- instead of from
+// window[0].  The engine tracks the reference's w_next (updatewindow,
+// inflate.ts:282-324, under inf_leave's own call condition,
+// inflate.ts:1059-1072) and copies from the call's first output byte, which
+// is always already written when read (tests/golden/inffast_wrap_defect.json,
+// made by the reference itself).  Without the flag it copies the true history
+// (zlib semantics).
 #include <hip/hip_runtime.h>
 #include "zs_common.h"
 #include "zs_kernels.h"
@@ -224,7 +230,8 @@ struct zs_ist {
   uint64_t total;     // bytes output so far (absolute)
   uint64_t flushed;   // bytes already copied from ring to dst (and checksummed)
   int mode, last, wrap, havedict, flags, d64, back;
-  uint32_t check, w_bits, w_size, w_have;
+  uint32_t check, w_bits, w_size, w_have, w_next;
+  int ref_wrap;  // reproduce inffast.ts:133-147 (see the top of this file)
   uint64_t hold;
   uint32_t bits, length, offset, extra, was;
   uint32_t lenbits, distbits, ncode, nlen, ndist, have_;
@@ -682,6 +689,16 @@ static __device__ int zs_inflate_call(zs_lds& L, zs_ist& S, uint32_t in0, uint32
                       S.mode = BAD;
                       goto fast_done;
                     }
+                    if (S.ref_wrap && dist > outmax) {
+                      // window-sourced copy: the wrap case of inffast.ts:126-147
+                      const uint32_t op2 = (uint32_t)(dist - outmax), wn = S.w_next;
+                      if (wn != 0 && wn < op2 && op2 - wn < len && wn >= len - (op2 - wn)) {
+                        const uint32_t op3 = op2 - wn;
+                        zs_copy(S, dist, op3);                            // window tail (true history)
+                        zs_copy(S, (uint32_t)(S.total - beg), len - op3);  // output[0..]: from this call's start
+                        break;
+                      }
+                    }
                     zs_copy(S, dist, len);
                     break;
                   } else if ((op & 64) == 0) {
@@ -835,9 +852,26 @@ inf_leave:
   {
     const uint32_t in_used = in_start - have;
     const uint32_t out_used = out_start - left;
-    // updatewindow bookkeeping (inflate.ts:282-324): w_have = min(w_size, output before the next call)
-    if (S.w_size == 0) S.w_size = 1u << S.w_bits;
-    S.w_have = (uint32_t)min<uint64_t>(S.w_size, (uint64_t)S.w_have + out_used);
+    // updatewindow bookkeeping (inflate.ts:282-324) under inf_leave's call
+    // condition (inflate.ts:1060-1067; note `|| flush != Z_FINISH` at top level)
+    const uint32_t written = out - left;
+    if (S.w_size || (written && S.mode < BAD && (S.d64 ? S.mode < DONE : S.mode < CHECK)) || !finish) {
+      if (S.w_size == 0) { S.w_size = 1u << S.w_bits; S.w_next = 0; S.w_have = 0; }
+      if (written >= S.w_size) {
+        S.w_next = 0;
+        S.w_have = S.w_size;
+      } else {
+        const uint32_t d = min(S.w_size - S.w_next, written);
+        if (written > d) {
+          S.w_next = written - d;
+          S.w_have = S.w_size;
+        } else {
+          S.w_next += d;
+          if (S.w_next == S.w_size) S.w_next = 0;
+          S.w_have = min(S.w_size, S.w_have + d);
+        }
+      }
+    }
     *consumed = in_used;
     *produced = out_used;
     S.total_in += in_used;
@@ -859,7 +893,7 @@ __global__ __launch_bounds__(64) void zs_k_inflate(const uint8_t* __restrict__ i
                                                    const uint64_t* __restrict__ out_off,
                                                    const uint32_t* __restrict__ out_cap, int wbits,
                                                    zs_inflate_result* __restrict__ res,
-                                                   const zs_lane_res* __restrict__ only) {
+                                                   const zs_lane_res* __restrict__ only, int flags) {
   zs_lds& L = *reinterpret_cast<zs_lds*>(zs_inflate_smem);
   const int s = blockIdx.x;
   if (only && only[s].bail == 0) return;  // decoded cleanly by the lane path
@@ -879,7 +913,8 @@ __global__ __launch_bounds__(64) void zs_k_inflate(const uint8_t* __restrict__ i
   S.mode = S.d64 ? TYPE : HEAD;
   S.last = 0; S.havedict = 0; S.flags = -1; S.back = -1;
   S.check = S.wrap ? (uint32_t)(S.wrap & 1) : 0;
-  S.w_size = 0; S.w_have = 0;
+  S.w_size = 0; S.w_have = 0; S.w_next = 0;
+  S.ref_wrap = (flags & ZS_INF_REF_WRAP) != 0;
   S.hold = 0; S.bits = 0;
   S.length = S.offset = S.extra = S.was = 0;
   S.lenbits = S.distbits = S.ncode = S.nlen = S.ndist = S.have_ = 0;
@@ -1078,7 +1113,7 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
                                                         const uint64_t* __restrict__ out_off,
                                                         const uint32_t* __restrict__ out_cap, int wbits, uint32_t n_members,
                                                         zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
-                                                        uint32_t* __restrict__ lens_out) {
+                                                        uint32_t* __restrict__ lens_out, int flags) {
   __shared__ zs_lane_lds LL[64];
   const uint32_t s = blockIdx.x * 64u + threadIdx.x;
   if (s >= n_members) return;
@@ -1092,11 +1127,18 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   R.bits = 0;
   R.pf = zs_lr_load4(R, 0);
   uint8_t* dst = out + out_off[s];
-  const uint32_t cap = out_cap[s];
+  // This path decodes a member in one go, without the stream layer's call
+  // boundaries.  A member whose input fits one 32 KiB sub-chunk and whose
+  // output fits one 64 KiB output buffer is decoded by ONE inflate() call of
+  // the reference (streams.ts:6-7,78-93) that never copies from the window, so
+  // the window-wrap behaviour (ZS_INF_REF_WRAP) cannot arise; any other member
+  // takes the exact path, which emulates the calls.
+  const bool ref_wrap = (flags & ZS_INF_REF_WRAP) != 0;
+  const uint32_t cap = ref_wrap ? min(out_cap[s], 65536u) : out_cap[s];
   uint32_t total = 0;
   zs_lane_res r = {1u, 0u, 0u, 0u};
   const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
-  bool bail = wbits == -16;                          // deflate64: exact path
+  bool bail = wbits == -16 || (ref_wrap && R.n > 32768u);  // deflate64 / several sub-chunks: exact path
   // ---- wrapper header (inflate.ts:377-580): plain zlib / gzip headers only
   if (!bail && wrap) {
     const uint32_t b0 = zs_lr_take(R, 8), b1 = zs_lr_take(R, 8);

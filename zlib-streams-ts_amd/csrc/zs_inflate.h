@@ -6,6 +6,8 @@
 #define ZS_PHASE_NONE_ 0
 #define ZS_PHASE_PROCESS_ 2
 #define ZS_PHASE_FINISH_ 3
+// inflate kernel flags
+#define ZS_INF_REF_WRAP 1  // reproduce the reference's inflate_fast window-wrap copy (inffast.ts:133-147)
 
 // z_stream messages (inflate.ts:397-1031, inffast.ts:108,197,210)
 enum zs_msg_id {
@@ -52,10 +54,10 @@ struct zs_lane_tabs;
 
 __global__ void zs_k_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                              const uint64_t* out_off, const uint32_t* out_cap, int wbits, zs_inflate_result* res,
-                             const zs_lane_res* only);
+                             const zs_lane_res* only, int flags);
 __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, uint32_t n_members,
-                                  zs_lane_tabs* tabs, zs_lane_res* res, uint32_t* lens_out);
+                                  zs_lane_tabs* tabs, zs_lane_res* res, uint32_t* lens_out, int flags);
 __global__ void zs_k_inflate_lane_verify(zs_lane_res* res, const uint32_t* check, uint32_t n);
 size_t zs_inflate_smem_bytes(int wbits);
 size_t zs_inflate_lane_scratch_bytes();
