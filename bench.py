@@ -74,7 +74,15 @@ def parse():
     ap.add_argument("--mode", default="deflate", choices=["deflate", "inflate"],
                     help="deflate: the headline (configs[1]); inflate: decode of pre-built members (configs[2], C5)")
     ap.add_argument("--replicas", type=int, default=16, help="inflate: members = streams x replicas (C3: 4096 x 16)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine option (zs_set_option), e.g. lane_block=16; repeatable")
     return ap.parse_args()
+
+
+def set_options(eng, args):
+    for o in args.option:
+        k, v = o.split("=")
+        eng.set_option(k, int(v))
 
 
 class Dist:
@@ -219,6 +227,7 @@ def main():
     d_len = torch.zeros(S, dtype=torch.int32, device=D.dev)
     in_off, in_len, out_off, out_cap = layout(S, L, cap)
     eng = zsamd.Engine(D.local)
+    set_options(eng, args)
     stream = torch.cuda.current_stream(D.dev)
 
     def run(n):
@@ -387,6 +396,7 @@ def main_inflate(args):
     dec_fmt = args.format
     enc_fmt = "deflate-raw" if dec_fmt == "deflate64-raw" else dec_fmt
     eng = zsamd.Engine(D.local)
+    set_options(eng, args)
     N_glob = S * R
     lo, hi = shard.shard_range(N_glob, D.world, D.rank)
     uniq = sorted({i % S for i in range(lo, hi)})

@@ -132,7 +132,13 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * "match_sweep" (default 1): levels 4..9, streams <= 65,537 B find matches by
  * a counting sort by hash + lock-step sweep (0: chain links + per-tile walk);
  * "parse_split" (default 0): levels 4..9 parse as per-range + per-stream
- * kernels (0: one wave per stream).  Options never change output bytes. */
+ * kernels (0: one wave per stream); "lane_block" (default 0 = by batch size;
+ * else 1..64, a power of two): members per workgroup of the inflate lane path.
+ * These options never change output bytes.  "inflate_ref_wrap" (default 1)
+ * does: 1 reproduces the reference's inflate_fast window-wrap copy
+ * (inffast.ts:133-147), which changes the output of members whose match
+ * crosses the reference's window wrap between inflate() calls; 0 decodes with
+ * zlib semantics (the bytes the compressor was given). */
 int zs_set_option(zs_ctx *ctx, const char *name, int value);
 
 /* Introspection for tests: copy an intermediate array of stream s of the last

@@ -96,6 +96,67 @@ def test_deflate64_fixtures_and_kats(engine):
     assert st == 1 and out == b"a" * 259
 
 
+@pytest.mark.parametrize("lane_block", [0, 1, 8, 64])
+def test_deflate64_lane_path_fixtures(engine, lane_block):
+    """The reference's deflate64 fixtures (distances > 32 KiB, codes 30/31,
+    length 285 with 16 extra bits) through the lane decoder at several
+    workgroup shapes, against the reference's output hashes."""
+    names = sorted(os.listdir(os.path.join(golden_io.GOLDEN, "d64")))
+    data = [open(os.path.join(golden_io.GOLDEN, "d64", f), "rb").read() for f in names]
+    data.append(bytes.fromhex("4b1cfdff07a3e5030000"))  # test-inflate9-length-code-285.spec.ts:9-15
+    cases = {c["name"]: c for c, _ in golden_io.inflate_cases()}
+    try:
+        engine.set_option("lane_block", lane_block)
+        res = engine.decompress_batch_raw(data * 3, "deflate64-raw", out_caps=[3 << 20] * (3 * len(data)))
+    finally:
+        engine.set_option("lane_block", 0)
+    for i, (st, ph, msg, out, cons) in enumerate(res):
+        k = i % len(data)
+        if k == len(names):
+            assert st == 1 and out == b"a" * 66539
+        else:
+            assert st == 1 and corpus.sha256(out) == cases["d64_" + names[k]]["out_sha256"], names[k]
+
+
+@pytest.mark.slow
+def test_c5_deflate64_decode_8192_streams(engine):
+    """C5-ii: the 8,192 T-corpus deflate-raw L6 streams --
+    the bodies of the C5 gzip members, pinned by the reference's golden hashes --
+    decoded as deflate64-raw give back their sources (no length-258 match, so
+    they are valid deflate64 with identical output), interleaved with the
+    reference's deflate64 fixtures."""
+    import zsamd
+
+    recs = golden_io.batch("t64_l6_gzip")
+    n = len(recs)
+    buf = bytes(zsamd.corpus("text", 0, n, 65536))
+    srcs = [buf[i * 65536:(i + 1) * 65536] for i in range(n)]
+    gz = engine.compress_batch(srcs, "gzip", 6)
+    bad = [i for i, c in enumerate(gz) if (len(c), hashlib.sha256(c).digest()[:16]) != recs[i]]
+    assert not bad, bad[:10]
+    raw = [c[10:-8] for c in gz]
+    names = sorted(os.listdir(os.path.join(golden_io.GOLDEN, "d64")))
+    fx = [open(os.path.join(golden_io.GOLDEN, "d64", f), "rb").read() for f in names]
+    cases = {c["name"]: c for c, _ in golden_io.inflate_cases()}
+    fcap = [cases["d64_" + f]["out_len"] + 64 for f in names]
+    items, caps = [], []
+    for i, r in enumerate(raw):
+        items.append(r)
+        caps.append(65536 + 64)
+        if i % 1024 == 0:
+            items.extend(fx)
+            caps.extend(fcap)
+    res = engine.decompress_batch_raw(items, "deflate64-raw", out_caps=caps)
+    outs = iter(res)
+    for i in range(n):
+        st, ph, msg, out, cons = next(outs)
+        assert st == 1 and out == srcs[i], i
+        if i % 1024 == 0:
+            for f in names:
+                st, ph, msg, out, cons = next(outs)
+                assert st == 1 and corpus.sha256(out) == cases["d64_" + f]["out_sha256"], f
+
+
 def test_capacity_too_small(engine):
     c = oracle.compress(bytes(100000), 6, "deflate-raw")[1]
     (st, ph, msg, out, cons), = engine.decompress_batch_raw([c], "deflate-raw", out_caps=[1000])
@@ -141,14 +202,16 @@ def _fast_vs_exact_corpus():
     rng = random.Random(2024)
     items = []
     for c, d in golden_io.inflate_cases():
-        if d is not None and c["format"] != "deflate64-raw":
+        if d is not None:
             items.append((c["format"], d, max(1 << 17, 40 * len(d))))
-    for k in range(60):
-        fmt = rng.choice(["deflate-raw", "deflate", "gzip"])
+    for k in range(80):
+        # deflate64-raw over deflate-raw streams: valid deflate64 unless a
+        # length-258 match appears (then a different, still deterministic decode)
+        fmt = rng.choice(["deflate-raw", "deflate", "gzip", "deflate64-raw"])
         n = rng.choice([0, 1, 7, 258, 5000, 65536, 70000, rng.randrange(1, 200000)])
         src = corpus.make({"kind": rng.choice(["text", "mixed", "rand", "zeros", "ramp"]), "n": n,
                            "seed": rng.randrange(1 << 32)})
-        comp = oracle.compress(src, rng.choice([1, 3, 6, 9]), fmt)[1]
+        comp = oracle.compress(src, rng.choice([1, 3, 6, 9]), "deflate-raw" if fmt == "deflate64-raw" else fmt)[1]
         cap = len(src) + 64
         variant = k % 6
         if variant == 1 and len(comp) > 4:
@@ -169,7 +232,7 @@ def test_lane_fast_path_matches_exact_path(engine):
     """The lane-per-member decoder (inflate_fast option) and the exact stream-layer
     state machine agree on status, phase, message, bytes and consumed input."""
     items = _fast_vs_exact_corpus()
-    for fmt in ("deflate-raw", "deflate", "gzip"):
+    for fmt in ("deflate-raw", "deflate", "gzip", "deflate64-raw"):
         its = [(d, cap) for f, d, cap in items if f == fmt]
         engine.set_option("inflate_fast", 1)
         fast = engine.decompress_batch_raw([d for d, _ in its], fmt, out_caps=[c for _, c in its])

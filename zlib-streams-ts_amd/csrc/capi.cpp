@@ -87,7 +87,8 @@ struct zs_ctx {
   bool inflate_fast = true;
   bool inflate_ref_wrap = true;  // reproduce the reference's inflate_fast window-wrap copy (inffast.ts:133-147)
   bool match_sweep = true;
-  bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)  // L4..9 streams <= 65537 B: bucket sort + sweep (0: chain links + walk)
+  bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)
+  int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res, d_pack;
   HostBuf h_in, h_out;
@@ -218,7 +219,11 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "parse_split")) c->parse_split = value != 0;
-  else return fail(ZS_STREAM_ERROR, "unknown option %s", name);
+  else if (!strcmp(name, "lane_block")) {
+    if (value != 0 && (value < 1 || value > 64 || (value & (value - 1))))
+      return fail(ZS_STREAM_ERROR, "lane_block must be 0 or a power of two <= 64");
+    c->lane_block = value;
+  } else return fail(ZS_STREAM_ERROR, "unknown option %s", name);
   return ZS_OK;
 }
 double zs_last_batch_ms(zs_ctx* c) { return c->total_ms; }
@@ -711,13 +716,20 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
   const uint32_t* d_ocap = (const uint32_t*)(dm + ml.out_cap);
   zs_lane_res* lres = nullptr;
   MARK("start");
-  if (c->inflate_fast && wbits != -16) {
-    // lane-per-member fast path; anything but a clean end of stream goes to the exact kernel
+  if (c->inflate_fast) {
+    // lane-per-member fast path; anything but a clean end of stream goes to the exact kernel.
+    // A lane's decode is a dependent chain of loads, so the chip wants many
+    // waves more than full ones: below 4096 waves of 64 members, members
+    // spread over more, thinner workgroups (one wave each) until 4096 waves
+    // or 8 members per wave.
+    uint32_t B = (uint32_t)c->lane_block;
+    if (!B)
+      for (B = 64; B > 8 && (n + B - 1) / B < 4096u;) B >>= 1;
     HIPCHK(c->ltabs.ensure(zs_inflate_lane_scratch_bytes() * (size_t)n));
     HIPCHK(c->lres.ensure(sizeof(zs_lane_res) * (size_t)n));
     HIPCHK(c->llen.ensure(8ull * n));
     lres = c->lres.as<zs_lane_res>();
-    zs_k_inflate_lane<<<(n + 63) / 64, 64, 0, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
+    zs_k_inflate_lane<<<(n + B - 1) / B, B, B * zs_inflate_lane_lds_bytes(), st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
                                                     (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
                                                     c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0);
     MARK("inflate_lane");

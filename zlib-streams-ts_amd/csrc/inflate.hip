@@ -982,17 +982,18 @@ size_t zs_inflate_smem_bytes(int wbits) {
 
 // ===================================================================== fast path
 // One LANE per member.  The exact kernel above spends a whole wave on one
-// stream because it re-enacts the stream layer's call boundaries; but for a
-// member that decodes cleanly those boundaries change nothing in the output
-// (the inffast window-wrap defect aside, which this engine does not reproduce),
-// so a lane can decode it straight through: zlib's own tables (inflate_table
-// above, so invalid codes are recognised exactly as the reference does), a
-// 64-bit bit buffer, output written to HBM and match history read back from it.
-// A member takes the exact path instead (zs_k_inflate over the bailed members)
-// on ANY condition that is not a clean end of stream -- a data error, truncated
-// input, a dictionary request, gzip header fields, deflate64, a checksum or
-// length mismatch, or output capacity -- so statuses, phases and messages
-// always come from the exact state machine.
+// stream because it re-enacts the stream layer's call boundaries; a member
+// whose decoding those boundaries cannot change decodes straight through in one
+// lane instead: a deflate64 member (the reference decodes it with the slow state
+// machine only, whose window copies are exact), or a deflate / zlib / gzip member
+// that one inflate() call of the reference decodes whole (see ZS_INF_REF_WRAP
+// below).  zlib's own tables (inflate_table above, so invalid codes are
+// recognised exactly as the reference does), a 64-bit bit buffer, output written
+// to HBM and match history read back from it.  A member takes the exact path
+// instead (zs_k_inflate over the bailed members) on ANY condition that is not a
+// clean end of stream -- a data error, truncated input, a dictionary request,
+// gzip header fields, a checksum or length mismatch, or output capacity -- so
+// statuses, phases and messages always come from the exact state machine.
 struct zs_lane_tabs {
   zcode codes[ENOUGH_LENS + ENOUGH_DISTS_9];
   uint16_t lens[320];
@@ -1091,20 +1092,23 @@ static __device__ void zs_lane_root(uint16_t* tab, uint32_t rbits, const uint16_
   }
 }
 
-// a root-table symbol as the zlib table entry the decoder consumes
-static __device__ __forceinline__ zcode zs_lit_entry(uint32_t sym) {
+// a root-table symbol as the zlib table entry the decoder consumes (zs_lbase /
+// zs_dbase's ops: 16 + extra bits, deflate64 128 + extra bits)
+static __device__ __forceinline__ zcode zs_lit_entry(uint32_t sym, bool d64) {
   if (sym < 256) return zpack(0, 0, sym);
   if (sym == 256) return zpack(32 + 64, 0, 0);
   const uint32_t c = sym - 257;  // length codes: base / extra bits (inflate/constants.ts:8-23)
-  if (c < 8) return zpack(16, 0, c + 3);
-  if (c == 28) return zpack(16, 0, 258);
+  const uint32_t f = d64 ? 128u : 16u;
+  if (c < 8) return zpack(f, 0, c + 3);
+  if (c == 28) return d64 ? zpack(128 + 16, 0, 3) : zpack(16, 0, 258);  // deflate64: 3 + 16 extra bits
   const uint32_t x = (c >> 2) - 1;
-  return zpack(16 + x, 0, ((4u | (c & 3u)) << x) + 3u);
+  return zpack(f + x, 0, ((4u | (c & 3u)) << x) + 3u);
 }
-static __device__ __forceinline__ zcode zs_dist_entry(uint32_t d) {
-  if (d < 4) return zpack(16, 0, d + 1);
-  const uint32_t x = (d >> 1) - 1;
-  return zpack(16 + x, 0, ((2u | (d & 1u)) << x) + 1u);
+static __device__ __forceinline__ zcode zs_dist_entry(uint32_t d, bool d64) {
+  const uint32_t f = d64 ? 128u : 16u;
+  if (d < 4) return zpack(f, 0, d + 1);
+  const uint32_t x = (d >> 1) - 1;  // codes 30/31 (deflate64 only): 32769 / 49153 + 14 extra bits
+  return zpack(f + x, 0, ((2u | (d & 1u)) << x) + 1u);
 }
 
 __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
@@ -1114,8 +1118,8 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
                                                         const uint32_t* __restrict__ out_cap, int wbits, uint32_t n_members,
                                                         zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
                                                         uint32_t* __restrict__ lens_out, int flags) {
-  __shared__ zs_lane_lds LL[64];
-  const uint32_t s = blockIdx.x * 64u + threadIdx.x;
+  extern __shared__ zs_lane_lds LL[];  // blockDim.x entries
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_members) return;
   zs_lane_tabs& T = tabs[s];
   zs_lane_lds& F = LL[threadIdx.x];
@@ -1133,12 +1137,16 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   // the reference (streams.ts:6-7,78-93) that never copies from the window, so
   // the window-wrap behaviour (ZS_INF_REF_WRAP) cannot arise; any other member
   // takes the exact path, which emulates the calls.
-  const bool ref_wrap = (flags & ZS_INF_REF_WRAP) != 0;
+  // deflate64 members never reach inflate_fast in the reference (inflate.ts:841),
+  // so they carry no call-boundary behaviour and decode here at any size.
+  const bool d64 = wbits == -16;
+  const bool ref_wrap = (flags & ZS_INF_REF_WRAP) != 0 && !d64;
   const uint32_t cap = ref_wrap ? min(out_cap[s], 65536u) : out_cap[s];
+  const uint32_t lmask = d64 ? 31u : 15u;  // length extra-bit mask (inflate.ts:891)
   uint32_t total = 0;
   zs_lane_res r = {1u, 0u, 0u, 0u};
   const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
-  bool bail = wbits == -16 || (ref_wrap && R.n > 32768u);  // deflate64 / several sub-chunks: exact path
+  bool bail = ref_wrap && R.n > 32768u;  // several sub-chunks: exact path
   // ---- wrapper header (inflate.ts:377-580): plain zlib / gzip headers only
   if (!bail && wrap) {
     const uint32_t b0 = zs_lr_take(R, 8), b1 = zs_lr_take(R, 8);
@@ -1177,24 +1185,24 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       for (; sym < 280; sym++) T.lens[sym] = 7;
       for (; sym < 288; sym++) T.lens[sym] = 8;
       lbits = 9;
-      zs_inflate_table(LENS, T.lens, 288, T.codes, &lbits, T.work, false, &used);
+      zs_inflate_table(LENS, T.lens, 288, T.codes, &lbits, T.work, d64, &used);
       for (sym = 0; sym < 32; sym++) T.lens[sym] = 5;
       dbits = 5;
-      zs_inflate_table(DISTS, T.lens, 32, T.codes + used, &dbits, T.work, false, &sym);
+      zs_inflate_table(DISTS, T.lens, 32, T.codes + used, &dbits, T.work, d64, &sym);
       lt = T.codes;
       dt = T.codes + used;
       for (sym = 0; sym < 288; sym++) T.lens[sym] = sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8;
       zs_lane_root(F.lit, ZS_LROOT, T.lens, 286);  // 286/287 stay out of the root: invalid codes decode via T
       for (sym = 0; sym < 30; sym++) T.lens[sym] = 5;
-      zs_lane_root(F.dist, ZS_DROOT, T.lens, 30);    // 30/31 likewise
+      zs_lane_root(F.dist, ZS_DROOT, T.lens, d64 ? 32 : 30);  // deflate: 30/31 likewise
     } else if (type == 2) {  // dynamic (inflate.ts:662-836)
       const uint32_t nlen = zs_lr_take(R, 5) + 257, ndist = zs_lr_take(R, 5) + 1, ncode = zs_lr_take(R, 4) + 4;
-      if (nlen > 286 || ndist > 30) { bail = true; break; }
+      if (nlen > 286 || (!d64 && ndist > 30)) { bail = true; break; }
       uint32_t i;
       for (i = 0; i < ncode; i++) T.lens[ZS_BL_ORDER[i]] = (uint16_t)zs_lr_take(R, 3);
       for (; i < 19; i++) T.lens[ZS_BL_ORDER[i]] = 0;
       uint32_t cbits = 7, used;
-      if (zs_inflate_table(CODES, T.lens, 19, T.codes, &cbits, T.work, false, &used)) { bail = true; break; }
+      if (zs_inflate_table(CODES, T.lens, 19, T.codes, &cbits, T.work, d64, &used)) { bail = true; break; }
       i = 0;
       while (i < nlen + ndist) {
         const zcode here = zs_lane_decode(R, T.codes, cbits);
@@ -1216,9 +1224,9 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (bail || zs_lr_over(R) || T.lens[256] == 0) { bail = true; break; }
       lbits = 9;
       uint32_t lused, dused;
-      if (zs_inflate_table(LENS, T.lens, nlen, T.codes, &lbits, T.work, false, &lused)) { bail = true; break; }
+      if (zs_inflate_table(LENS, T.lens, nlen, T.codes, &lbits, T.work, d64, &lused)) { bail = true; break; }
       dbits = 6;
-      if (zs_inflate_table(DISTS, T.lens + nlen, ndist, T.codes + lused, &dbits, T.work, false, &dused)) {
+      if (zs_inflate_table(DISTS, T.lens + nlen, ndist, T.codes + lused, &dbits, T.work, d64, &dused)) {
         bail = true;
         break;
       }
@@ -1238,7 +1246,7 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (fe >> 12) {
         R.hold >>= fe >> 12;
         R.bits -= fe >> 12;
-        here = zs_lit_entry(fe & 0x1ffu);
+        here = zs_lit_entry(fe & 0x1ffu, d64);
       } else {
         here = zs_lane_decode(R, lt, lbits);
       }
@@ -1249,19 +1257,19 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
         continue;
       }
       if (op & 32) break;                   // end of block
-      if (!(op & 16)) { bail = true; break; }  // "invalid literal/length code"
-      uint32_t len = C_VAL(here) + zs_lr_take(R, op & 15u);
+      if (op & 64) { bail = true; break; }  // "invalid literal/length code"
+      uint32_t len = C_VAL(here) + zs_lr_take(R, op & lmask);
       if (R.bits < 32) zs_lr_fill(R);
       const uint32_t de = F.dist[(uint32_t)R.hold & ((1u << ZS_DROOT) - 1)];
       if (de >> 12) {
         R.hold >>= de >> 12;
         R.bits -= de >> 12;
-        here = zs_dist_entry(de & 0x1fu);
+        here = zs_dist_entry(de & 0x1fu, d64);
       } else {
         here = zs_lane_decode(R, dt, dbits);
       }
       op = C_OP(here);
-      if (!(op & 16)) { bail = true; break; }  // "invalid distance code"
+      if (op & 64) { bail = true; break; }  // "invalid distance code"
       const uint32_t dist = C_VAL(here) + zs_lr_take(R, op & 15u);
       if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
       const uint8_t* from = dst + total - dist;
@@ -1305,6 +1313,7 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
 }
 
 size_t zs_inflate_lane_scratch_bytes() { return sizeof(zs_lane_tabs); }
+size_t zs_inflate_lane_lds_bytes() { return sizeof(zs_lane_lds); }
 
 // checksum of the decoded output against the trailer: a mismatch sends the member to the exact path
 __global__ void zs_k_inflate_lane_verify(zs_lane_res* __restrict__ res, const uint32_t* __restrict__ check,

@@ -61,3 +61,4 @@ __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, con
 __global__ void zs_k_inflate_lane_verify(zs_lane_res* res, const uint32_t* check, uint32_t n);
 size_t zs_inflate_smem_bytes(int wbits);
 size_t zs_inflate_lane_scratch_bytes();
+size_t zs_inflate_lane_lds_bytes();
