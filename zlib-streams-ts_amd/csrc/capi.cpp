@@ -719,12 +719,12 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
   if (c->inflate_fast) {
     // lane-per-member fast path; anything but a clean end of stream goes to the exact kernel.
     // A lane's decode is a dependent chain of loads, so the chip wants many
-    // waves more than full ones: below 4096 waves of 64 members, members
-    // spread over more, thinner workgroups (one wave each) until 4096 waves
-    // or 8 members per wave.
+    // waves more than full ones: below 1024 waves of 64 members (one per
+    // SIMD), members spread over more, thinner workgroups (one wave each)
+    // until 1024 waves or 8 members per wave.
     uint32_t B = (uint32_t)c->lane_block;
     if (!B)
-      for (B = 64; B > 8 && (n + B - 1) / B < 4096u;) B >>= 1;
+      for (B = 64; B > 8 && (n + B - 1) / B < 1024u;) B >>= 1;
     HIPCHK(c->ltabs.ensure(zs_inflate_lane_scratch_bytes() * (size_t)n));
     HIPCHK(c->lres.ensure(sizeof(zs_lane_res) * (size_t)n));
     HIPCHK(c->llen.ensure(8ull * n));
