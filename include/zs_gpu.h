@@ -122,6 +122,10 @@ int zs_adler32_batch_device(zs_ctx *ctx, uint32_t n_streams, const uint8_t *d_in
  * the named phase ("match", "parse", "trees", "emit", "prev", "inflate", ...).
  * Returns -1 when no timing is available. */
 double zs_last_batch_ms(zs_ctx *ctx);
+/* Members of the last inflate batch that the lane-per-member path decoded
+ * (the rest went through the exact stream-layer state machine).  Synchronizes
+ * the batch's stream.  For tests and tuning. */
+uint32_t zs_last_inflate_lane_count(zs_ctx *ctx);
 double zs_last_phase_ms(zs_ctx *ctx, const char *phase);
 void zs_set_timing(zs_ctx *ctx, int on);
 /* Engine options: "timing" (0/1, as zs_set_timing); "inflate_fast" (default 1):

@@ -241,3 +241,22 @@ def test_lane_fast_path_matches_exact_path(engine):
         engine.set_option("inflate_fast", 1)
         for i, (a, b) in enumerate(zip(fast, exact)):
             assert a == b, (fmt, i, a[:3], b[:3], len(a[3]), len(b[3]), a[4], b[4])
+
+
+@pytest.mark.parametrize("fmt", ["deflate-raw", "deflate", "gzip", "deflate64-raw"])
+def test_lane_path_decodes_clean_members(engine, fmt):
+    """Clean members (one reference inflate() call: <= 32 KiB in, <= 64 KiB out)
+    decode on the lane path, not through the exact fallback."""
+    rng = random.Random(5)
+    srcs = [corpus.make({"kind": k, "n": n, "seed": rng.randrange(1 << 32)})
+            for k in ("text", "mixed", "zeros", "ramp") for n in (1, 100, 5000, 40000, 65536)]
+    srcs.append(b"")
+    enc = "deflate-raw" if fmt == "deflate64-raw" else fmt
+    comps = [oracle.compress(s, lvl, enc)[1] for s, lvl in zip(srcs, [1, 6, 9] * 20)]
+    # deflate64 over deflate streams: only those without a length-258 match are valid
+    keep = [(s, c) for s, c in zip(srcs, comps)
+            if len(c) <= 32768 and oracle.decompress(c, fmt, cap=len(s) + 64)[1] == s]
+    res = engine.decompress_batch_raw([c for _, c in keep], fmt, out_caps=[len(s) + 64 for s, _ in keep])
+    for (s, c), (st, ph, msg, out, cons) in zip(keep, res):
+        assert st == 1 and out == s
+    assert engine.last_lane_count() == len(keep)

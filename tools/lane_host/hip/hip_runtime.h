@@ -1,0 +1,27 @@
+// Host stand-in for the few HIP names inflate_lane.hip uses, so that the lane
+// kernel's own source compiles as plain C++ and runs one lane at a time on the
+// CPU (tools/lane_host/lane_host.cpp).  Test tooling only: the product is the
+// gfx950 build of the same file.
+#pragma once
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <algorithm>
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __noinline__ __attribute__((noinline))
+#define __launch_bounds__(x)
+#define __shared__
+struct uint4 {
+  uint32_t x, y, z, w;
+};
+static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
+struct zs_dim3 {
+  uint32_t x, y, z;
+};
+extern zs_dim3 threadIdx, blockIdx, blockDim;
+using std::max;
+using std::min;
+typedef int hipError_t;

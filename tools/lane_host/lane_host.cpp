@@ -1,0 +1,51 @@
+// Runs the lane-per-member inflate kernel (zlib-streams-ts_amd/csrc/inflate_lane.hip)
+// on the CPU, one member at a time, from its own source (host stand-ins for the
+// HIP names in hip/hip_runtime.h next to this file).  Test tooling: lets the CPU
+// suite check the lane decoder's logic against the oracle without a GPU.
+//
+// usage: lane_host WBITS FLAGS < members > results
+//   stdin:  u32 count, then per member: u32 in_len, u32 out_cap, in_len bytes
+//   stdout: per member: u32 bail, u32 out_len, u32 consumed, u32 want, out_len bytes
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+#include "hip/hip_runtime.h"
+zs_dim3 threadIdx, blockIdx, blockDim;
+#include "../../zlib-streams-ts_amd/csrc/inflate_lane.hip"
+zs_lane_lds LL[1];
+
+static void rd(void* p, size_t n) {
+  if (fread(p, 1, n, stdin) != n) {
+    fprintf(stderr, "lane_host: short input\n");
+    exit(2);
+  }
+}
+int main(int argc, char** argv) {
+  if (argc < 3) return 2;
+  const int wbits = atoi(argv[1]), flags = atoi(argv[2]);
+  uint32_t n;
+  rd(&n, 4);
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t len, cap;
+    rd(&len, 4);
+    rd(&cap, 4);
+    // 16-byte aligned buffers with slack, as device allocations are; the member
+    // starts at a varying misalignment to exercise the reader's edges
+    const uint32_t mis = i % 16;
+    std::vector<uint4> ib((len + mis + 64) / 16 + 1), ob((cap + mis + 64) / 16 + 1);
+    uint8_t* in = (uint8_t*)ib.data();
+    rd(in + mis, len);
+    uint64_t ioff = mis, ooff = (i * 5) % 16;
+    zs_lane_res r;
+    uint32_t lo;
+    threadIdx = {0, 0, 0};
+    blockIdx = {0, 0, 0};
+    blockDim = {1, 1, 1};
+    std::vector<zs_lane_tabs> tabs(1);
+    zs_k_inflate_lane(in, &ioff, &len, (uint8_t*)ob.data(), &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags);
+    fwrite(&r, 4, 4, stdout);
+    fwrite((uint8_t*)ob.data() + ooff, 1, r.bail ? 0 : r.out_len, stdout);
+  }
+  return 0;
+}

@@ -83,7 +83,8 @@ struct zs_ctx {
   bool timing = false;
   bool check_phases = false;  // synchronise after every phase and name the one that failed
   // workspace
-  Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen;
+  Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen, lstat;
+  hipStream_t last_stream = nullptr;  // stream of the last inflate batch
   bool inflate_fast = true;
   bool inflate_ref_wrap = true;  // reproduce the reference's inflate_fast window-wrap copy (inffast.ts:133-147)
   bool match_sweep = true;
@@ -200,7 +201,7 @@ void zs_ctx_destroy(zs_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (Buf* b : {&c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
+  for (Buf* b : {&c->lstat, &c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
                  &c->istate, &c->d_in, &c->d_out, &c->d_res, &c->d_pack})
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&c->h_in, &c->h_out})
@@ -227,6 +228,13 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   return ZS_OK;
 }
 double zs_last_batch_ms(zs_ctx* c) { return c->total_ms; }
+uint32_t zs_last_inflate_lane_count(zs_ctx* c) {
+  uint32_t v = 0;
+  if (!c || !c->lstat.p || hipStreamSynchronize(c->last_stream) != hipSuccess ||
+      hipMemcpy(&v, c->lstat.p, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return v;
+}
 double zs_last_phase_ms(zs_ctx* c, const char* phase) {
   double t = -1;
   for (auto& p : c->phase_ms)
@@ -667,10 +675,12 @@ static const char* kInflateMsgs[ZS_MSG_COUNT] = {
 extern "C" const char* zs_inflate_message(int32_t i) { return (i >= 0 && i < ZS_MSG_COUNT) ? kInflateMsgs[i] : ""; }
 
 __global__ void zs_k_inflate_finish(const zs_inflate_result* r, const zs_lane_res* lane, int32_t* status,
-                                    int32_t* phase, int32_t* msg, uint32_t* out_len, uint32_t* consumed, int n) {
+                                    int32_t* phase, int32_t* msg, uint32_t* out_len, uint32_t* consumed, int n,
+                                    uint32_t* lane_count) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   if (lane && lane[s].bail == 0) {  // clean member from the lane path
+    atomicAdd(lane_count, 1u);
     status[s] = ZS_Z_STREAM_END;
     phase[s] = ZS_PHASE_NONE_;
     msg[s] = ZS_MSG_NONE;
@@ -729,7 +739,10 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
     HIPCHK(c->lres.ensure(sizeof(zs_lane_res) * (size_t)n));
     HIPCHK(c->llen.ensure(8ull * n));
     lres = c->lres.as<zs_lane_res>();
-    zs_k_inflate_lane<<<(n + B - 1) / B, B, B * zs_inflate_lane_lds_bytes(), st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
+    while (B > 1 && B * zs_inflate_lane_lds_bytes() > 160u * 1024u) B >>= 1;  // one CU's LDS
+    const size_t lsm = B * zs_inflate_lane_lds_bytes();
+    HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate_lane, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm));
+    zs_k_inflate_lane<<<(n + B - 1) / B, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
                                                     (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
                                                     c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0);
     MARK("inflate_lane");
@@ -743,8 +756,11 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
   zs_k_inflate<<<n, 64, smem, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
                                     c->istate.as<zs_inflate_result>(), lres, c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0);
   MARK("inflate");
+  HIPCHK(c->lstat.ensure(16));
+  HIPCHK(hipMemsetAsync(c->lstat.p, 0, 4, st));
   zs_k_inflate_finish<<<(n + 255) / 256, 256, 0, st>>>(c->istate.as<zs_inflate_result>(), lres, d_status, d_phase,
-                                                       d_msg, d_out_len, d_consumed, (int)n);
+                                                       d_msg, d_out_len, d_consumed, (int)n, c->lstat.as<uint32_t>());
+  c->last_stream = st;
   MARK("finish");
   HIPCHK(hipGetLastError());
   collect_marks(c);

@@ -33,157 +33,14 @@
 #include "zs_common.h"
 #include "zs_kernels.h"
 #include "zs_inflate.h"
+#include "zs_inftab.h"
 
 #define IN_CHUNK 32768u   // streams.ts:7
 #define OUT_BUF 65536u    // streams.ts:6
-#define ENOUGH_LENS 852u  // inflate/constants.ts:4-6
-#define ENOUGH_DISTS_9 594u
 #define FLUSH_AT 4096u    // ring bytes flushed to HBM per step
-
-typedef uint32_t zcode;  // op << 24 | bits << 16 | val (inflate/utils.ts:51-72)
-#define C_OP(c) ((c) >> 24)
-#define C_BITS(c) (((c) >> 16) & 0xffu)
-#define C_VAL(c) ((c) & 0xffffu)
 
 enum { HEAD = 0, FLAGS, TIME, OS, EXLEN, EXTRA, NAME, COMMENT, HCRC, DICTID, DICT, TYPE, TYPEDO, STORED, COPY_, COPY,
        TABLE, LENLENS, CODELENS, LEN_, LEN, LENEXT, DIST, DISTEXT, MATCH, LIT, CHECK, LENGTH, DONE, BAD };
-enum { CODES = 0, LENS, DISTS };
-
-static __device__ __forceinline__ zcode zpack(uint32_t op, uint32_t bits, uint32_t val) {
-  return (op << 24) | (bits << 16) | val;
-}
-
-// length/distance tables, inflate/constants.ts:8-45 (ops: 16 + extra, deflate64: 128 + extra)
-static __device__ __forceinline__ void zs_lbase(uint32_t i, bool d64, uint32_t& base, uint32_t& op) {
-  static constexpr uint16_t lb[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-  static constexpr uint8_t le[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-  if (i < 28) { base = lb[i]; op = (d64 ? 128u : 16u) + le[i]; }
-  else if (i == 28) { base = d64 ? 3u : 258u; op = d64 ? 144u : 16u; }
-  else { base = 0; op = d64 ? (i == 29 ? 72u : 78u) : (i == 29 ? 73u : 200u); }
-}
-static __device__ __forceinline__ void zs_dbase(uint32_t i, bool d64, uint32_t& base, uint32_t& op) {
-  static constexpr uint16_t db[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,    65,    97,    129,
-                                      193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-  static constexpr uint8_t de[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-  if (i < 30) { base = db[i]; op = (d64 ? 128u : 16u) + de[i]; }
-  else if (d64) { base = i == 30 ? 32769u : 49153u; op = 128u + 14u; }
-  else { base = 0; op = 64u; }
-}
-
-// inflate_table (inftrees.ts:62-279).  Returns 0 ok, -1 bad code set, 1 over ENOUGH.
-// All lanes execute it on identical values (writes are duplicated, benign).
-static __device__ int zs_inflate_table(int type, const uint16_t* lens, uint32_t codes, zcode* table, uint32_t* bits_io,
-                                       uint16_t* work, bool d64, uint32_t* used_out) {
-  uint32_t len, sym, min, max, root, curr, drop, used, huff, incr, fill, low, mask;
-  int left;
-  zcode here;
-  uint32_t next = 0;
-  uint16_t count[16], offs[16];
-  const uint32_t enough_d = d64 ? ENOUGH_DISTS_9 : 592u;
-  for (len = 0; len <= 15; len++) count[len] = 0;
-  for (sym = 0; sym < codes; sym++) count[lens[sym]]++;
-  root = *bits_io;
-  for (max = 15; max >= 1; max--) if (count[max] != 0) break;
-  if (root > max) root = max;
-  if (max == 0) {
-    if (!d64) {  // _createTableWhenNoCodes
-      table[0] = zpack(64, 1, 0);
-      table[1] = zpack(64, 1, 0);
-      *bits_io = 1;
-      *used_out = 0;
-      return 0;
-    }
-    return -1;
-  }
-  for (min = 1; min < max; min++) if (count[min] != 0) break;
-  if (root < min) root = min;
-  left = 1;
-  for (len = 1; len <= 15; len++) {
-    left <<= 1;
-    left -= count[len];
-    if (left < 0) return -1;
-  }
-  if (left > 0 && (type == CODES || max != 1)) return -1;
-  offs[1] = 0;
-  for (len = 1; len < 15; len++) offs[len + 1] = (uint16_t)(offs[len] + count[len]);
-  for (sym = 0; sym < codes; sym++) if (lens[sym] != 0) work[offs[lens[sym]]++] = (uint16_t)sym;
-  const int match = type == CODES ? (d64 ? 19 : 20) : type == LENS ? (d64 ? 256 : 257) : (d64 ? -1 : 0);
-  huff = 0;
-  sym = 0;
-  len = min;
-  curr = root;
-  drop = 0;
-  low = 0xffffffffu;
-  used = 1u << root;
-  mask = used - 1;
-#define ZS_OVER(u) ((type == LENS && (d64 ? (u) >= ENOUGH_LENS : (u) > ENOUGH_LENS)) || \
-                    (type == DISTS && (d64 ? (u) >= enough_d : (u) > enough_d)))
-  if (ZS_OVER(used)) return 1;
-  for (;;) {
-    const int w = work[sym];
-    if (d64 ? w < match : w + 1 < match) {
-      here = zpack(0, len - drop, (uint32_t)w);
-    } else if (d64 ? w > match : w >= match) {
-      uint32_t b, op;
-      if (type == CODES) { b = (uint32_t)work[w - match]; op = b; }  // unreachable for valid CODES tables
-      else if (type == LENS) zs_lbase((uint32_t)(w - 257), d64, b, op);
-      else zs_dbase((uint32_t)(d64 ? w : w - match), d64, b, op);
-      here = zpack(op, len - drop, b);
-    } else {
-      here = zpack(32 + 64, len - drop, 0);
-    }
-    incr = 1u << (len - drop);
-    fill = 1u << curr;
-    min = fill;
-    do { fill -= incr; table[next + (huff >> drop) + fill] = here; } while (fill != 0);
-    incr = 1u << (len - 1);
-    while (huff & incr) incr >>= 1;
-    if (incr != 0) { huff &= incr - 1; huff += incr; } else huff = 0;
-    sym++;
-    if (--count[len] == 0) {
-      if (len == max) break;
-      len = lens[work[sym]];
-    }
-    if (len > root && (huff & mask) != low) {
-      if (drop == 0) drop = root;
-      next += 1u << curr;
-      curr = len - drop;
-      left = 1 << curr;
-      while (curr + drop < max) {
-        left -= count[curr + drop];
-        if (left <= 0) break;
-        curr++;
-        left <<= 1;
-      }
-      used += 1u << curr;
-      if (ZS_OVER(used)) return 1;
-      low = huff & mask;
-      table[low] = zpack(curr, root, next);
-    }
-  }
-  if (huff != 0) {
-    here = zpack(64, len - drop, 0);
-    while (huff != 0) {
-      if (drop != 0 && (huff & mask) != low) {
-        drop = 0;
-        len = root;
-        next = 0;
-        curr = root;
-        here = zpack(64, len, 0);
-      }
-      table[next + (huff >> drop)] = here;
-      incr = 1u << (len - 1);
-      while (huff & incr) incr >>= 1;
-      if (incr != 0) { huff &= incr - 1; huff += incr; } else huff = 0;
-    }
-  }
-#undef ZS_OVER
-  *used_out = used;
-  *bits_io = root;
-  return 0;
-}
-
 // ---------------------------------------------------------- checksums (wave)
 static __device__ uint32_t zs_crc_mul(uint32_t a, uint32_t b) {
   uint32_t m = 1u << 31, p = 0;
@@ -980,340 +837,7 @@ size_t zs_inflate_smem_bytes(int wbits) {
   return sizeof(zs_lds) + ring;
 }
 
-// ===================================================================== fast path
-// One LANE per member.  The exact kernel above spends a whole wave on one
-// stream because it re-enacts the stream layer's call boundaries; a member
-// whose decoding those boundaries cannot change decodes straight through in one
-// lane instead: a deflate64 member (the reference decodes it with the slow state
-// machine only, whose window copies are exact), or a deflate / zlib / gzip member
-// that one inflate() call of the reference decodes whole (see ZS_INF_REF_WRAP
-// below).  zlib's own tables (inflate_table above, so invalid codes are
-// recognised exactly as the reference does), a 64-bit bit buffer, output written
-// to HBM and match history read back from it.  A member takes the exact path
-// instead (zs_k_inflate over the bailed members) on ANY condition that is not a
-// clean end of stream -- a data error, truncated input, a dictionary request,
-// gzip header fields, a checksum or length mismatch, or output capacity -- so
-// statuses, phases and messages always come from the exact state machine.
-struct zs_lane_tabs {
-  zcode codes[ENOUGH_LENS + ENOUGH_DISTS_9];
-  uint16_t lens[320];
-  uint16_t work[288];
-};
-
-struct zs_lane_reader {
-  const uint8_t* src;
-  uint32_t n, pos;  // bytes moved into hold so far
-  uint64_t hold;
-  uint32_t bits;
-  uint32_t pf;      // input bytes [pos, pos + 4), loaded one refill ahead (zero past the end)
-};
-
-static __device__ __forceinline__ uint32_t zs_lr_load4(const zs_lane_reader& R, uint32_t at) {
-  uint32_t v = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++)
-    if (at + k < R.n) v |= (uint32_t)R.src[at + k] << (8 * k);
-  return v;
-}
-// bits < 32 -> bits >= 32: the prefetched word enters hold and the next one is
-// requested, so its latency overlaps the decoding of the bits just added
-static __device__ __forceinline__ void zs_lr_fill(zs_lane_reader& R) {
-  R.hold |= (uint64_t)R.pf << R.bits;
-  R.bits += 32;
-  R.pos += 4;
-  R.pf = zs_lr_load4(R, R.pos);
-}
-// bits consumed so far
-static __device__ __forceinline__ uint64_t zs_lr_bitpos(const zs_lane_reader& R) {
-  return (uint64_t)R.pos * 8u - R.bits;
-}
-// consumed bits beyond the input: a truncated stream (the exact path reports it)
-static __device__ __forceinline__ bool zs_lr_over(const zs_lane_reader& R) {
-  return zs_lr_bitpos(R) > (uint64_t)R.n * 8u;
-}
-static __device__ __forceinline__ uint32_t zs_lr_take(zs_lane_reader& R, uint32_t k) {  // k <= 32
-  if (R.bits < k) zs_lr_fill(R);
-  const uint32_t v = (uint32_t)R.hold & (k == 32 ? 0xffffffffu : ((1u << k) - 1));
-  R.hold >>= k;
-  R.bits -= k;
-  return v;
-}
-static __device__ __forceinline__ void zs_lr_align(zs_lane_reader& R) {
-  const uint32_t d = R.bits & 7u;
-  R.hold >>= d;
-  R.bits -= d;
-}
-
-// decode one Huffman symbol with a zlib table (root `rbits`); returns the final entry
-static __device__ __forceinline__ zcode zs_lane_decode(zs_lane_reader& R, const zcode* t, uint32_t rbits) {
-  if (R.bits < 32) zs_lr_fill(R);
-  zcode here = t[(uint32_t)R.hold & ((1u << rbits) - 1)];
-  if (C_OP(here) && (C_OP(here) & 0xf0) == 0) {  // second-level table
-    const uint32_t rb = C_BITS(here);
-    const zcode last = here;
-    here = t[C_VAL(last) + (((uint32_t)R.hold & ((1u << (rb + C_OP(last))) - 1)) >> rb)];
-    R.hold >>= rb;
-    R.bits -= rb;
-  }
-  R.hold >>= C_BITS(here);
-  R.bits -= C_BITS(here);
-  return here;
-}
-
-// LDS root tables of one lane: 8-bit lit/len and 6-bit distance roots, u16
-// entries (code length << 12 | symbol), 0 = code longer than the root (the lane
-// then decodes with its zlib table in HBM).  640 B per lane: four 64-lane
-// workgroups fill a CU's 160 KB.
-#define ZS_LROOT 8u
-#define ZS_DROOT 6u
-struct zs_lane_lds {
-  uint16_t lit[1u << ZS_LROOT];
-  uint16_t dist[1u << ZS_DROOT];
-};
-
-static __device__ void zs_lane_root(uint16_t* tab, uint32_t rbits, const uint16_t* lens, uint32_t n) {
-  uint32_t count[16], next[16];
-  for (uint32_t l = 0; l < 16; l++) count[l] = 0;
-  for (uint32_t i = 0; i < n; i++) count[lens[i]]++;
-  count[0] = 0;
-  uint32_t code = 0;
-  for (uint32_t l = 1; l < 16; l++) {  // canonical first codes (RFC 1951 3.2.2)
-    code = (code + count[l - 1]) << 1;
-    next[l] = code;
-  }
-  for (uint32_t k = 0; k < (1u << rbits); k++) tab[k] = 0;
-  for (uint32_t sym = 0; sym < n; sym++) {
-    const uint32_t l = lens[sym];
-    if (l == 0) continue;
-    const uint32_t c = next[l]++;
-    if (l > rbits) continue;
-    const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);  // the stream sends codes MSB first
-    for (uint32_t k = r; k < (1u << rbits); k += 1u << l) tab[k] = (uint16_t)((l << 12) | sym);
-  }
-}
-
-// a root-table symbol as the zlib table entry the decoder consumes (zs_lbase /
-// zs_dbase's ops: 16 + extra bits, deflate64 128 + extra bits)
-static __device__ __forceinline__ zcode zs_lit_entry(uint32_t sym, bool d64) {
-  if (sym < 256) return zpack(0, 0, sym);
-  if (sym == 256) return zpack(32 + 64, 0, 0);
-  const uint32_t c = sym - 257;  // length codes: base / extra bits (inflate/constants.ts:8-23)
-  const uint32_t f = d64 ? 128u : 16u;
-  if (c < 8) return zpack(f, 0, c + 3);
-  if (c == 28) return d64 ? zpack(128 + 16, 0, 3) : zpack(16, 0, 258);  // deflate64: 3 + 16 extra bits
-  const uint32_t x = (c >> 2) - 1;
-  return zpack(f + x, 0, ((4u | (c & 3u)) << x) + 3u);
-}
-static __device__ __forceinline__ zcode zs_dist_entry(uint32_t d, bool d64) {
-  const uint32_t f = d64 ? 128u : 16u;
-  if (d < 4) return zpack(f, 0, d + 1);
-  const uint32_t x = (d >> 1) - 1;  // codes 30/31 (deflate64 only): 32769 / 49153 + 14 extra bits
-  return zpack(f + x, 0, ((2u | (d & 1u)) << x) + 1u);
-}
-
-__global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
-                                                        const uint64_t* __restrict__ in_off,
-                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
-                                                        const uint64_t* __restrict__ out_off,
-                                                        const uint32_t* __restrict__ out_cap, int wbits, uint32_t n_members,
-                                                        zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
-                                                        uint32_t* __restrict__ lens_out, int flags) {
-  extern __shared__ zs_lane_lds LL[];  // blockDim.x entries
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n_members) return;
-  zs_lane_tabs& T = tabs[s];
-  zs_lane_lds& F = LL[threadIdx.x];
-  zs_lane_reader R;
-  R.src = in + in_off[s];
-  R.n = in_len[s];
-  R.pos = 0;
-  R.hold = 0;
-  R.bits = 0;
-  R.pf = zs_lr_load4(R, 0);
-  uint8_t* dst = out + out_off[s];
-  // This path decodes a member in one go, without the stream layer's call
-  // boundaries.  A member whose input fits one 32 KiB sub-chunk and whose
-  // output fits one 64 KiB output buffer is decoded by ONE inflate() call of
-  // the reference (streams.ts:6-7,78-93) that never copies from the window, so
-  // the window-wrap behaviour (ZS_INF_REF_WRAP) cannot arise; any other member
-  // takes the exact path, which emulates the calls.
-  // deflate64 members never reach inflate_fast in the reference (inflate.ts:841),
-  // so they carry no call-boundary behaviour and decode here at any size.
-  const bool d64 = wbits == -16;
-  const bool ref_wrap = (flags & ZS_INF_REF_WRAP) != 0 && !d64;
-  const uint32_t cap = ref_wrap ? min(out_cap[s], 65536u) : out_cap[s];
-  const uint32_t lmask = d64 ? 31u : 15u;  // length extra-bit mask (inflate.ts:891)
-  uint32_t total = 0;
-  zs_lane_res r = {1u, 0u, 0u, 0u};
-  const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
-  bool bail = ref_wrap && R.n > 32768u;  // several sub-chunks: exact path
-  // ---- wrapper header (inflate.ts:377-580): plain zlib / gzip headers only
-  if (!bail && wrap) {
-    const uint32_t b0 = zs_lr_take(R, 8), b1 = zs_lr_take(R, 8);
-    if ((wrap & 2) && b0 == 0x1f && b1 == 0x8b) {
-      const uint32_t cm = zs_lr_take(R, 8), flg = zs_lr_take(R, 8);
-      zs_lr_take(R, 32);  // MTIME
-      zs_lr_take(R, 16);  // XFL, OS
-      if (cm != 8 || flg != 0) bail = true;  // FEXTRA / FNAME / FCOMMENT / FHCRC / reserved: exact path
-    } else if (wrap & 1) {
-      if (((b0 << 8) | b1) % 31 || (b0 & 15) != 8 || (b0 >> 4) + 8 > 15 || (b1 & 0x20)) bail = true;
-    } else {
-      bail = true;  // "incorrect header check"
-    }
-  }
-  // ---- blocks
-  bool last = false;
-  while (!bail && !last) {
-    last = zs_lr_take(R, 1) != 0;
-    const uint32_t type = zs_lr_take(R, 2);
-    const zcode* lt;
-    const zcode* dt;
-    uint32_t lbits, dbits;
-    if (type == 0) {  // stored (inflate.ts:615-660)
-      zs_lr_align(R);
-      const uint32_t len = zs_lr_take(R, 16), nlen = zs_lr_take(R, 16);
-      if (len != (nlen ^ 0xffffu) || zs_lr_over(R) || total + len > cap) { bail = true; break; }
-      for (uint32_t i = 0; i < len; i++) dst[total + i] = (uint8_t)zs_lr_take(R, 8);
-      total += len;
-      if (zs_lr_over(R)) { bail = true; break; }
-      continue;
-    }
-    if (type == 1) {  // fixed tables (inflate.ts:218-280)
-      uint32_t sym, used;
-      for (sym = 0; sym < 144; sym++) T.lens[sym] = 8;
-      for (; sym < 256; sym++) T.lens[sym] = 9;
-      for (; sym < 280; sym++) T.lens[sym] = 7;
-      for (; sym < 288; sym++) T.lens[sym] = 8;
-      lbits = 9;
-      zs_inflate_table(LENS, T.lens, 288, T.codes, &lbits, T.work, d64, &used);
-      for (sym = 0; sym < 32; sym++) T.lens[sym] = 5;
-      dbits = 5;
-      zs_inflate_table(DISTS, T.lens, 32, T.codes + used, &dbits, T.work, d64, &sym);
-      lt = T.codes;
-      dt = T.codes + used;
-      for (sym = 0; sym < 288; sym++) T.lens[sym] = sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8;
-      zs_lane_root(F.lit, ZS_LROOT, T.lens, 286);  // 286/287 stay out of the root: invalid codes decode via T
-      for (sym = 0; sym < 30; sym++) T.lens[sym] = 5;
-      zs_lane_root(F.dist, ZS_DROOT, T.lens, d64 ? 32 : 30);  // deflate: 30/31 likewise
-    } else if (type == 2) {  // dynamic (inflate.ts:662-836)
-      const uint32_t nlen = zs_lr_take(R, 5) + 257, ndist = zs_lr_take(R, 5) + 1, ncode = zs_lr_take(R, 4) + 4;
-      if (nlen > 286 || (!d64 && ndist > 30)) { bail = true; break; }
-      uint32_t i;
-      for (i = 0; i < ncode; i++) T.lens[ZS_BL_ORDER[i]] = (uint16_t)zs_lr_take(R, 3);
-      for (; i < 19; i++) T.lens[ZS_BL_ORDER[i]] = 0;
-      uint32_t cbits = 7, used;
-      if (zs_inflate_table(CODES, T.lens, 19, T.codes, &cbits, T.work, d64, &used)) { bail = true; break; }
-      i = 0;
-      while (i < nlen + ndist) {
-        const zcode here = zs_lane_decode(R, T.codes, cbits);
-        const uint32_t v = C_VAL(here);
-        if (v < 16) { T.lens[i++] = (uint16_t)v; continue; }
-        uint32_t rep, val = 0;
-        if (v == 16) {
-          if (i == 0) { bail = true; break; }
-          val = T.lens[i - 1];
-          rep = 3 + zs_lr_take(R, 2);
-        } else if (v == 17) {
-          rep = 3 + zs_lr_take(R, 3);
-        } else {
-          rep = 11 + zs_lr_take(R, 7);
-        }
-        if (i + rep > nlen + ndist) { bail = true; break; }
-        while (rep--) T.lens[i++] = (uint16_t)val;
-      }
-      if (bail || zs_lr_over(R) || T.lens[256] == 0) { bail = true; break; }
-      lbits = 9;
-      uint32_t lused, dused;
-      if (zs_inflate_table(LENS, T.lens, nlen, T.codes, &lbits, T.work, d64, &lused)) { bail = true; break; }
-      dbits = 6;
-      if (zs_inflate_table(DISTS, T.lens + nlen, ndist, T.codes + lused, &dbits, T.work, d64, &dused)) {
-        bail = true;
-        break;
-      }
-      lt = T.codes;
-      dt = T.codes + lused;
-      zs_lane_root(F.lit, ZS_LROOT, T.lens, nlen);
-      zs_lane_root(F.dist, ZS_DROOT, T.lens + nlen, ndist);
-    } else {
-      bail = true;  // "invalid block type"
-      break;
-    }
-    // symbols (inffast.ts:5-228 semantics, without the call boundaries)
-    for (;;) {
-      if (R.bits < 32) zs_lr_fill(R);
-      zcode here;
-      const uint32_t fe = F.lit[(uint32_t)R.hold & ((1u << ZS_LROOT) - 1)];
-      if (fe >> 12) {
-        R.hold >>= fe >> 12;
-        R.bits -= fe >> 12;
-        here = zs_lit_entry(fe & 0x1ffu, d64);
-      } else {
-        here = zs_lane_decode(R, lt, lbits);
-      }
-      uint32_t op = C_OP(here);
-      if (op == 0) {
-        if (total >= cap) { bail = true; break; }
-        dst[total++] = (uint8_t)C_VAL(here);
-        continue;
-      }
-      if (op & 32) break;                   // end of block
-      if (op & 64) { bail = true; break; }  // "invalid literal/length code"
-      uint32_t len = C_VAL(here) + zs_lr_take(R, op & lmask);
-      if (R.bits < 32) zs_lr_fill(R);
-      const uint32_t de = F.dist[(uint32_t)R.hold & ((1u << ZS_DROOT) - 1)];
-      if (de >> 12) {
-        R.hold >>= de >> 12;
-        R.bits -= de >> 12;
-        here = zs_dist_entry(de & 0x1fu, d64);
-      } else {
-        here = zs_lane_decode(R, dt, dbits);
-      }
-      op = C_OP(here);
-      if (op & 64) { bail = true; break; }  // "invalid distance code"
-      const uint32_t dist = C_VAL(here) + zs_lr_take(R, op & 15u);
-      if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
-      const uint8_t* from = dst + total - dist;
-      uint8_t* to = dst + total;
-      if (dist >= 8) {  // 8 independent loads, then 8 stores: one memory round trip per 8 bytes
-        for (uint32_t i = 0; i < len; i += 8) {
-          uint8_t b[8];
-#pragma unroll
-          for (int k = 0; k < 8; k++) b[k] = i + k < len ? from[i + k] : 0;
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            if (i + k < len) to[i + k] = b[k];
-        }
-      } else {  // overlapping copy: the source is being written
-        for (uint32_t i = 0; i < len; i++) to[i] = from[i];
-      }
-      total += len;
-    }
-    if (zs_lr_over(R)) bail = true;
-  }
-  // ---- trailer (inflate.ts:1006-1036)
-  if (!bail && wrap) {
-    zs_lr_align(R);
-    const uint32_t a = zs_lr_take(R, 32);
-    if (wrap & 2 && !(wrap & 1)) {  // gzip: crc32 LE, then ISIZE LE
-      r.want = a;
-      const uint32_t isize = zs_lr_take(R, 32);
-      if (isize != total) bail = true;
-    } else {
-      r.want = __builtin_bswap32(a);  // zlib: adler32 big-endian
-    }
-    if (zs_lr_over(R)) bail = true;
-  }
-  if (!bail) {
-    r.bail = 0;
-    r.out_len = total;
-    r.consumed = (uint32_t)((zs_lr_bitpos(R) + 7u) >> 3);
-  }
-  res[s] = r;
-  lens_out[s] = r.out_len;  // for the checksum pass over the decoded bytes
-}
-
-size_t zs_inflate_lane_scratch_bytes() { return sizeof(zs_lane_tabs); }
-size_t zs_inflate_lane_lds_bytes() { return sizeof(zs_lane_lds); }
+// The lane-per-member fast path lives in inflate_lane.hip.
 
 // checksum of the decoded output against the trailer: a mismatch sends the member to the exact path
 __global__ void zs_k_inflate_lane_verify(zs_lane_res* __restrict__ res, const uint32_t* __restrict__ check,

@@ -1,0 +1,341 @@
+// inflate_lane.hip -- the lane-per-member inflate path of zs_inflate_batch*
+// (see the comment below); zs_k_inflate in inflate.hip is the exact path.
+#include <hip/hip_runtime.h>
+#include "zs_common.h"
+#include "zs_inflate.h"
+#include "zs_inftab.h"
+
+// One LANE per member.  The exact kernel above spends a whole wave on one
+// stream because it re-enacts the stream layer's call boundaries; a member
+// whose decoding those boundaries cannot change decodes straight through in one
+// lane instead: a deflate64 member (the reference decodes it with the slow state
+// machine only, whose window copies are exact), or a deflate / zlib / gzip member
+// that one inflate() call of the reference decodes whole (see ZS_INF_REF_WRAP
+// below).  zlib's own tables (inflate_table above, so invalid codes are
+// recognised exactly as the reference does), a 64-bit bit buffer, output written
+// to HBM and match history read back from it.  A member takes the exact path
+// instead (zs_k_inflate over the bailed members) on ANY condition that is not a
+// clean end of stream -- a data error, truncated input, a dictionary request,
+// gzip header fields, a checksum or length mismatch, or output capacity -- so
+// statuses, phases and messages always come from the exact state machine.
+struct zs_lane_tabs {
+  zcode codes[ENOUGH_LENS + ENOUGH_DISTS_9];
+  uint16_t lens[320];
+  uint16_t work[288];
+};
+
+struct zs_lane_reader {
+  const uint8_t* src;
+  uint32_t n, pos;  // bytes moved into hold so far
+  uint64_t hold;
+  uint32_t bits;
+  uint32_t pf;      // input bytes [pos, pos + 4), loaded one refill ahead (zero past the end)
+};
+
+static __device__ __forceinline__ uint32_t zs_lr_load4(const zs_lane_reader& R, uint32_t at) {
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++)
+    if (at + k < R.n) v |= (uint32_t)R.src[at + k] << (8 * k);
+  return v;
+}
+// bits < 32 -> bits >= 32: the prefetched word enters hold and the next one is
+// requested, so its latency overlaps the decoding of the bits just added
+static __device__ __forceinline__ void zs_lr_fill(zs_lane_reader& R) {
+  R.hold |= (uint64_t)R.pf << R.bits;
+  R.bits += 32;
+  R.pos += 4;
+  R.pf = zs_lr_load4(R, R.pos);
+}
+// bits consumed so far
+static __device__ __forceinline__ uint64_t zs_lr_bitpos(const zs_lane_reader& R) {
+  return (uint64_t)R.pos * 8u - R.bits;
+}
+// consumed bits beyond the input: a truncated stream (the exact path reports it)
+static __device__ __forceinline__ bool zs_lr_over(const zs_lane_reader& R) {
+  return zs_lr_bitpos(R) > (uint64_t)R.n * 8u;
+}
+static __device__ __forceinline__ uint32_t zs_lr_take(zs_lane_reader& R, uint32_t k) {  // k <= 32
+  if (R.bits < k) zs_lr_fill(R);
+  const uint32_t v = (uint32_t)R.hold & (k == 32 ? 0xffffffffu : ((1u << k) - 1));
+  R.hold >>= k;
+  R.bits -= k;
+  return v;
+}
+static __device__ __forceinline__ void zs_lr_align(zs_lane_reader& R) {
+  const uint32_t d = R.bits & 7u;
+  R.hold >>= d;
+  R.bits -= d;
+}
+
+// decode one Huffman symbol with a zlib table (root `rbits`); returns the final entry
+static __device__ __forceinline__ zcode zs_lane_decode(zs_lane_reader& R, const zcode* t, uint32_t rbits) {
+  if (R.bits < 32) zs_lr_fill(R);
+  zcode here = t[(uint32_t)R.hold & ((1u << rbits) - 1)];
+  if (C_OP(here) && (C_OP(here) & 0xf0) == 0) {  // second-level table
+    const uint32_t rb = C_BITS(here);
+    const zcode last = here;
+    here = t[C_VAL(last) + (((uint32_t)R.hold & ((1u << (rb + C_OP(last))) - 1)) >> rb)];
+    R.hold >>= rb;
+    R.bits -= rb;
+  }
+  R.hold >>= C_BITS(here);
+  R.bits -= C_BITS(here);
+  return here;
+}
+
+// LDS root tables of one lane: 8-bit lit/len and 6-bit distance roots, u16
+// entries (code length << 12 | symbol), 0 = code longer than the root (the lane
+// then decodes with its zlib table in HBM).  640 B per lane: four 64-lane
+// workgroups fill a CU's 160 KB.
+#define ZS_LROOT 8u
+#define ZS_DROOT 6u
+struct zs_lane_lds {
+  uint16_t lit[1u << ZS_LROOT];
+  uint16_t dist[1u << ZS_DROOT];
+};
+
+static __device__ void zs_lane_root(uint16_t* tab, uint32_t rbits, const uint16_t* lens, uint32_t n) {
+  uint32_t count[16], next[16];
+  for (uint32_t l = 0; l < 16; l++) count[l] = 0;
+  for (uint32_t i = 0; i < n; i++) count[lens[i]]++;
+  count[0] = 0;
+  uint32_t code = 0;
+  for (uint32_t l = 1; l < 16; l++) {  // canonical first codes (RFC 1951 3.2.2)
+    code = (code + count[l - 1]) << 1;
+    next[l] = code;
+  }
+  for (uint32_t k = 0; k < (1u << rbits); k++) tab[k] = 0;
+  for (uint32_t sym = 0; sym < n; sym++) {
+    const uint32_t l = lens[sym];
+    if (l == 0) continue;
+    const uint32_t c = next[l]++;
+    if (l > rbits) continue;
+    const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);  // the stream sends codes MSB first
+    for (uint32_t k = r; k < (1u << rbits); k += 1u << l) tab[k] = (uint16_t)((l << 12) | sym);
+  }
+}
+
+// a root-table symbol as the zlib table entry the decoder consumes (zs_lbase /
+// zs_dbase's ops: 16 + extra bits, deflate64 128 + extra bits)
+static __device__ __forceinline__ zcode zs_lit_entry(uint32_t sym, bool d64) {
+  if (sym < 256) return zpack(0, 0, sym);
+  if (sym == 256) return zpack(32 + 64, 0, 0);
+  const uint32_t c = sym - 257;  // length codes: base / extra bits (inflate/constants.ts:8-23)
+  const uint32_t f = d64 ? 128u : 16u;
+  if (c < 8) return zpack(f, 0, c + 3);
+  if (c == 28) return d64 ? zpack(128 + 16, 0, 3) : zpack(16, 0, 258);  // deflate64: 3 + 16 extra bits
+  const uint32_t x = (c >> 2) - 1;
+  return zpack(f + x, 0, ((4u | (c & 3u)) << x) + 3u);
+}
+static __device__ __forceinline__ zcode zs_dist_entry(uint32_t d, bool d64) {
+  const uint32_t f = d64 ? 128u : 16u;
+  if (d < 4) return zpack(f, 0, d + 1);
+  const uint32_t x = (d >> 1) - 1;  // codes 30/31 (deflate64 only): 32769 / 49153 + 14 extra bits
+  return zpack(f + x, 0, ((2u | (d & 1u)) << x) + 1u);
+}
+
+__global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off,
+                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_off,
+                                                        const uint32_t* __restrict__ out_cap, int wbits, uint32_t n_members,
+                                                        zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
+                                                        uint32_t* __restrict__ lens_out, int flags) {
+  extern __shared__ zs_lane_lds LL[];  // blockDim.x entries
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_members) return;
+  zs_lane_tabs& T = tabs[s];
+  zs_lane_lds& F = LL[threadIdx.x];
+  zs_lane_reader R;
+  R.src = in + in_off[s];
+  R.n = in_len[s];
+  R.pos = 0;
+  R.hold = 0;
+  R.bits = 0;
+  R.pf = zs_lr_load4(R, 0);
+  uint8_t* dst = out + out_off[s];
+  // This path decodes a member in one go, without the stream layer's call
+  // boundaries.  A member whose input fits one 32 KiB sub-chunk and whose
+  // output fits one 64 KiB output buffer is decoded by ONE inflate() call of
+  // the reference (streams.ts:6-7,78-93) that never copies from the window, so
+  // the window-wrap behaviour (ZS_INF_REF_WRAP) cannot arise; any other member
+  // takes the exact path, which emulates the calls.
+  // deflate64 members never reach inflate_fast in the reference (inflate.ts:841),
+  // so they carry no call-boundary behaviour and decode here at any size.
+  const bool d64 = wbits == -16;
+  const bool ref_wrap = (flags & ZS_INF_REF_WRAP) != 0 && !d64;
+  const uint32_t cap = ref_wrap ? min(out_cap[s], 65536u) : out_cap[s];
+  const uint32_t lmask = d64 ? 31u : 15u;  // length extra-bit mask (inflate.ts:891)
+  uint32_t total = 0;
+  zs_lane_res r = {1u, 0u, 0u, 0u};
+  const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
+  bool bail = ref_wrap && R.n > 32768u;  // several sub-chunks: exact path
+  // ---- wrapper header (inflate.ts:377-580): plain zlib / gzip headers only
+  if (!bail && wrap) {
+    const uint32_t b0 = zs_lr_take(R, 8), b1 = zs_lr_take(R, 8);
+    if ((wrap & 2) && b0 == 0x1f && b1 == 0x8b) {
+      const uint32_t cm = zs_lr_take(R, 8), flg = zs_lr_take(R, 8);
+      zs_lr_take(R, 32);  // MTIME
+      zs_lr_take(R, 16);  // XFL, OS
+      if (cm != 8 || flg != 0) bail = true;  // FEXTRA / FNAME / FCOMMENT / FHCRC / reserved: exact path
+    } else if (wrap & 1) {
+      if (((b0 << 8) | b1) % 31 || (b0 & 15) != 8 || (b0 >> 4) + 8 > 15 || (b1 & 0x20)) bail = true;
+    } else {
+      bail = true;  // "incorrect header check"
+    }
+  }
+  // ---- blocks
+  bool last = false;
+  while (!bail && !last) {
+    last = zs_lr_take(R, 1) != 0;
+    const uint32_t type = zs_lr_take(R, 2);
+    const zcode* lt;
+    const zcode* dt;
+    uint32_t lbits, dbits;
+    if (type == 0) {  // stored (inflate.ts:615-660)
+      zs_lr_align(R);
+      const uint32_t len = zs_lr_take(R, 16), nlen = zs_lr_take(R, 16);
+      if (len != (nlen ^ 0xffffu) || zs_lr_over(R) || total + len > cap) { bail = true; break; }
+      for (uint32_t i = 0; i < len; i++) dst[total + i] = (uint8_t)zs_lr_take(R, 8);
+      total += len;
+      if (zs_lr_over(R)) { bail = true; break; }
+      continue;
+    }
+    if (type == 1) {  // fixed tables (inflate.ts:218-280)
+      uint32_t sym, used;
+      for (sym = 0; sym < 144; sym++) T.lens[sym] = 8;
+      for (; sym < 256; sym++) T.lens[sym] = 9;
+      for (; sym < 280; sym++) T.lens[sym] = 7;
+      for (; sym < 288; sym++) T.lens[sym] = 8;
+      lbits = 9;
+      zs_inflate_table(LENS, T.lens, 288, T.codes, &lbits, T.work, d64, &used);
+      for (sym = 0; sym < 32; sym++) T.lens[sym] = 5;
+      dbits = 5;
+      zs_inflate_table(DISTS, T.lens, 32, T.codes + used, &dbits, T.work, d64, &sym);
+      lt = T.codes;
+      dt = T.codes + used;
+      for (sym = 0; sym < 288; sym++) T.lens[sym] = sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8;
+      zs_lane_root(F.lit, ZS_LROOT, T.lens, 286);  // 286/287 stay out of the root: invalid codes decode via T
+      for (sym = 0; sym < 30; sym++) T.lens[sym] = 5;
+      zs_lane_root(F.dist, ZS_DROOT, T.lens, d64 ? 32 : 30);  // deflate: 30/31 likewise
+    } else if (type == 2) {  // dynamic (inflate.ts:662-836)
+      const uint32_t nlen = zs_lr_take(R, 5) + 257, ndist = zs_lr_take(R, 5) + 1, ncode = zs_lr_take(R, 4) + 4;
+      if (nlen > 286 || (!d64 && ndist > 30)) { bail = true; break; }
+      uint32_t i;
+      for (i = 0; i < ncode; i++) T.lens[ZS_BL_ORDER[i]] = (uint16_t)zs_lr_take(R, 3);
+      for (; i < 19; i++) T.lens[ZS_BL_ORDER[i]] = 0;
+      uint32_t cbits = 7, used;
+      if (zs_inflate_table(CODES, T.lens, 19, T.codes, &cbits, T.work, d64, &used)) { bail = true; break; }
+      i = 0;
+      while (i < nlen + ndist) {
+        const zcode here = zs_lane_decode(R, T.codes, cbits);
+        const uint32_t v = C_VAL(here);
+        if (v < 16) { T.lens[i++] = (uint16_t)v; continue; }
+        uint32_t rep, val = 0;
+        if (v == 16) {
+          if (i == 0) { bail = true; break; }
+          val = T.lens[i - 1];
+          rep = 3 + zs_lr_take(R, 2);
+        } else if (v == 17) {
+          rep = 3 + zs_lr_take(R, 3);
+        } else {
+          rep = 11 + zs_lr_take(R, 7);
+        }
+        if (i + rep > nlen + ndist) { bail = true; break; }
+        while (rep--) T.lens[i++] = (uint16_t)val;
+      }
+      if (bail || zs_lr_over(R) || T.lens[256] == 0) { bail = true; break; }
+      lbits = 9;
+      uint32_t lused, dused;
+      if (zs_inflate_table(LENS, T.lens, nlen, T.codes, &lbits, T.work, d64, &lused)) { bail = true; break; }
+      dbits = 6;
+      if (zs_inflate_table(DISTS, T.lens + nlen, ndist, T.codes + lused, &dbits, T.work, d64, &dused)) {
+        bail = true;
+        break;
+      }
+      lt = T.codes;
+      dt = T.codes + lused;
+      zs_lane_root(F.lit, ZS_LROOT, T.lens, nlen);
+      zs_lane_root(F.dist, ZS_DROOT, T.lens + nlen, ndist);
+    } else {
+      bail = true;  // "invalid block type"
+      break;
+    }
+    // symbols (inffast.ts:5-228 semantics, without the call boundaries)
+    for (;;) {
+      if (R.bits < 32) zs_lr_fill(R);
+      zcode here;
+      const uint32_t fe = F.lit[(uint32_t)R.hold & ((1u << ZS_LROOT) - 1)];
+      if (fe >> 12) {
+        R.hold >>= fe >> 12;
+        R.bits -= fe >> 12;
+        here = zs_lit_entry(fe & 0x1ffu, d64);
+      } else {
+        here = zs_lane_decode(R, lt, lbits);
+      }
+      uint32_t op = C_OP(here);
+      if (op == 0) {
+        if (total >= cap) { bail = true; break; }
+        dst[total++] = (uint8_t)C_VAL(here);
+        continue;
+      }
+      if (op & 32) break;                   // end of block
+      if (op & 64) { bail = true; break; }  // "invalid literal/length code"
+      uint32_t len = C_VAL(here) + zs_lr_take(R, op & lmask);
+      if (R.bits < 32) zs_lr_fill(R);
+      const uint32_t de = F.dist[(uint32_t)R.hold & ((1u << ZS_DROOT) - 1)];
+      if (de >> 12) {
+        R.hold >>= de >> 12;
+        R.bits -= de >> 12;
+        here = zs_dist_entry(de & 0x1fu, d64);
+      } else {
+        here = zs_lane_decode(R, dt, dbits);
+      }
+      op = C_OP(here);
+      if (op & 64) { bail = true; break; }  // "invalid distance code"
+      const uint32_t dist = C_VAL(here) + zs_lr_take(R, op & 15u);
+      if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
+      const uint8_t* from = dst + total - dist;
+      uint8_t* to = dst + total;
+      if (dist >= 8) {  // 8 independent loads, then 8 stores: one memory round trip per 8 bytes
+        for (uint32_t i = 0; i < len; i += 8) {
+          uint8_t b[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) b[k] = i + k < len ? from[i + k] : 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            if (i + k < len) to[i + k] = b[k];
+        }
+      } else {  // overlapping copy: the source is being written
+        for (uint32_t i = 0; i < len; i++) to[i] = from[i];
+      }
+      total += len;
+    }
+    if (zs_lr_over(R)) bail = true;
+  }
+  // ---- trailer (inflate.ts:1006-1036)
+  if (!bail && wrap) {
+    zs_lr_align(R);
+    const uint32_t a = zs_lr_take(R, 32);
+    if (wrap & 2 && !(wrap & 1)) {  // gzip: crc32 LE, then ISIZE LE
+      r.want = a;
+      const uint32_t isize = zs_lr_take(R, 32);
+      if (isize != total) bail = true;
+    } else {
+      r.want = __builtin_bswap32(a);  // zlib: adler32 big-endian
+    }
+    if (zs_lr_over(R)) bail = true;
+  }
+  if (!bail) {
+    r.bail = 0;
+    r.out_len = total;
+    r.consumed = (uint32_t)((zs_lr_bitpos(R) + 7u) >> 3);
+  }
+  res[s] = r;
+  lens_out[s] = r.out_len;  // for the checksum pass over the decoded bytes
+}
+
+size_t zs_inflate_lane_scratch_bytes() { return sizeof(zs_lane_tabs); }
+size_t zs_inflate_lane_lds_bytes() { return sizeof(zs_lane_lds); }
+

@@ -43,22 +43,22 @@ struct zs_inflate_result {
   uint32_t consumed;
 };
 
-// Outcome of the lane-per-member fast path (inflate.hip).
+// Outcome of the lane-per-member fast path (inflate_lane.hip).
 struct zs_lane_res {
   uint32_t bail;      // 0: decoded cleanly; 1: the exact path decides
   uint32_t out_len;
   uint32_t consumed;
   uint32_t want;      // trailer check value (zlib: adler32, gzip: crc32)
 };
-struct zs_lane_tabs;
 
 __global__ void zs_k_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                              const uint64_t* out_off, const uint32_t* out_cap, int wbits, zs_inflate_result* res,
                              const zs_lane_res* only, int flags);
+struct zs_lane_tabs;
 __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, uint32_t n_members,
                                   zs_lane_tabs* tabs, zs_lane_res* res, uint32_t* lens_out, int flags);
 __global__ void zs_k_inflate_lane_verify(zs_lane_res* res, const uint32_t* check, uint32_t n);
 size_t zs_inflate_smem_bytes(int wbits);
-size_t zs_inflate_lane_scratch_bytes();
 size_t zs_inflate_lane_lds_bytes();
+size_t zs_inflate_lane_scratch_bytes();

@@ -99,6 +99,8 @@ def lib():
     L.zs_adler32_batch_device.argtypes = [_P, ctypes.c_uint32, _P, _U64P, _U32P, _P, _P]
     L.zs_last_batch_ms.restype = ctypes.c_double
     L.zs_last_batch_ms.argtypes = [_P]
+    L.zs_last_inflate_lane_count.restype = ctypes.c_uint32
+    L.zs_last_inflate_lane_count.argtypes = [_P]
     L.zs_last_phase_ms.restype = ctypes.c_double
     L.zs_last_phase_ms.argtypes = [_P, ctypes.c_char_p]
     L.zs_set_timing.argtypes = [_P, ctypes.c_int]
@@ -174,6 +176,10 @@ class Engine:
 
     def set_timing(self, on: bool):
         self._L.zs_set_timing(self._ctx, 1 if on else 0)
+
+    def last_lane_count(self) -> int:
+        """members of the last inflate batch decoded by the lane path"""
+        return self._L.zs_last_inflate_lane_count(self._ctx)
 
     def last_ms(self, phase: Optional[str] = None) -> float:
         if phase is None:
