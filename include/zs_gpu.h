@@ -110,12 +110,21 @@ int zs_inflate_batch(zs_ctx *ctx, int wbits, uint32_t n_streams, const uint8_t *
 /* The z_stream message for a d_msg index (inflate.ts:397-1031, inffast.ts:108,197,210). */
 const char *zs_inflate_message(int32_t msg_index);
 
-/* Per-stream checksums of device-resident buffers (crc32.ts / adler32.ts),
- * written to d_check[i].  crc32 of an empty stream is 0, adler32 is 1. */
+/* Per-stream checksums, check[i] = crc32(seeds[i], in[i]) / adler32(seeds[i], in[i])
+ * with the reference's semantics (common/crc32.ts:26-58, common/adler32.ts:4-25):
+ * the seed is a running checksum being continued; an empty stream returns the
+ * seed unchanged.  seeds: host array of n_streams values, or NULL for the
+ * initial values (crc32 0, adler32 1).  The _device forms take device buffers
+ * and write d_check on the device (asynchronously on hip_stream); the host forms
+ * take host buffers and return when check[] is filled. */
 int zs_crc32_batch_device(zs_ctx *ctx, uint32_t n_streams, const uint8_t *d_in, const uint64_t *in_off,
-                          const uint32_t *in_len, uint32_t *d_check, void *hip_stream);
+                          const uint32_t *in_len, const uint32_t *seeds, uint32_t *d_check, void *hip_stream);
 int zs_adler32_batch_device(zs_ctx *ctx, uint32_t n_streams, const uint8_t *d_in, const uint64_t *in_off,
-                            const uint32_t *in_len, uint32_t *d_check, void *hip_stream);
+                            const uint32_t *in_len, const uint32_t *seeds, uint32_t *d_check, void *hip_stream);
+int zs_crc32_batch(zs_ctx *ctx, uint32_t n_streams, const uint8_t *in, const uint64_t *in_off,
+                   const uint32_t *in_len, const uint32_t *seeds, uint32_t *check);
+int zs_adler32_batch(zs_ctx *ctx, uint32_t n_streams, const uint8_t *in, const uint64_t *in_off,
+                     const uint32_t *in_len, const uint32_t *seeds, uint32_t *check);
 
 /* Kernel timing of the last batch call on this context (HIP events on the
  * stream the kernels ran on): total device milliseconds and the duration of

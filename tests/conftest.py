@@ -15,6 +15,12 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def engine():
+    # torch's HIP runtime first (tests that hand torch device buffers to the
+    # engine need it to see the device), then the engine's
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.init()
     import zsamd
 
     return zsamd.Engine(0)

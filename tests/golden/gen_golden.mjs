@@ -193,7 +193,42 @@ function genBatchPart(setName, K, P) {
   fs.writeFileSync(`/tmp/golden_${setName}_${P}.bin`, rec);
 }
 
+// Level 0 (deflate_stored, deflate.ts:1140-1279, reachable as {level: 0}): the
+// stored-block layout depends on the stream layer's 32 KiB input sub-chunks and
+// 64 KiB output buffers, so it is recorded per size: output length and hash, and
+// the stored blocks' lengths parsed back from the output.
+function storedBlocks(format, out) {
+  let p = format == "gzip" ? 10 : format == "deflate" ? 2 : 0;
+  const blocks = [];
+  for (;;) {
+    const hdr = out[p], len = out[p + 1] | (out[p + 2] << 8);
+    if ((hdr & 6) != 0) throw new Error("not a stored block");
+    blocks.push(len);
+    p += 5 + len;
+    if (hdr & 1) break;
+  }
+  return { blocks, end: p };
+}
+function genLevel0() {
+  const sizes = [0, 1, 5, 100, 4096, 32767, 32768, 32769, 65530, 65531, 65535, 65536, 65537, 65540, 70000, 98303,
+                 98304, 98305, 131071, 131072, 131073, 163840, 196608, 200003, 262144, 300000, 524288, 1048576, 1048581];
+  const cases = [];
+  for (const n of sizes) {
+    const input = text(streamSeed(50), n);
+    for (const format of FORMATS) {
+      const out = compress(format, 0, input);
+      const { blocks, end } = storedBlocks(format, out);
+      cases.push({ n, format, seed_index: 50, out_len: out.length, out_sha256: sha(out), blocks, trailer: out.length - end,
+                   out_hex: out.length <= 256 ? Buffer.from(out).toString("hex") : undefined });
+    }
+  }
+  fs.writeFileSync(path.join(HERE, "deflate_level0.json"), JSON.stringify({ generator: "gen_golden.mjs level0",
+    reference: "zlib-streams-ts v1.0.13 dist bundle", input: "text(streamSeed(50), n)", cases }, null, 0));
+  console.log("level0 cases", cases.length);
+}
+
 const [mode, a, b, c] = process.argv.slice(2);
 if (mode == "small") { genSmall(); genInflate(); }
+else if (mode == "level0") genLevel0();
 else if (mode == "batch") genBatchPart(a, +b, +c);
-else console.log("usage: node gen_golden.mjs small | batch SET K P");
+else console.log("usage: node gen_golden.mjs small | level0 | batch SET K P");

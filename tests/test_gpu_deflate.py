@@ -191,3 +191,24 @@ def test_c4_256k_streams_match_reference_goldens(engine, name, level):
 def test_lds_atomic_lane_order_selftest(engine):
     """The chain builder's hardware assumption (selftest.hip) holds on this part."""
     assert engine.selftest() == 0
+
+
+def test_level0_stored_layout_matches_reference_goldens(engine):
+    """Level 0 (deflate_stored, deflate.ts:1140-1279) through the stream layer:
+    tests/golden/deflate_level0.json, made by the reference bundle for sizes
+    0..1 MiB in the three formats (gen_golden.mjs level0)."""
+    import json
+    import os
+
+    g = json.load(open(os.path.join(golden_io.GOLDEN, "deflate_level0.json")))
+    by_fmt = {}
+    for c in g["cases"]:
+        by_fmt.setdefault(c["format"], []).append(c)
+    for fmt, cases in by_fmt.items():
+        inputs = [corpus.text(corpus.stream_seed(c["seed_index"]), c["n"]) for c in cases]
+        res = engine.compress_batch_raw(inputs, fmt, 0)
+        for c, (st, out) in zip(cases, res):
+            assert st == 1 and len(out) == c["out_len"] and corpus.sha256(out) == c["out_sha256"], (fmt, c["n"])
+    # and they decode (stored blocks) to their inputs
+    comp = engine.compress_batch(inputs, "gzip", 0)
+    assert engine.decompress_batch(comp, "gzip") == inputs

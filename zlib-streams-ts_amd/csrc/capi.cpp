@@ -279,6 +279,45 @@ __global__ void zs_k_copy_check(const uint32_t* check, zs_stream* streams, int n
   if (s < n) streams[s].check = check[s];
 }
 
+// level 0: stored blocks (zs_k_stored), trailer checksums from zs_k_checksum
+static int deflate_stored_batch(zs_ctx* c, int wrap, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                                const uint32_t* in_len, uint8_t* d_out, const uint64_t* out_off,
+                                const uint32_t* out_cap, int32_t* d_status, uint32_t* d_out_len, hipStream_t st) {
+  MetaLayout ml(n);
+  c->hmeta.resize(ml.bytes);
+  c->last_n = n;
+  uint8_t* hm = c->hmeta.data();
+  memcpy(hm + ml.in_off, in_off, 8ull * n);
+  memcpy(hm + ml.in_len, in_len, 4ull * n);
+  memcpy(hm + ml.out_off, out_off, 8ull * n);
+  memcpy(hm + ml.out_cap, out_cap, 4ull * n);
+  uint64_t max_total = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
+    const uint64_t t = (wrap == 0 ? 0 : wrap == 1 ? 6 : 18) + 5ull * (in_len[i] / ZS_STORED_CHUNK + 1) + in_len[i];
+    max_total = std::max(max_total, t);
+  }
+  HIPCHK(c->meta.ensure(ml.bytes));
+  HIPCHK(c->check.ensure(4ull * n));
+  HIPCHK(hipMemcpyAsync(c->meta.p, hm, ml.bytes, hipMemcpyHostToDevice, st));
+  uint8_t* dm = c->meta.as<uint8_t>();
+  const uint64_t* d_in_off = (const uint64_t*)(dm + ml.in_off);
+  const uint32_t* d_in_len = (const uint32_t*)(dm + ml.in_len);
+  MARK("start");
+  if (wrap) {
+    zs_k_checksum<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, c->check.as<uint32_t>(), wrap == 1 ? 1 : 2);
+    MARK("checksum");
+  }
+  const dim3 g((unsigned)((max_total + 4095) / 4096), n);  // 256 threads x 16 bytes per workgroup
+  zs_k_stored<<<g, 256, 0, st>>>(d_in, d_in_off, d_in_len, d_out, (const uint64_t*)(dm + ml.out_off),
+                                 (const uint32_t*)(dm + ml.out_cap), c->check.as<uint32_t>(), wrap, d_status,
+                                 d_out_len);
+  MARK("stored");
+  HIPCHK(hipGetLastError());
+  collect_marks(c);
+  return ZS_OK;
+}
+
 extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* d_in,
                                        const uint64_t* in_off, const uint32_t* in_len, uint8_t* d_out,
                                        const uint64_t* out_off, const uint32_t* out_cap, int32_t* d_status,
@@ -291,10 +330,11 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   else if (wbits == 31) wrap = 2;
   else return fail(ZS_STREAM_ERROR, "unsupported windowBits (use -15, 15 or 31)");
   if (level < 0 || level > 9) return fail(ZS_STREAM_ERROR, "invalid level");  // deflate.ts:281-294
-  if (level == 0) return fail(ZS_STREAM_ERROR, "level 0 (deflate_stored) is not implemented by the GPU engine");
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
+  if (level == 0) return deflate_stored_batch(c, wrap, n, d_in, in_off, in_len, d_out, out_off, out_cap, d_status,
+                                              d_out_len, st);
   // host-side layout: workspace bases
   MetaLayout ml(n);
   c->hmeta.resize(ml.bytes);
@@ -505,26 +545,23 @@ extern "C" int zs_deflate_batch(zs_ctx* c, int level, int wbits, uint32_t n, con
   return fetch_out(c, n, ooff.data(), d_len, out_len, out, out_off);  // out_len is 0 for failed streams
 }
 
-extern "C" int zs_crc32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
-                                     const uint32_t* in_len, uint32_t* d_check, void* hip_stream);
-extern "C" int zs_adler32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
-                                       const uint32_t* in_len, uint32_t* d_check, void* hip_stream);
-
 static int checksum_batch(zs_ctx* c, int kind, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
-                          const uint32_t* in_len, uint32_t* d_check, void* hip_stream) {
+                          const uint32_t* in_len, const uint32_t* seeds, uint32_t* d_check, void* hip_stream) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   MetaLayout ml(n);
-  c->hmeta.resize(ml.bytes);
+  c->hmeta.resize(ml.bytes + (seeds ? 4ull * n : 0));
   memcpy(c->hmeta.data() + ml.in_off, in_off, 8ull * n);
   memcpy(c->hmeta.data() + ml.in_len, in_len, 4ull * n);
-  HIPCHK(c->meta.ensure(ml.bytes));
-  HIPCHK(hipMemcpyAsync(c->meta.p, c->hmeta.data(), ml.bytes, hipMemcpyHostToDevice, st));
+  if (seeds) memcpy(c->hmeta.data() + ml.bytes, seeds, 4ull * n);
+  HIPCHK(c->meta.ensure(c->hmeta.size()));
+  HIPCHK(hipMemcpyAsync(c->meta.p, c->hmeta.data(), c->hmeta.size(), hipMemcpyHostToDevice, st));
   MARK("start");
   zs_k_checksum<<<n, 64, 0, st>>>(d_in, (const uint64_t*)(c->meta.as<uint8_t>() + ml.in_off),
-                                  (const uint32_t*)(c->meta.as<uint8_t>() + ml.in_len), d_check, kind);
+                                  (const uint32_t*)(c->meta.as<uint8_t>() + ml.in_len), d_check, kind,
+                                  seeds ? (const uint32_t*)(c->meta.as<uint8_t>() + ml.bytes) : nullptr);
   MARK("checksum");
   HIPCHK(hipGetLastError());
   collect_marks(c);
@@ -532,12 +569,40 @@ static int checksum_batch(zs_ctx* c, int kind, uint32_t n, const uint8_t* d_in, 
 }
 
 extern "C" int zs_crc32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
-                                     const uint32_t* in_len, uint32_t* d_check, void* hip_stream) {
-  return checksum_batch(c, 2, n, d_in, in_off, in_len, d_check, hip_stream);
+                                     const uint32_t* in_len, const uint32_t* seeds, uint32_t* d_check,
+                                     void* hip_stream) {
+  return checksum_batch(c, 2, n, d_in, in_off, in_len, seeds, d_check, hip_stream);
 }
 extern "C" int zs_adler32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
-                                       const uint32_t* in_len, uint32_t* d_check, void* hip_stream) {
-  return checksum_batch(c, 1, n, d_in, in_off, in_len, d_check, hip_stream);
+                                       const uint32_t* in_len, const uint32_t* seeds, uint32_t* d_check,
+                                       void* hip_stream) {
+  return checksum_batch(c, 1, n, d_in, in_off, in_len, seeds, d_check, hip_stream);
+}
+
+// host buffers: staged through the context's pinned buffer, results copied back
+static int checksum_host(zs_ctx* c, int kind, uint32_t n, const uint8_t* in, const uint64_t* in_off,
+                         const uint32_t* in_len, const uint32_t* seeds, uint32_t* check) {
+  if (!c) return fail(ZS_STREAM_ERROR, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  if (n == 0) return ZS_OK;
+  std::vector<uint64_t> doff;
+  uint64_t total = 0;
+  int r = stage_in(c, n, in, in_off, in_len, doff, total);
+  if (r != ZS_OK) return r;
+  HIPCHK(c->d_res.ensure(4ull * n + 16));
+  r = checksum_batch(c, kind, n, c->d_in.as<uint8_t>(), doff.data(), in_len, seeds, c->d_res.as<uint32_t>(), nullptr);
+  if (r != ZS_OK) return r;
+  HIPCHK(hipMemcpyAsync(check, c->d_res.p, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return ZS_OK;
+}
+extern "C" int zs_crc32_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* in_off,
+                              const uint32_t* in_len, const uint32_t* seeds, uint32_t* check) {
+  return checksum_host(c, 2, n, in, in_off, in_len, seeds, check);
+}
+extern "C" int zs_adler32_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* in_off,
+                                const uint32_t* in_len, const uint32_t* seeds, uint32_t* check) {
+  return checksum_host(c, 1, n, in, in_off, in_len, seeds, check);
 }
 
 // ------------------------------------------------------------------ corpus

@@ -9,6 +9,11 @@
 //   polynomial 0xedb88320).
 //   Adler-32 (common/adler32.ts:4-25): A = 1 + sum x_j, B = n + sum (n-j) x_j
 //   (mod 65521); each lane sums its segment, a wave reduction finishes it.
+// A per-stream seed continues a running checksum as crc32(crc, buf) /
+// adler32(adler, buf) do: CRC(seed, data) = seed * x^(8n) + CRC(0, data) (mod P),
+// and Adler with (a0, b0) = (seed & 0xffff, seed >> 16): A = a0 + sum x_j,
+// B = b0 + n a0 + sum (n-j) x_j.  An empty stream returns the seed unchanged,
+// unreduced, as the reference's loops never run (adler32.ts:14, crc32.ts:34-57).
 #include <hip/hip_runtime.h>
 #include "zs_common.h"
 #include "zs_kernels.h"
@@ -40,7 +45,7 @@ static __device__ uint32_t zs_x8nmodp(uint64_t len) {
 
 __global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                     const uint32_t* __restrict__ in_len, uint32_t* __restrict__ check,
-                                                    int kind) {
+                                                    int kind, const uint32_t* __restrict__ seeds) {
   __shared__ uint32_t T[256];
   __shared__ uint32_t seg_crc[64];
   const int s = blockIdx.x;
@@ -61,7 +66,8 @@ __global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ 
     seg_crc[lane] = c ^ 0xffffffffu;
     __syncthreads();
     if (lane == 0) {
-      uint32_t crc = 0;  // crc32 of nothing (crc32.ts:27-29)
+      const uint32_t seed = seeds ? seeds[s] : 0u;
+      uint32_t crc = seed;  // crc32 of nothing (crc32.ts:27-29): the seed
       if (n) {
         crc = seg_crc[0];
         const uint32_t xp = zs_x8nmodp(per);
@@ -71,6 +77,7 @@ __global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ 
           const uint32_t xl = hi - lo == per ? xp : zs_x8nmodp(hi - lo);
           crc = zs_multmodp(xl, crc) ^ seg_crc[i];
         }
+        if (seed) crc ^= zs_multmodp(zs_x8nmodp(n), seed);
       }
       check[s] = crc;
     }
@@ -88,9 +95,11 @@ __global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ 
       w += __shfl_down(w, d, 64);
     }
     if (lane == 0) {
-      const uint32_t A = (uint32_t)((1 + a) % 65521);
-      const uint32_t B = (uint32_t)(((uint64_t)n % 65521 + w) % 65521);
-      check[s] = (B << 16) | A;
+      const uint32_t seed = seeds ? seeds[s] : 1u;
+      const uint64_t a0 = seed & 0xffffu, b0 = seed >> 16;
+      const uint32_t A = (uint32_t)((a0 + a) % 65521);
+      const uint32_t B = (uint32_t)((b0 + ((uint64_t)n % 65521) * a0 + w) % 65521);
+      check[s] = n ? (B << 16) | A : seed;
     }
   }
 }

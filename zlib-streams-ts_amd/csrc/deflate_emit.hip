@@ -555,3 +555,68 @@ __global__ void zs_k_wrap(const zs_stream* __restrict__ streams, uint8_t* __rest
     for (int i = 0; i < 4; i++) put_byte(tb + 4 + i, in_len[s] >> (8 * i));
   }
 }
+
+// ------------------------------------------------------------------- level 0
+// deflate_stored (deflate.ts:1140-1279) under the stream layer's call pattern
+// (streams.ts:78-93: 32 KiB input sub-chunks per deflate(Z_NO_FLUSH) call, each
+// with a fresh 64 KiB output buffer, then deflate(Z_FINISH)): every full
+// sub-chunk leaves as one 32768-byte stored block copied straight from the
+// input, and Z_FINISH emits the remainder (possibly empty) as the last block.
+// The layout is a function of the length alone (pinned for 0..1 MiB against the
+// reference: tests/golden/deflate_level0.json), so each thread writes four
+// output words, mapping every output byte to a header byte or an input byte.
+__global__ __launch_bounds__(256) void zs_k_stored(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                   const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                   const uint64_t* __restrict__ out_off,
+                                                   const uint32_t* __restrict__ out_cap,
+                                                   const uint32_t* __restrict__ check, int wrap, int32_t* status,
+                                                   uint32_t* out_len_res) {
+  const uint32_t s = blockIdx.y;
+  const uint32_t n = in_len[s];
+  const uint32_t hl = wrap == 0 ? 0 : wrap == 1 ? 2 : 10, tl = wrap == 0 ? 0 : wrap == 1 ? 4 : 8;
+  const uint32_t nblk = n / ZS_STORED_CHUNK + 1;
+  const uint64_t body = 5ull * nblk + n;
+  const uint64_t total = hl + body + tl;
+  const bool fits = total <= out_cap[s];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    status[s] = fits ? ZS_Z_STREAM_END : ZS_Z_BUF_ERROR;
+    out_len_res[s] = (uint32_t)total;
+  }
+  if (!fits) return;
+  const uint8_t* src = in + in_off[s];
+  uint32_t* ow = (uint32_t*)(out + out_off[s]);
+  const uint32_t ck = wrap ? check[s] : 0;
+  const uint32_t xfl = 4u;  // level < 2 (deflate.ts:795)
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint64_t w = w0 + q;
+    if (4 * w >= total) break;
+    uint32_t word = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const uint64_t o = 4 * w + j;
+      uint32_t b = 0;
+      if (o >= total) {
+        b = 0;
+      } else if (o < hl) {
+        if (wrap == 1) b = o == 0 ? 0x78u : 0x01u;  // level_flags 0 (deflate.ts:757-771)
+        else b = o == 0 ? 31u : o == 1 ? 139u : o == 2 ? 8u : o == 8 ? xfl : o == 9 ? 255u : 0u;
+      } else if (o < hl + body) {
+        const uint64_t r = o - hl;
+        const uint32_t k = (uint32_t)(r / (ZS_STORED_CHUNK + 5)), p = (uint32_t)(r % (ZS_STORED_CHUNK + 5));
+        const uint32_t len = k + 1 == nblk ? n - k * ZS_STORED_CHUNK : ZS_STORED_CHUNK;
+        if (p == 0) b = k + 1 == nblk ? 1u : 0u;  // BFINAL, BTYPE 00, then byte alignment
+        else if (p < 3) b = (len >> (8 * (p - 1))) & 0xffu;
+        else if (p < 5) b = (~len >> (8 * (p - 3))) & 0xffu;
+        else b = src[(uint64_t)k * ZS_STORED_CHUNK + p - 5];
+      } else {
+        const uint32_t t = (uint32_t)(o - hl - body);
+        if (wrap == 1) b = (ck >> (24 - 8 * t)) & 0xffu;                        // adler32, big-endian
+        else b = t < 4 ? (ck >> (8 * t)) & 0xffu : (n >> (8 * (t - 4))) & 0xffu;  // crc32, ISIZE
+      }
+      word |= b << (8 * j);
+    }
+    ow[w] = word;
+  }
+}

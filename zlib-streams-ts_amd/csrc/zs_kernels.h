@@ -66,8 +66,11 @@ __global__ void zs_k_layout(const uint32_t* blk_base, zs_block* blocks, zs_strea
 __global__ void zs_k_emit(const uint8_t* in, const uint64_t* in_off, const uint64_t* pos_base, const uint32_t* blk_base,
                           const uint32_t* syms, const zs_block* blocks, const zs_stream* streams, const uint32_t* codes,
                           const uint32_t* hdr, uint8_t* out, const uint64_t* out_off, int wrap);
+__global__ void zs_k_stored(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                            const uint64_t* out_off, const uint32_t* out_cap, const uint32_t* check, int wrap,
+                            int32_t* status, uint32_t* out_len_res);
 __global__ void zs_k_wrap(const zs_stream* streams, uint8_t* out, const uint64_t* out_off, const uint32_t* in_len,
                           int wrap, int level, int nstreams);
 __global__ void zs_k_checksum(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t* check,
-                              int kind);
+                              int kind, const uint32_t* seeds = nullptr);
 __global__ void zs_k_selftest(uint32_t* bad, int rounds);

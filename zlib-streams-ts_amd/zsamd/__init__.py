@@ -95,8 +95,10 @@ def lib():
                                               _P, _P, _P, _P, _P, _P]
         L.zs_inflate_message.restype = ctypes.c_char_p
         L.zs_inflate_message.argtypes = [ctypes.c_int32]
-    L.zs_crc32_batch_device.argtypes = [_P, ctypes.c_uint32, _P, _U64P, _U32P, _P, _P]
-    L.zs_adler32_batch_device.argtypes = [_P, ctypes.c_uint32, _P, _U64P, _U32P, _P, _P]
+    L.zs_crc32_batch_device.argtypes = [_P, ctypes.c_uint32, _P, _U64P, _U32P, _U32P, _P, _P]
+    L.zs_adler32_batch_device.argtypes = [_P, ctypes.c_uint32, _P, _U64P, _U32P, _U32P, _P, _P]
+    L.zs_crc32_batch.argtypes = [_P, ctypes.c_uint32, ctypes.c_char_p, _U64P, _U32P, _U32P, _U32P]
+    L.zs_adler32_batch.argtypes = [_P, ctypes.c_uint32, ctypes.c_char_p, _U64P, _U32P, _U32P, _U32P]
     L.zs_last_batch_ms.restype = ctypes.c_double
     L.zs_last_batch_ms.argtypes = [_P]
     L.zs_last_inflate_lane_count.restype = ctypes.c_uint32
@@ -298,10 +300,36 @@ class Engine:
                                      in_off, in_len, _P(h_out), out_off, out_cap, status, out_len)
         self._check(r, "zs_deflate_batch")
 
-    def checksum_device(self, kind: str, n: int, d_in: int, in_off, in_len, d_check: int, hip_stream: int = 0):
+    def checksum_device(self, kind: str, n: int, d_in: int, in_off, in_len, d_check: int, hip_stream: int = 0,
+                        seeds=None):
+        """crc32 / adler32 of n device-resident streams (seeds: ctypes u32 array or None)"""
         fn = self._L.zs_crc32_batch_device if kind == "crc32" else self._L.zs_adler32_batch_device
-        r = fn(self._ctx, n, _P(d_in), in_off, in_len, _P(d_check), _P(hip_stream) if hip_stream else None)
+        r = fn(self._ctx, n, _P(d_in), in_off, in_len, seeds, _P(d_check), _P(hip_stream) if hip_stream else None)
         self._check(r, "checksum")
+
+    def checksum(self, kind: str, bufs: Sequence[bytes], seeds: Optional[Sequence[int]] = None) -> List[int]:
+        """[crc32(seed, buf)] or [adler32(seed, buf)] per buffer (common/crc32.ts:26,
+        common/adler32.ts:4 semantics; seeds None = initial values)."""
+        n = len(bufs)
+        if n == 0:
+            return []
+        offs, lens, o = [], [], 0
+        for b in bufs:
+            offs.append(o)
+            lens.append(len(b))
+            o += len(b)
+        sd = (ctypes.c_uint32 * n)(*[x & 0xffffffff for x in seeds]) if seeds is not None else None
+        out = (ctypes.c_uint32 * n)()
+        fn = self._L.zs_crc32_batch if kind == "crc32" else self._L.zs_adler32_batch
+        r = fn(self._ctx, n, b"".join(bufs), (ctypes.c_uint64 * n)(*offs), (ctypes.c_uint32 * n)(*lens), sd, out)
+        self._check(r, "checksum")
+        return list(out)
+
+    def crc32(self, bufs: Sequence[bytes], seeds: Optional[Sequence[int]] = None) -> List[int]:
+        return self.checksum("crc32", bufs, seeds)
+
+    def adler32(self, bufs: Sequence[bytes], seeds: Optional[Sequence[int]] = None) -> List[int]:
+        return self.checksum("adler32", bufs, seeds)
 
 
 _default: Optional[Engine] = None
