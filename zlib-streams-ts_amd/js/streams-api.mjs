@@ -50,12 +50,14 @@ function decompressWbits(format) {
   return w;
 }
 
-function runCompress(inputs, format, options) {
+// The addon runs each batch on a worker thread (napi_async_work) and settles a
+// Promise: the event loop is not blocked while the GPU works.
+async function runCompress(inputs, format, options) {
   const wbits = compressWbits(format);
   const level = options.level === undefined ? -1 : options.level;  // -1 -> 6, deflate.ts:268-270
   let res;
   try {
-    res = addon.compressBatch(checkInputs(inputs), wbits, level, options.device || 0);
+    res = await addon.compressBatch(checkInputs(inputs), wbits, level, options.device || 0);
   } catch (e) {
     // argument validation of deflateInit2_ (deflate.ts:281-294) surfaces as the stream layer's init error
     if (e.code === String(Z_STREAM_ERROR)) throw streamError(Z_STREAM_ERROR, PHASE_INIT);
@@ -64,11 +66,11 @@ function runCompress(inputs, format, options) {
   return res.outputs.map((out, i) => (res.status[i] === Z_STREAM_END ? out : streamError(res.status[i], PHASE_FINISH)));
 }
 
-function runDecompress(inputs, format, options) {
+async function runDecompress(inputs, format, options) {
   const wbits = decompressWbits(format);
   const ins = checkInputs(inputs);
   const cap = options.outCapacity === undefined ? ins.map((x) => Math.max(65536, 16 * x.length)) : options.outCapacity;
-  const res = addon.decompressBatch(ins, wbits, cap, options.device || 0);
+  const res = await addon.decompressBatch(ins, wbits, cap, options.device || 0);
   return res.outputs.map((out, i) => {
     if (res.status[i] === Z_STREAM_END) return out;
     const err = streamError(res.status[i], res.phase[i]);
@@ -81,7 +83,7 @@ const settle = (xs) => xs.map((x) => (x instanceof Error ? { status: "rejected",
 
 /** Compress every input as an independent stream; rejects with the first stream's error. */
 export async function compressBatch(inputs, format = "deflate", options = {}) {
-  const out = runCompress(inputs, format, options);
+  const out = await runCompress(inputs, format, options);
   const bad = out.find((x) => x instanceof Error);
   if (bad) throw bad;
   return out;
@@ -89,7 +91,7 @@ export async function compressBatch(inputs, format = "deflate", options = {}) {
 
 /** Decompress every input as an independent stream; rejects with the first stream's error. */
 export async function decompressBatch(inputs, format = "deflate", options = {}) {
-  const out = runDecompress(inputs, format, options);
+  const out = await runDecompress(inputs, format, options);
   const bad = out.find((x) => x instanceof Error);
   if (bad) throw bad;
   return out;
@@ -97,11 +99,11 @@ export async function decompressBatch(inputs, format = "deflate", options = {}) 
 
 /** Per-stream outcomes, Promise.allSettled style. */
 export async function compressBatchSettled(inputs, format = "deflate", options = {}) {
-  return settle(runCompress(inputs, format, options));
+  return settle(await runCompress(inputs, format, options));
 }
 
 export async function decompressBatchSettled(inputs, format = "deflate", options = {}) {
-  return settle(runDecompress(inputs, format, options));
+  return settle(await runDecompress(inputs, format, options));
 }
 
 export const deflateBound = (length, format = "deflate") => addon.deflateBound(length, compressWbits(format));

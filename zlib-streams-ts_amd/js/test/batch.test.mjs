@@ -37,7 +37,6 @@ async function main() {
   // deflate: every golden case at levels 1..9, batched per (level, format)
   const groups = new Map();
   for (const x of deflateCases()) {
-    if (x.c.level < 1) continue;  // level 0 (deflate_stored) is not offered by the GPU engine
     const k = x.c.level + "/" + x.c.format;
     if (!groups.has(k)) groups.set(k, []);
     groups.get(k).push(x);
@@ -68,6 +67,20 @@ async function main() {
     const back = await api.decompressBatch(await api.compressBatch(inputs, format), format);
     back.forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(inputs[i])) === 0, `round trip ${format} ${i}`));
   }
+  // level 0 (deflate_stored) against the reference-made layout goldens
+  const l0 = JSON.parse(readFileSync(join(golden, "deflate_level0.json"), "utf8")).cases.filter((c) => c.n <= 300000);
+  for (const format of ["deflate", "deflate-raw", "gzip"]) {
+    const cs = l0.filter((c) => c.format === format);
+    const outs = await api.compressBatch(cs.map((c) => corpus.text(corpus.streamSeed(c.seed_index), c.n)), format, { level: 0 });
+    cs.forEach((c, i) => expect(outs[i].length === c.out_len && sha(outs[i]) === c.out_sha256, `level 0 ${format} ${c.n}`));
+  }
+  // the batch runs on a worker thread: the event loop turns while the GPU works
+  let turned = false;
+  const big = Array.from({ length: 512 }, (_, i) => corpus.text(corpus.streamSeed(i), 65536));
+  const pending = api.compressBatch(big, "deflate-raw", { level: 6 });
+  setImmediate(() => { turned = true; });
+  await pending;
+  expect(turned, "event loop not blocked by a batch");
   // deflateInit2_ validation (deflate.ts:281-294) surfaces as the stream layer's init error
   let msg = "";
   try { await api.compressBatch([inputs[0]], "deflate", { level: 10 }); } catch (e) { msg = e.message; }

@@ -5,9 +5,13 @@
  * the duration of one call (napi_get_typedarray_info), packs them into one
  * host batch, runs zs_deflate_batch / zs_inflate_batch on the GPU and returns
  * fresh Uint8Arrays -- nothing is retained after the call (SURVEY.md 8(b)
- * "Ownership").  Synchronous; one device context per GPU, created lazily.
+ * "Ownership").  The batch calls return Promises: the GPU work runs on a libuv
+ * worker thread (napi_async_work), so the event loop keeps running; batches
+ * on one device are serialized (one context per GPU, created lazily on the JS
+ * thread).
  */
 #include <node_api.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -110,8 +114,135 @@ static int32_t arg_i32(napi_env env, napi_value v, int32_t dflt) {
   return x;
 }
 
+/* One batch in flight: inputs packed on the JS thread (the borrowed
+ * Uint8Arrays are not touched after the call returns), the GPU work on a libuv
+ * worker thread (napi_async_work), results built back on the JS thread. */
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  int inflate;  /* 0 compress, 1 decompress */
+  int dev, wbits, level;
+  uint32_t n;
+  zs_ctx *ctx;
+  uint64_t *in_off, *out_off;
+  uint32_t *in_len, *cap, *olen, *cons;
+  int32_t *status, *phase, *msg;
+  uint8_t *blob, *out;
+  int rc;
+  char err[512];
+} job;
+
+/* one batch at a time per device context (the context's workspaces are reused) */
+static pthread_mutex_t g_dev_mtx[MAX_DEV];
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+static void init_mutexes(void) {
+  for (int i = 0; i < MAX_DEV; i++) pthread_mutex_init(&g_dev_mtx[i], NULL);
+}
+
+static void job_free(job *j) {
+  if (!j) return;
+  free(j->in_off); free(j->out_off); free(j->in_len); free(j->cap); free(j->olen); free(j->cons);
+  free(j->status); free(j->phase); free(j->msg); free(j->blob); free(j->out);
+  free(j);
+}
+
+static job *job_new(uint32_t n) {
+  job *j = (job *)calloc(1, sizeof(job));
+  if (!j) return NULL;
+  j->n = n;
+  j->in_off = (uint64_t *)calloc(n + 1, 8);
+  j->out_off = (uint64_t *)calloc(n + 1, 8);
+  j->in_len = (uint32_t *)calloc(n + 1, 4);
+  j->cap = (uint32_t *)calloc(n + 1, 4);
+  j->olen = (uint32_t *)calloc(n + 1, 4);
+  j->cons = (uint32_t *)calloc(n + 1, 4);
+  j->status = (int32_t *)calloc(n + 1, 4);
+  j->phase = (int32_t *)calloc(n + 1, 4);
+  j->msg = (int32_t *)calloc(n + 1, 4);
+  if (!j->in_off || !j->out_off || !j->in_len || !j->cap || !j->olen || !j->cons || !j->status || !j->phase || !j->msg) {
+    job_free(j);
+    return NULL;
+  }
+  return j;
+}
+
+/* worker thread: no N-API calls here */
+static void job_execute(napi_env env, void *data) {
+  job *j = (job *)data;
+  (void)env;
+  pthread_mutex_lock(&g_dev_mtx[j->dev]);
+  if (j->n == 0) j->rc = ZS_OK;
+  else if (j->inflate)
+    j->rc = zs_inflate_batch(j->ctx, j->wbits, j->n, j->blob, j->in_off, j->in_len, j->out, j->out_off, j->cap,
+                             j->status, j->phase, j->msg, j->olen, j->cons);
+  else
+    j->rc = zs_deflate_batch(j->ctx, j->level, j->wbits, j->n, j->blob, j->in_off, j->in_len, j->out, j->out_off,
+                             j->cap, j->status, j->olen);
+  if (j->rc != ZS_OK) snprintf(j->err, sizeof j->err, "%s", zs_last_error());  /* the error is per thread */
+  pthread_mutex_unlock(&g_dev_mtx[j->dev]);
+}
+
+static napi_value build_result(napi_env env, job *j) {
+  napi_value outs, obj;
+  if (napi_create_array_with_length(env, j->n, &outs) != napi_ok || napi_create_object(env, &obj) != napi_ok) return NULL;
+  napi_value msgs = NULL;
+  if (j->inflate && napi_create_array_with_length(env, j->n, &msgs) != napi_ok) return NULL;
+  for (uint32_t i = 0; i < j->n; i++) {
+    napi_value u = make_u8(env, j->out + j->out_off[i], j->status[i] == ZS_STREAM_END ? j->olen[i] : 0);
+    if (!u || napi_set_element(env, outs, i, u) != napi_ok) return NULL;
+    if (j->inflate) {
+      napi_value s;
+      const char *m = zs_inflate_message(j->msg[i]);
+      if (napi_create_string_utf8(env, m ? m : "", NAPI_AUTO_LENGTH, &s) != napi_ok ||
+          napi_set_element(env, msgs, i, s) != napi_ok)
+        return NULL;
+    }
+  }
+  napi_set_named_property(env, obj, "status", make_i32(env, j->status, j->n));
+  if (j->inflate) {
+    napi_set_named_property(env, obj, "phase", make_i32(env, j->phase, j->n));
+    napi_set_named_property(env, obj, "consumed", make_i32(env, (const int32_t *)j->cons, j->n));
+    napi_set_named_property(env, obj, "message", msgs);
+  }
+  napi_set_named_property(env, obj, "outputs", outs);
+  return obj;
+}
+
+/* JS thread: settle the promise */
+static void job_complete(napi_env env, napi_status st, void *data) {
+  job *j = (job *)data;
+  napi_value v = NULL;
+  if (st == napi_ok && j->rc == ZS_OK) v = build_result(env, j);
+  if (v) {
+    napi_resolve_deferred(env, j->deferred, v);
+  } else {
+    char c[16];
+    napi_value code, msg, e;
+    const int rc = j->rc != ZS_OK ? j->rc : ZS_MEM_ERROR;
+    snprintf(c, sizeof c, "%d", rc);
+    napi_create_string_utf8(env, c, NAPI_AUTO_LENGTH, &code);
+    napi_create_string_utf8(env, j->rc != ZS_OK ? j->err : "could not build the batch result", NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, code, msg, &e);
+    napi_reject_deferred(env, j->deferred, e);
+  }
+  napi_delete_async_work(env, j->work);
+  job_free(j);
+}
+
+static napi_value queue_job(napi_env env, job *j, const char *name) {
+  napi_value promise, res_name;
+  if (napi_create_promise(env, &j->deferred, &promise) != napi_ok ||
+      napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name) != napi_ok ||
+      napi_create_async_work(env, NULL, res_name, job_execute, job_complete, j, &j->work) != napi_ok ||
+      napi_queue_async_work(env, j->work) != napi_ok) {
+    job_free(j);
+    return throw_code(env, ZS_MEM_ERROR, "could not queue the batch");
+  }
+  return promise;
+}
+
 /* compressBatch(inputs: Uint8Array[], wbits, level, device) ->
- *   {status: Int32Array, outputs: Uint8Array[]} */
+ *   Promise<{status: Int32Array, outputs: Uint8Array[]}> */
 static napi_value CompressBatch(napi_env env, napi_callback_info info) {
   size_t argc = 4;
   napi_value argv[4];
@@ -120,51 +251,41 @@ static napi_value CompressBatch(napi_env env, napi_callback_info info) {
   view *v = NULL;
   uint32_t n = 0;
   if (get_views(env, argv[0], &v, &n) != 0) return throw_code(env, ZS_STREAM_ERROR, "inputs must be Uint8Array[]");
-  const int wbits = arg_i32(env, argv[1], -15), level = arg_i32(env, argv[2], -1);
   const int dev = argc > 3 ? arg_i32(env, argv[3], 0) : 0;
   zs_ctx *ctx = ctx_for(env, dev);
-  if (!ctx) { free(v); return NULL; }
-  uint64_t *in_off = (uint64_t *)calloc(n + 1, 8), *out_off = (uint64_t *)calloc(n + 1, 8);
-  uint32_t *in_len = (uint32_t *)calloc(n + 1, 4), *cap = (uint32_t *)calloc(n + 1, 4), *olen = (uint32_t *)calloc(n + 1, 4);
-  int32_t *status = (int32_t *)calloc(n + 1, 4);
+  job *j = ctx ? job_new(n) : NULL;
+  if (!j) {
+    free(v);
+    return ctx ? throw_code(env, ZS_MEM_ERROR, "out of host memory") : NULL;
+  }
+  j->ctx = ctx;
+  j->dev = dev;
+  j->wbits = arg_i32(env, argv[1], -15);
+  j->level = arg_i32(env, argv[2], -1);
   uint64_t tin = 0, tout = 0;
   for (uint32_t i = 0; i < n; i++) {
-    in_off[i] = tin;
-    in_len[i] = (uint32_t)v[i].n;
+    j->in_off[i] = tin;
+    j->in_len[i] = (uint32_t)v[i].n;
     tin += v[i].n;
-    out_off[i] = tout;
-    cap[i] = (uint32_t)((zs_deflate_bound(v[i].n, wbits) + 3) & ~3ull);
-    tout += cap[i];
+    j->out_off[i] = tout;
+    j->cap[i] = (uint32_t)((zs_deflate_bound(v[i].n, j->wbits) + 3) & ~3ull);
+    tout += j->cap[i];
   }
-  uint8_t *blob = (uint8_t *)malloc(tin ? tin : 1), *out = (uint8_t *)malloc(tout ? tout : 1);
-  napi_value res = NULL;
-  if (!in_off || !out_off || !in_len || !cap || !olen || !status || !blob || !out) {
-    throw_code(env, ZS_MEM_ERROR, "out of host memory");
-    goto done;
+  j->blob = (uint8_t *)malloc(tin ? tin : 1);
+  j->out = (uint8_t *)malloc(tout ? tout : 1);
+  if (!j->blob || !j->out) {
+    free(v);
+    job_free(j);
+    return throw_code(env, ZS_MEM_ERROR, "out of host memory");
   }
   for (uint32_t i = 0; i < n; i++)
-    if (v[i].n) memcpy(blob + in_off[i], v[i].p, v[i].n);
-  int r = n ? zs_deflate_batch(ctx, level, wbits, n, blob, in_off, in_len, out, out_off, cap, status, olen) : ZS_OK;
-  if (r != ZS_OK) {
-    throw_code(env, r, zs_last_error());
-    goto done;
-  }
-  napi_value outs, obj;
-  if (napi_create_array_with_length(env, n, &outs) != napi_ok || napi_create_object(env, &obj) != napi_ok) goto done;
-  for (uint32_t i = 0; i < n; i++) {
-    napi_value u = make_u8(env, out + out_off[i], status[i] == ZS_STREAM_END ? olen[i] : 0);
-    if (!u || napi_set_element(env, outs, i, u) != napi_ok) goto done;
-  }
-  napi_set_named_property(env, obj, "status", make_i32(env, status, n));
-  napi_set_named_property(env, obj, "outputs", outs);
-  res = obj;
-done:
-  free(v); free(in_off); free(out_off); free(in_len); free(cap); free(olen); free(status); free(blob); free(out);
-  return res;
+    if (v[i].n) memcpy(j->blob + j->in_off[i], v[i].p, v[i].n);
+  free(v);
+  return queue_job(env, j, "zs.compressBatch");
 }
 
 /* decompressBatch(inputs: Uint8Array[], wbits, outCapacity: number | number[], device) ->
- *   {status, phase: Int32Array, message: string[], outputs: Uint8Array[], consumed: Int32Array} */
+ *   Promise<{status, phase: Int32Array, message: string[], outputs: Uint8Array[], consumed: Int32Array}> */
 static napi_value DecompressBatch(napi_env env, napi_callback_info info) {
   size_t argc = 4;
   napi_value argv[4];
@@ -173,24 +294,21 @@ static napi_value DecompressBatch(napi_env env, napi_callback_info info) {
   view *v = NULL;
   uint32_t n = 0;
   if (get_views(env, argv[0], &v, &n) != 0) return throw_code(env, ZS_STREAM_ERROR, "inputs must be Uint8Array[]");
-  const int wbits = arg_i32(env, argv[1], -15);
   const int dev = argc > 3 ? arg_i32(env, argv[3], 0) : 0;
   zs_ctx *ctx = ctx_for(env, dev);
-  if (!ctx) { free(v); return NULL; }
+  job *j = ctx ? job_new(n) : NULL;
+  if (!j) {
+    free(v);
+    return ctx ? throw_code(env, ZS_MEM_ERROR, "out of host memory") : NULL;
+  }
+  j->inflate = 1;
+  j->ctx = ctx;
+  j->dev = dev;
+  j->wbits = arg_i32(env, argv[1], -15);
   bool caps_arr = false;
   napi_is_array(env, argv[2], &caps_arr);
   const int32_t cap_all = caps_arr ? 0 : arg_i32(env, argv[2], 1 << 16);
-  uint64_t *in_off = (uint64_t *)calloc(n + 1, 8), *out_off = (uint64_t *)calloc(n + 1, 8);
-  uint32_t *in_len = (uint32_t *)calloc(n + 1, 4), *cap = (uint32_t *)calloc(n + 1, 4);
-  uint32_t *olen = (uint32_t *)calloc(n + 1, 4), *cons = (uint32_t *)calloc(n + 1, 4);
-  int32_t *status = (int32_t *)calloc(n + 1, 4), *phase = (int32_t *)calloc(n + 1, 4), *msg = (int32_t *)calloc(n + 1, 4);
   uint64_t tin = 0, tout = 0;
-  uint8_t *blob = NULL, *out = NULL;
-  napi_value res = NULL;
-  if (!in_off || !out_off || !in_len || !cap || !olen || !cons || !status || !phase || !msg) {
-    throw_code(env, ZS_MEM_ERROR, "out of host memory");
-    goto done;
-  }
   for (uint32_t i = 0; i < n; i++) {
     int32_t c = cap_all;
     if (caps_arr) {
@@ -199,48 +317,24 @@ static napi_value DecompressBatch(napi_env env, napi_callback_info info) {
       c = arg_i32(env, e, 1 << 16);
     }
     if (c < 0) c = 0;
-    in_off[i] = tin;
-    in_len[i] = (uint32_t)v[i].n;
+    j->in_off[i] = tin;
+    j->in_len[i] = (uint32_t)v[i].n;
     tin += v[i].n;
-    out_off[i] = tout;
-    cap[i] = ((uint32_t)c + 3u) & ~3u;
-    tout += cap[i];
+    j->out_off[i] = tout;
+    j->cap[i] = ((uint32_t)c + 3u) & ~3u;
+    tout += j->cap[i];
   }
-  blob = (uint8_t *)malloc(tin ? tin : 1);
-  out = (uint8_t *)malloc(tout ? tout : 1);
-  if (!blob || !out) {
-    throw_code(env, ZS_MEM_ERROR, "out of host memory");
-    goto done;
+  j->blob = (uint8_t *)malloc(tin ? tin : 1);
+  j->out = (uint8_t *)malloc(tout ? tout : 1);
+  if (!j->blob || !j->out) {
+    free(v);
+    job_free(j);
+    return throw_code(env, ZS_MEM_ERROR, "out of host memory");
   }
   for (uint32_t i = 0; i < n; i++)
-    if (v[i].n) memcpy(blob + in_off[i], v[i].p, v[i].n);
-  int r = n ? zs_inflate_batch(ctx, wbits, n, blob, in_off, in_len, out, out_off, cap, status, phase, msg, olen, cons)
-            : ZS_OK;
-  if (r != ZS_OK) {
-    throw_code(env, r, zs_last_error());
-    goto done;
-  }
-  napi_value outs, msgs, obj;
-  if (napi_create_array_with_length(env, n, &outs) != napi_ok || napi_create_array_with_length(env, n, &msgs) != napi_ok ||
-      napi_create_object(env, &obj) != napi_ok)
-    goto done;
-  for (uint32_t i = 0; i < n; i++) {
-    napi_value u = make_u8(env, out + out_off[i], status[i] == ZS_STREAM_END ? olen[i] : 0), s;
-    const char *m = zs_inflate_message(msg[i]);
-    if (!u || napi_set_element(env, outs, i, u) != napi_ok) goto done;
-    if (napi_create_string_utf8(env, m ? m : "", NAPI_AUTO_LENGTH, &s) != napi_ok || napi_set_element(env, msgs, i, s) != napi_ok)
-      goto done;
-  }
-  napi_set_named_property(env, obj, "status", make_i32(env, status, n));
-  napi_set_named_property(env, obj, "phase", make_i32(env, phase, n));
-  napi_set_named_property(env, obj, "consumed", make_i32(env, (const int32_t *)cons, n));
-  napi_set_named_property(env, obj, "message", msgs);
-  napi_set_named_property(env, obj, "outputs", outs);
-  res = obj;
-done:
-  free(v); free(in_off); free(out_off); free(in_len); free(cap); free(olen); free(cons); free(status); free(phase);
-  free(msg); free(blob); free(out);
-  return res;
+    if (v[i].n) memcpy(j->blob + j->in_off[i], v[i].p, v[i].n);
+  free(v);
+  return queue_job(env, j, "zs.decompressBatch");
 }
 
 static napi_value DeflateBound(napi_env env, napi_callback_info info) {
@@ -274,6 +368,7 @@ static napi_value SelfTest(napi_env env, napi_callback_info info) {
 }
 
 static napi_value Init(napi_env env, napi_value exports) {
+  pthread_once(&g_once, init_mutexes);
   napi_property_descriptor d[] = {
       {"compressBatch", NULL, CompressBatch, NULL, NULL, NULL, napi_default, NULL},
       {"decompressBatch", NULL, DecompressBatch, NULL, NULL, NULL, napi_default, NULL},
