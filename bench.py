@@ -249,7 +249,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        for ph in ("checksum", "prev", "match", "parse", "trees", "layout", "emit", "finish"):
+        for ph in ("checksum", "bucket", "prev", "sweep", "match", "stored", "fast", "parse", "trees", "layout", "emit",
+                   "finish"):
             v = eng.last_ms(ph)
             if v >= 0:
                 phases[ph] = phases.get(ph, 0.0) + v

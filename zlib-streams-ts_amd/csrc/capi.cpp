@@ -400,13 +400,13 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
       // longer ones: chain links + per-tile chain walk (deflate_match.hip)
       zs_k_bucket<<<n, 256, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
       if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
-      MARK("prev");
+      MARK("bucket");
       zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
                                      cfg.chain, cfg.nice);
       if (max_len > 65537u)
         zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
                                        cfg.chain, cfg.nice, 65537u);
-      MARK("match");
+      MARK("sweep");
     } else {
       // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
       zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
@@ -433,7 +433,7 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
     HIPCHK(hipFuncSetAttribute((const void*)zs_k_fast, hipFuncAttributeMaxDynamicSharedMemorySize, fast_smem));
     zs_k_fast<<<n, 64, fast_smem, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
                                         cfg.chain, cfg.lazy, cfg.nice);
-    MARK("parse");
+    MARK("fast");
   }
   zs_k_trees<<<dim3(max_blk, n), 64, 0, st>>>(d_in, d_in_off, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
                                               c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), (int)n);

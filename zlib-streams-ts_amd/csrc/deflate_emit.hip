@@ -27,7 +27,7 @@ struct zs_tw {  // LDS workspace of one wave, common/types.ts DeflateState tree 
   uint16_t dfreq[2 * ZS_D_CODES + 1], dlen[2 * ZS_D_CODES + 1], ddad[2 * ZS_D_CODES + 1], dcode[2 * ZS_D_CODES + 1];
   uint16_t bfreq[2 * ZS_BL_CODES + 1], blen[2 * ZS_BL_CODES + 1], bdad[2 * ZS_BL_CODES + 1], bcode[2 * ZS_BL_CODES + 1];
   int16_t heap[2 * ZS_L_CODES + 1];
-  uint8_t depth[2 * ZS_L_CODES + 1];
+  uint32_t hk[2 * ZS_L_CODES + 2];  // working heap: freq << 17 | depth << 10 | node
   uint16_t bl_count[16];
   uint32_t hist[ZS_L_CODES + ZS_D_CODES];
   uint32_t hdr[ZS_HDR_WORDS];
@@ -48,22 +48,30 @@ struct zs_tstate {
   uint32_t hbits;
 };
 
-static __device__ __forceinline__ bool zs_smaller(const uint16_t* f, const uint8_t* depth, int n, int m) {
-  return f[n] < f[m] || (f[n] == f[m] && depth[n] <= depth[m]);  // trees.ts:163-165
-}
+// The heap orders nodes by freq, then depth (smaller(n, m): freq[n] < freq[m] ||
+// (freq[n] == freq[m] && depth[n] <= depth[m]), trees.ts:163-165).  Each heap
+// entry carries its own key -- freq << 17 | depth << 10 | node, so the order is
+// the order of (entry >> 10) -- and a sift step costs one LDS read of the two
+// children instead of a dependent chain through the freq and depth arrays.
+// Widths: a block's total frequency is at most 16,384 (ZS_SYM_END symbols +
+// end-of-block), below 2^15; depths stay far below 2^7; nodes below 2^10.
+static __device__ __forceinline__ uint32_t zs_hkey(uint32_t e) { return e >> 10; }
 
-static __device__ void zs_pqdownheap(zs_tstate& t, const uint16_t* f, int k) {  // trees.ts:167-185
-  int16_t* heap = t.w->heap;
-  const int v = heap[k];
+static __device__ void zs_pqdownheap(zs_tstate& t, int k) {  // trees.ts:167-185
+  uint32_t* hk = t.w->hk;
+  const uint32_t v = hk[k];
   int j = k << 1;
   while (j <= t.heap_len) {
-    if (j < t.heap_len && zs_smaller(f, t.w->depth, heap[j + 1], heap[j])) j++;
-    if (zs_smaller(f, t.w->depth, v, heap[j])) break;
-    heap[k] = heap[j];
+    const uint32_t a = hk[j], b = hk[j + 1];  // hk[heap_len + 1] is never selected (j < heap_len test)
+    const bool right = j < t.heap_len && zs_hkey(b) <= zs_hkey(a);
+    const uint32_t c = right ? b : a;
+    j += right ? 1 : 0;
+    if (zs_hkey(v) <= zs_hkey(c)) break;
+    hk[k] = c;
     k = j;
     j <<= 1;
   }
-  heap[k] = (int16_t)v;
+  hk[k] = v;
 }
 
 static __device__ void zs_gen_bitlen(zs_tstate& t, zs_tdesc& d) {  // trees.ts:187-259
@@ -121,38 +129,41 @@ static __device__ void zs_gen_codes(zs_tstate& t, zs_tdesc& d) {  // trees.ts:54
 
 static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:261-316
   int16_t* heap = t.w->heap;
-  uint8_t* depth = t.w->depth;
-  int n, m, max_code = -1, node;
+  uint32_t* hk = t.w->hk;
+  int n, max_code = -1, node;
   t.heap_len = 0;
   t.heap_max = ZS_HEAP_SIZE;
   for (n = 0; n < d.elems; n++) {
-    if (d.freq[n] != 0) { heap[++t.heap_len] = (int16_t)(max_code = n); depth[n] = 0; }
+    if (d.freq[n] != 0) hk[++t.heap_len] = ((uint32_t)d.freq[n] << 17) | (uint32_t)(max_code = n);
     else d.len[n] = 0;
   }
   while (t.heap_len < 2) {
-    node = heap[++t.heap_len] = (int16_t)(max_code < 2 ? ++max_code : 0);
+    node = max_code < 2 ? ++max_code : 0;
+    hk[++t.heap_len] = (1u << 17) | (uint32_t)node;
     d.freq[node] = 1;
-    depth[node] = 0;
     t.opt_len--;
     if (d.stat) t.static_len -= d.stat[node] >> 16;
   }
   d.max_code = max_code;
-  for (n = t.heap_len / 2; n >= 1; n--) zs_pqdownheap(t, d.freq, n);
+  for (n = t.heap_len / 2; n >= 1; n--) zs_pqdownheap(t, n);
   node = d.elems;
   do {
-    n = heap[1];
-    heap[1] = heap[t.heap_len--];
-    zs_pqdownheap(t, d.freq, 1);
-    m = heap[1];
-    heap[--t.heap_max] = (int16_t)n;
-    heap[--t.heap_max] = (int16_t)m;
-    d.freq[node] = (uint16_t)(d.freq[n] + d.freq[m]);
-    depth[node] = (uint8_t)((depth[n] >= depth[m] ? depth[n] : depth[m]) + 1);
-    d.dad[n] = d.dad[m] = (uint16_t)node;
-    heap[1] = (int16_t)node++;
-    zs_pqdownheap(t, d.freq, 1);
+    const uint32_t en = hk[1];
+    hk[1] = hk[t.heap_len--];
+    zs_pqdownheap(t, 1);
+    const uint32_t em = hk[1];
+    const uint32_t nn = en & 1023u, mm = em & 1023u;
+    heap[--t.heap_max] = (int16_t)nn;
+    heap[--t.heap_max] = (int16_t)mm;
+    const uint32_t f = (en >> 17) + (em >> 17);
+    const uint32_t dn = (en >> 10) & 127u, dm = (em >> 10) & 127u;
+    d.freq[node] = (uint16_t)f;
+    d.dad[nn] = d.dad[mm] = (uint16_t)node;
+    hk[1] = (f << 17) | (((dn >= dm ? dn : dm) + 1) << 10) | (uint32_t)node;
+    node++;
+    zs_pqdownheap(t, 1);
   } while (t.heap_len >= 2);
-  heap[--t.heap_max] = heap[1];
+  heap[--t.heap_max] = (int16_t)(hk[1] & 1023u);
   zs_gen_bitlen(t, d);
   zs_gen_codes(t, d);
 }
@@ -227,15 +238,26 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   for (uint32_t i = lane; i < ZS_L_CODES + ZS_D_CODES; i += 64) w.hist[i] = 0;
   for (uint32_t i = lane; i < ZS_HDR_WORDS; i += 64) w.hdr[i] = 0;
   __syncthreads();
-  // histogram (deflate/utils.ts:55-81 tallies, done in parallel)
-  for (uint32_t i = lane; i < blk.sym_count; i += 64) {
-    const uint32_t v = sy[i];
-    if (v & 0x80000000u) {
-      const uint32_t lc = (v >> 16) & 0xff, dist = (v & 0xffffu) - 1;
-      atomicAdd(&w.hist[ZS_LENGTH_CODE[lc] + 257], 1u);
-      atomicAdd(&w.hist[ZS_L_CODES + (dist < 256 ? ZS_DIST_CODE[dist] : ZS_DIST_CODE[256 + (dist >> 7)])], 1u);
-    } else {
-      atomicAdd(&w.hist[v], 1u);
+  // histogram (deflate/utils.ts:55-81 tallies, done in parallel); eight symbol
+  // loads in flight per lane before their atomics, so the wave waits for
+  // memory once per 512 symbols rather than once per 64
+  for (uint32_t i0 = 0; i0 < blk.sym_count; i0 += 512) {
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint32_t i = i0 + 64 * k + lane;
+      v[k] = i < blk.sym_count ? sy[i] : 0xffffffffu;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      if (v[k] == 0xffffffffu) continue;
+      if (v[k] & 0x80000000u) {
+        const uint32_t lc = (v[k] >> 16) & 0xff, dist = (v[k] & 0xffffu) - 1;
+        atomicAdd(&w.hist[ZS_LENGTH_CODE[lc] + 257], 1u);
+        atomicAdd(&w.hist[ZS_L_CODES + (dist < 256 ? ZS_DIST_CODE[dist] : ZS_DIST_CODE[256 + (dist >> 7)])], 1u);
+      } else {
+        atomicAdd(&w.hist[v[k]], 1u);
+      }
     }
   }
   __syncthreads();
