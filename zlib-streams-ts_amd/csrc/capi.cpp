@@ -429,7 +429,7 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
     }
     MARK("parse");
   } else {
-    const int fast_smem = 2 * 32768 * 2;  // head[] + prev[] (u16 x 32 K each)
+    const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
     HIPCHK(hipFuncSetAttribute((const void*)zs_k_fast, hipFuncAttributeMaxDynamicSharedMemorySize, fast_smem));
     zs_k_fast<<<n, 64, fast_smem, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
                                         cfg.chain, cfg.lazy, cfg.nice);

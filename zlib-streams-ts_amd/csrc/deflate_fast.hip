@@ -9,8 +9,12 @@
 // (u16, 32 K entries each, slid by 32 K on the same schedule as fill_window,
 // deflate.ts:180-190) resident in LDS.  All 64 lanes run the state machine in
 // lock-step and cooperate on the byte work: a candidate is compared 64 bytes
-// per step (one coalesced load + ballot), the input bytes the hash needs are
-// prefetched 256 at a time into registers and read back with readlane.
+// per step (ballot).  The bytes come from LDS and registers, not from memory:
+// a 32 KiB ring in LDS holds the input before the current 256-byte chunk
+// (everything a candidate at distance <= MAX_DIST can start at), and two
+// registers per lane hold the current and next chunk (the scan bytes, the hash
+// bytes, the literals), the next-but-one chunk's load in flight as the parse
+// enters a chunk.  head + prev + ring fill the CU's 160 KiB of LDS.
 #include <hip/hip_runtime.h>
 #include "zs_common.h"
 #include "zs_kernels.h"
@@ -18,12 +22,7 @@
 struct zs_fast_lds {
   uint16_t head[32768];
   uint16_t prev[32768];
-};
-
-// Prefetched input window: lane l holds bytes [pf0 + 4l, pf0 + 4l + 4).
-struct zs_pf {
-  uint32_t pf0;
-  uint32_t w;
+  uint32_t ring[8192];  // input byte x (x < 256 c) at byte (x & 32767)
 };
 
 static __device__ __forceinline__ uint32_t zs_load_word(const uint8_t* src, uint32_t n, uint32_t at) {
@@ -32,13 +31,6 @@ static __device__ __forceinline__ uint32_t zs_load_word(const uint8_t* src, uint
   for (uint32_t k = 0; k < 4; k++)
     if (at + k < n) v |= (uint32_t)src[at + k] << (8 * k);
   return v;
-}
-
-// byte q of the input through the register window (q in [pf0, pf0 + 252))
-static __device__ __forceinline__ uint32_t zs_pf_byte(const zs_pf& pf, uint32_t q) {
-  const uint32_t o = q - pf.pf0;
-  const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)pf.w, (int)(o >> 2));
-  return (word >> (8 * (o & 3))) & 0xffu;
 }
 
 __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
@@ -58,18 +50,44 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
   for (uint32_t i = lane; i < 32768; i += 64) { L.head[i] = 0; L.prev[i] = 0; }  // CLEAR_HASH (deflate.ts:120-123)
   __syncthreads();
 
-  zs_pf pf;
-  pf.pf0 = 0;
-  pf.w = zs_load_word(src, n, 4 * lane);
-  auto refill = [&](uint32_t q) {  // make [q, q + 8) readable
-    if (q - pf.pf0 + 8 > 252) {
-      pf.pf0 = q;
-      pf.w = zs_load_word(src, n, q + 4 * lane);
+  // chunk window: r0 = input bytes [256 c + 4 lane, +4), r1 = the next chunk's
+  uint32_t c = 0;
+  uint32_t r0 = zs_load_word(src, n, 4 * lane), r1 = zs_load_word(src, n, 256 + 4 * lane);
+  uint8_t* const ringb = reinterpret_cast<uint8_t*>(L.ring);
+  auto advance_to = [&](uint32_t q) {  // make the window's first chunk the one holding q
+    while (q >= 256u * (c + 1)) {
+      L.ring[((256u * c) & 32767u) / 4 + lane] = r0;  // chunk c leaves the registers for the ring
+      r0 = r1;
+      r1 = zs_load_word(src, n, 256u * (c + 2) + 4 * lane);
+      c++;
     }
   };
-  auto hash_at = [&](uint32_t q) -> uint32_t {  // SURVEY A1; caller guarantees q + 2 < n
-    refill(q);
-    return ((zs_pf_byte(pf, q) << 10) ^ (zs_pf_byte(pf, q + 1) << 5) ^ zs_pf_byte(pf, q + 2)) & ZS_HASH_MASK;
+  // byte q (wave-uniform, q in [256 c, 256 c + 512)) of the window
+  auto win_byte = [&](uint32_t q) -> uint32_t {
+    const uint32_t o = q - 256u * c;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)(o < 256u ? r0 : r1), (int)((o >> 2) & 63u));
+    return (w >> (8 * (o & 3))) & 0xffu;
+  };
+  // byte y of the input for this lane (y in [256 c - 32768, 256 c + 512)): the
+  // ring below the window, the window's registers (cross-lane) above.  Every
+  // lane must execute it (ds_bpermute reads the registers of other lanes).
+  auto lane_byte = [&](uint32_t y) -> uint32_t {
+    const uint32_t o = y - 256u * c;  // wraps for y below the window
+    const int from = (int)(((o >> 2) & 63u) * 4u);
+    const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)r0);
+    const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)r1);
+    const uint32_t rb = ringb[y & 32767u];
+    const uint32_t wb = ((o & 256u) ? w1 : w0) >> (8 * (o & 3));
+    return y < 256u * c ? rb : wb & 0xffu;
+  };
+  // SURVEY A1 (caller guarantees q + 2 < n, q < 256 c + 510); rolled one byte
+  // at a time over consecutive positions as UPDATE_HASH does (deflate.ts:109-111)
+  uint32_t hq = 0xfffffff0u, hv = 0;  // hq + 1 never equals a position
+  auto hash_at = [&](uint32_t q) -> uint32_t {
+    hv = q == hq + 1 ? ((hv << 5) ^ win_byte(q + 2)) & ZS_HASH_MASK
+                     : ((win_byte(q) << 10) ^ (win_byte(q + 1) << 5) ^ win_byte(q + 2)) & ZS_HASH_MASK;
+    hq = q;
+    return hv;
   };
 
   uint32_t base = 0;  // absolute position of window index 0
@@ -80,10 +98,8 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
     const uint32_t h = hash_at(q);
     const uint32_t rel = q - base;
     const uint32_t hh = L.head[h];
-    __builtin_amdgcn_s_waitcnt(0xc07f);
+    // lane 0 writes; the wave's later LDS reads are ordered behind these writes
     if (lane == 0) { L.prev[rel & 0x7fffu] = (uint16_t)hh; L.head[h] = (uint16_t)rel; }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
     return hh;
   };
   // Symbols are held one per lane (lane nsym % 64) and stored 64 at a time: a
@@ -117,6 +133,7 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
   };
 
   while (p < n) {
+    advance_to(p);
     // fill_window slide (deflate.ts:180-190): same schedule as deflate_slow
     if (p - base >= ZS_SLIDE_AT && min(n, base + 65536u) - p < ZS_MIN_LOOKAHEAD) {
       for (uint32_t i = lane; i < 32768; i += 64) {
@@ -139,12 +156,15 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
       const uint32_t nice = look < (uint32_t)nice_cfg ? look : (uint32_t)nice_cfg;
       const uint32_t limit = srel > ZS_MAX_DIST ? srel - ZS_MAX_DIST : 0;
       uint32_t best = ZS_MIN_MATCH - 1, cur = hash_head;
-      const uint32_t sb = p + lane < n ? src[p + lane] : 0x100u;  // scan bytes 0..63
+      // lane_byte reads other lanes' registers: every lane runs it, then masks
+      const uint32_t sbv = lane_byte(p + lane);
+      const uint32_t sb = p + lane < n ? sbv : 0x100u;  // scan bytes 0..63
       do {
         const uint32_t mpos = base + cur;
         uint32_t k = 0;
-        // compare 64 bytes per step
-        uint32_t mb = mpos + lane < n ? src[mpos + lane] : 0x1ffu;
+        // compare 64 bytes per step (the first 64 from LDS / registers, any further ones from memory)
+        const uint32_t mbv = lane_byte(mpos + lane);
+        uint32_t mb = mpos + lane < n ? mbv : 0x1ffu;
         uint64_t neq = __ballot(mb != sb || lane >= maxc);
         while (neq == 0 && k + 64 < maxc) {
           k += 64;
@@ -172,7 +192,7 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
       p = after;
       ml = 0;
     } else {
-      emit(p < n ? (refill(p), zs_pf_byte(pf, p)) : 0u);
+      emit(win_byte(p));
       p++;
     }
     if (in_blk == ZS_SYM_END) close_block(p, 0);
