@@ -148,6 +148,35 @@ def profiled_traffic(kernel, kernel_ms):
     return None, "no committed profile for %s" % kernel
 
 
+def profiled_ceilings(kernel, kernel_ms):
+    """The SQ-counter ratios that bound `kernel` below the HBM roofline, from the
+    newest committed tools/pmc_sq.sh summary (profiles/*/sq_summary*.json,
+    written by tools/sq_summary.py --json): LDS bank-conflict cycles over LDS
+    cycles, VALU busy over SIMD-cycles, and the active / parked / issue-stalled
+    split of wave cycles.  Used only when that profile's kernel duration agrees
+    with this run's within 15 % (counter passes run a little slower)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_summary*.json")) +
+                   glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            e = json.load(open(f)).get(kernel)
+        except (OSError, ValueError):
+            continue
+        if not e:
+            continue
+        src = os.path.relpath(f, ROOT)
+        prof_ms = e["avg_ns"] / 1e6
+        if abs(prof_ms - kernel_ms) > 0.15 * kernel_ms:
+            return {"source": "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)}
+        out = {k: e[k] for k in ("lds_bank_conflict_frac", "valu_busy", "active_frac_of_wave_cycles",
+                                 "wait_frac_of_wave_cycles", "wait_inst_frac_of_wave_cycles") if k in e}
+        out["source"] = "%s (%s avg %.3f ms under --pmc)" % (src, kernel, prof_ms)
+        return out
+    return {"source": "no committed SQ summary for %s" % kernel}
+
+
 def timed_port(fn, items, seconds, threads):
     """Runs fn(item) over items until `seconds` of wall time pass; returns
     (items done, wall seconds).  The oracle is a ctypes C library, so threads
@@ -341,7 +370,8 @@ def main():
             roof = {"bound": "hbm", "kernel": "zs_k_" + dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "traffic_source": tsrc, "algorithmic_bytes": alg, "kernel_ms": phase_avg[dom],
-                    "phase_ms": phase_avg, "pipeline_ms": round(sum(phase_avg.values()), 4)}
+                    "phase_ms": phase_avg, "pipeline_ms": round(sum(phase_avg.values()), 4),
+                    "ceilings": profiled_ceilings("zs_k_" + dom, phase_avg[dom])}
         cpu = None
         if not (args.no_cpu_baseline or D.world > 1):
             import oracle
@@ -515,7 +545,8 @@ def main_inflate(args):
             "roofline": {"bound": "hbm", "kernel": "zs_k_" + dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg,
-                         "kernel_ms": round(k_ms, 4), "phase_ms": phase_avg},
+                         "kernel_ms": round(k_ms, 4), "phase_ms": phase_avg,
+                         "ceilings": profiled_ceilings("zs_k_" + dom, k_ms)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -43,7 +43,16 @@ int main(int argc, char** argv) {
     blockIdx = {0, 0, 0};
     blockDim = {1, 1, 1};
     std::vector<zs_lane_tabs> tabs(1);
-    zs_k_inflate_lane(in, &ioff, &len, (uint8_t*)ob.data(), &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags);
+    uint8_t* ob8 = (uint8_t*)ob.data();
+    const size_t obn = ob.size() * sizeof(uint4);
+    for (size_t k = 0; k < obn; k++) ob8[k] = 0xa5;  // guard pattern around the member's output
+    zs_k_inflate_lane(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags);
+    for (size_t k = 0; k < obn; k++)
+      if ((k < ooff || k >= ooff + cap) && ob8[k] != 0xa5) {
+        fprintf(stderr, "lane_host: member %u wrote byte %zu outside [%lu, %lu)\n", i, k, (unsigned long)ooff,
+                (unsigned long)(ooff + cap));
+        exit(3);
+      }
     fwrite(&r, 4, 4, stdout);
     fwrite((uint8_t*)ob.data() + ooff, 1, r.bail ? 0 : r.out_len, stdout);
   }

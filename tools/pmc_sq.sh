@@ -12,4 +12,5 @@ for group in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_C
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $group --output-format csv -d "$OUT/sq$i" -o run -- python3 bench.py --no-cpu-baseline --no-shard-sweep --no-e2e --no-verify --steps 2 --warmup 1 "$@" > "$OUT/sq$i.log" 2>&1 || exit $?
 done
+python3 tools/sq_summary.py "$OUT" zs_k_ --json "$OUT/sq_summary.json" > "$OUT/sq_summary.txt"
 echo pmc-done

@@ -89,6 +89,7 @@ struct zs_ctx {
   bool inflate_ref_wrap = true;  // reproduce the reference's inflate_fast window-wrap copy (inffast.ts:133-147)
   bool match_sweep = true;
   bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)
+  int parse_win = 32;        // L4..9 parse: match-table entries staged per lane in LDS (32, 16; 0: direct loads)
   int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res, d_pack;
@@ -220,7 +221,10 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "parse_split")) c->parse_split = value != 0;
-  else if (!strcmp(name, "lane_block")) {
+  else if (!strcmp(name, "parse_win")) {
+    if (value != 0 && value != 16 && value != 32) return fail(ZS_STREAM_ERROR, "parse_win must be 0, 16 or 32");
+    c->parse_win = value;
+  } else if (!strcmp(name, "lane_block")) {
     if (value != 0 && (value < 1 || value > 64 || (value & (value - 1))))
       return fail(ZS_STREAM_ERROR, "lane_block must be 0 or a power of two <= 64");
     c->lane_block = value;
@@ -424,8 +428,9 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
       zs_k_parse_b<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, d_rng, c->mres.as<uint2>(),
                                      c->syms.as<uint32_t>(), d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
     } else {
-      zs_k_parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(),
-                                   c->syms.as<uint32_t>(), d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
+      auto parse = c->parse_win == 32 ? zs_k_parse : c->parse_win == 16 ? zs_k_parse16 : zs_k_parse_direct;
+      parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(),
+                              c->syms.as<uint32_t>(), d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
     }
     MARK("parse");
   } else {

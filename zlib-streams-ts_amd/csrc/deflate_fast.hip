@@ -25,14 +25,6 @@ struct zs_fast_lds {
   uint32_t ring[8192];  // input byte x (x < 256 c) at byte (x & 32767)
 };
 
-static __device__ __forceinline__ uint32_t zs_load_word(const uint8_t* src, uint32_t n, uint32_t at) {
-  uint32_t v = 0;
-  if (at + 4 <= n && ((uintptr_t)(src + at) & 3u) == 0) return *(const uint32_t*)(src + at);
-  for (uint32_t k = 0; k < 4; k++)
-    if (at + k < n) v |= (uint32_t)src[at + k] << (8 * k);
-  return v;
-}
-
 __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                 const uint32_t* __restrict__ in_len,
                                                 const uint64_t* __restrict__ pos_base,

@@ -14,13 +14,18 @@
 //           segment's first position ("speculative"), recording its symbols
 //           and the (position, match_available) pairs it passes with
 //           prev_length = 2 inside the segment (sync points);
-//   pass B  lane 0 replays the TRUE parse across each segment boundary only
-//           until it reaches a sync point of the next segment -- from there the
-//           speculative symbols are exact (2-3 steps per segment on text);
-//   pass C  the wave splices catch-up + speculative symbols into the stream's
-//           symbol array and closes a block after every 16383rd tallied symbol
-//           (deflate.ts:336; FLUSH_BLOCK sets block_start = strstart,
-//           deflate.ts:1120-1124) from a prefix sum of symbol lengths.
+//   pass B  the TRUE parse across each segment boundary, only until it
+//           reaches a sync point of the next segment -- from there the
+//           speculative symbols are exact (2-3 steps per segment on text).
+//           All boundaries at once: lane k enters segment k with the
+//           speculative end state of segment k - 1, which is the true state
+//           whenever segment k - 1 synced; an in-order check redoes the rare
+//           boundary whose predecessor did not;
+//   pass C  a gather concatenates each segment's catch-up + speculative
+//           symbols into the stream's symbol array; a block closes after every
+//           16383rd tallied symbol (deflate.ts:336; FLUSH_BLOCK sets
+//           block_start = strstart, deflate.ts:1120-1124), its input end the
+//           cut symbol's segment start plus the lengths before it.
 //
 // fill_window's slide schedule (deflate.ts:180-190) enters the parse only
 // through the NIL head slot at exactly MAX_DIST: that happens iff
@@ -39,24 +44,56 @@
 static_assert(ZS_SPEC_SLOTS % 4 == 0 && ZS_SEG_WORDS % 4 == 0, "16-byte aligned scratch regions");
 static_assert(ZS_SEG == ZS_PARSE_SEG && ZS_SEG_WORDS == ZS_PARSE_SEG_WORDS, "scratch layout shared with capi.cpp");
 
-struct zs_seg_info {
-  uint32_t end;         // first position >= the segment end visited by the speculative parse
-  uint32_t nspec;       // speculative symbols
-  uint32_t ma, ml, ms;  // speculative state at `end`
-  uint32_t start;       // position where the segment's final symbol run starts
-  uint32_t nfix;        // catch-up symbols (true parse) preceding the splice
-  uint32_t from;        // first speculative symbol kept (ZS_NONE: none)
+// Per-lane match-table windows of pass A (WIN > 0): the wave stages, for every
+// lane, the WIN table entries from its position (and the input bytes there) in
+// LDS, then parses from LDS until every lane has left its window.  One memory
+// round trip per stage instead of one per parse step: a step's position depends
+// on the previous step's entry, so direct loads put the full memory latency on
+// every step.  Entry k of lane l is at m[k / 2][l] (a lane's reads are 16 B
+// apart from its neighbours': conflict-free), bytes in[w + 4 j, +4) at s[j][l].
+// WIN = 32 (the default, 19 KiB of LDS: 8 workgroups per CU) halves the
+// stages of WIN = 16 (10 KiB: all 16 workgroups a CU gets at 4096 streams
+// fit) and measures faster: 2.10 vs 2.26 ms at 4096 streams, 3.2 ms with
+// direct loads (profiles/r02).
+template <uint32_t WIN>
+struct zs_parse_win {
+  uint4 m[WIN / 2][64];
+  uint32_t s[WIN / 4][64];
+};
+template <>
+struct zs_parse_win<0> {};
+
+// per-segment values pass C looks up by segment
+struct zs_seg_tab {
+  uint32_t off[65];  // first run symbol of each segment in the round (exclusive prefix; off[64] = round total)
+  uint32_t nf[64];   // catch-up symbols
+  uint32_t from[64]; // first speculative symbol kept (ZS_NONE: none)
 };
 
-__global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                 const uint32_t* __restrict__ in_len,
-                                                 const uint64_t* __restrict__ pos_base,
-                                                 const uint32_t* __restrict__ blk_base, const uint2* __restrict__ mres,
-                                                 uint32_t* __restrict__ syms, zs_block* __restrict__ blocks,
-                                                 zs_stream* __restrict__ streams, uint32_t* __restrict__ scratch,
-                                                 int good, int lazy) {
-  __shared__ zs_seg_info seg[64];
-  __shared__ uint32_t sh_tail[1];  // true parse's match_available after the round
+static __device__ __forceinline__ uint32_t zs_sym_len(uint32_t v) {
+  return (v & 0x80000000u) ? ((v >> 16) & 0xffu) + ZS_MIN_MATCH : 1u;
+}
+static __device__ __forceinline__ zs_pstate zs_read_state(const zs_pstate& x, uint32_t l) {
+  zs_pstate r;
+  r.p = (uint32_t)__builtin_amdgcn_readlane((int)x.p, (int)l);
+  r.ma = (uint32_t)__builtin_amdgcn_readlane((int)x.ma, (int)l);
+  r.ml = (uint32_t)__builtin_amdgcn_readlane((int)x.ml, (int)l);
+  r.ms = (uint32_t)__builtin_amdgcn_readlane((int)x.ms, (int)l);
+  return r;
+}
+
+#define ZS_GATHER 16  // pass C: 64-symbol chunks loaded before any is stored
+
+template <uint32_t WIN>
+static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_seg_tab& T,
+                                                     const uint8_t* __restrict__ in,
+                                                     const uint64_t* __restrict__ in_off,
+                                                     const uint32_t* __restrict__ in_len,
+                                                     const uint64_t* __restrict__ pos_base,
+                                                     const uint32_t* __restrict__ blk_base,
+                                                     const uint2* __restrict__ mres, uint32_t* __restrict__ syms,
+                                                     zs_block* __restrict__ blocks, zs_stream* __restrict__ streams,
+                                                     uint32_t* __restrict__ scratch, int good, int lazy) {
   const int s = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint32_t n = in_len[s];
@@ -67,25 +104,28 @@ __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in,
   zs_block* blk = blocks + blk_base[s];
   const uint32_t nseg = (n + ZS_SEG - 1) / ZS_SEG;
 
-  zs_pstate t = {0, 0, ZS_MIN_MATCH - 1, 0};  // true parse state (lane 0)
-  uint32_t total = 0;  // symbols written (wave-uniform)
-  uint32_t last_start = 0;  // start position of the last symbol written (lane 63 of the last chunk)
+  zs_pstate t = {0, 0, ZS_MIN_MATCH - 1, 0};  // the true parse state entering the round (wave-uniform)
+  uint32_t total = 0;     // symbols written (wave-uniform)
+  uint32_t last_sym = 0;  // the last symbol written (wave-uniform)
 
   for (uint32_t r0 = 0; r0 < nseg; r0 += 64) {
     const uint32_t nr = min(64u, nseg - r0);
-    // ---- pass A: speculative parse of segment r0 + lane
-    if (lane < nr) {
-      const uint32_t k = r0 + lane;
-      const uint32_t a = k * ZS_SEG, b = min(n, a + ZS_SEG);
-      uint32_t* spec = scr + (size_t)lane * ZS_SEG_WORDS;
-      uint32_t* sync = spec + ZS_SPEC_SLOTS;
-      zs_pstate st = {a, 0, ZS_MIN_MATCH - 1, 0};
-      uint32_t cnt = 0, nsync = 0;
+    const bool mine = lane < nr;  // lane owns segment r0 + lane
+    const uint32_t a = mine ? (r0 + lane) * ZS_SEG : n, b = mine ? min(n, a + ZS_SEG) : n;
+    uint32_t* spec = scr + (size_t)lane * ZS_SEG_WORDS;
+    uint32_t* sync = spec + ZS_SPEC_SLOTS;
+    uint32_t* fix = sync + ZS_SYNC_SLOTS;
+
+    // ---- pass A: speculative parse of the lane's segment from the position-0 state
+    zs_pstate st = {a, 0, ZS_MIN_MATCH - 1, 0};
+    uint32_t cnt = 0;
+    {
+      uint32_t nsync = 0;
       // Symbols and sync entries are gathered four at a time and stored as one
       // 16-byte write: on gfx9 stores share vmcnt with loads, so a store in every
-      // iteration would make each match-table load wait for the previous stores.
+      // iteration would make the next load wait for the previous stores.
       uint4 sacc = make_uint4(0, 0, 0, 0), yacc = make_uint4(0, 0, 0, 0);
-      while (st.p < b) {
+      auto step = [&](uint2 e, uint32_t lit) __attribute__((always_inline)) {
         // sync key: (position - a) << 1 | match_available, with the symbol count
         if (st.ml == ZS_MIN_MATCH - 1) {
           const uint32_t y = ((st.p - a) << 17) | (st.ma << 16) | cnt, m = nsync & 3u;
@@ -95,8 +135,7 @@ __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in,
           yacc.w = m == 3 ? y : yacc.w;
           if (++nsync % 4 == 0) *reinterpret_cast<uint4*>(sync + nsync - 4) = yacc;
         }
-        const uint32_t p = st.p;
-        const uint32_t v = zs_parse_step(st, M[p], p > 0 ? src[p - 1] : 0u, n, good, lazy);
+        const uint32_t v = zs_parse_step(st, e, lit, n, good, lazy);
         if (v != ZS_NONE) {
           const uint32_t m = cnt & 3u;
           sacc.x = m == 0 ? v : sacc.x;
@@ -105,128 +144,174 @@ __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in,
           sacc.w = m == 3 ? v : sacc.w;
           if (++cnt % 4 == 0) *reinterpret_cast<uint4*>(spec + cnt - 4) = sacc;
         }
-      }
-      for (uint32_t i = nsync & ~3u; i < nsync; i++) sync[i] = (i & 3u) == 0 ? yacc.x : (i & 3u) == 1 ? yacc.y : yacc.z;
-      for (uint32_t i = cnt & ~3u; i < cnt; i++) spec[i] = (i & 3u) == 0 ? sacc.x : (i & 3u) == 1 ? sacc.y : sacc.z;
-      sync[nsync] = ZS_NONE;
-      if (b == n && st.ma) spec[cnt++] = src[n - 1];  // final deferred literal (deflate.ts:1429-1432)
-      seg[lane].end = st.p;
-      seg[lane].nspec = cnt;
-      seg[lane].ma = st.ma;
-      seg[lane].ml = st.ml;
-      seg[lane].ms = st.ms;
-    }
-    __syncthreads();
-
-    // ---- pass B: the true parse across each boundary, until it meets a sync point
-    if (lane == 0) {
-      for (uint32_t j = 0; j < nr; j++) {
-        const uint32_t a = (r0 + j) * ZS_SEG, b = min(n, a + ZS_SEG);
-        const uint32_t* spec = scr + (size_t)j * ZS_SEG_WORDS;
-        const uint32_t* sync = spec + ZS_SPEC_SLOTS;
-        uint32_t* fix = scr + (size_t)j * ZS_SEG_WORDS + ZS_SPEC_SLOTS + ZS_SYNC_SLOTS;
-        uint32_t nf = 0, from = ZS_NONE, si = 0, sv = sync[0];
-        uint4 facc = make_uint4(0, 0, 0, 0);
-        seg[j].start = t.p - t.ma;  // a pending literal in[t.p - 1] opens the run
-        while (t.p < b) {
-          if (t.ml == ZS_MIN_MATCH - 1) {
-            const uint32_t key = ((t.p - a) << 1) | t.ma;
-            while ((sv >> 16) < key) sv = sync[++si];  // sentinel 0xffffffff stops the scan
-            if ((sv >> 16) == key) { from = sv & 0xffffu; break; }
+      };
+      if constexpr (WIN == 0) {
+        while (st.p < b) {
+          const uint32_t p = st.p;
+          step(M[p], p > 0 ? src[p - 1] : 0u);
+        }
+      } else {
+        while (__ballot(st.p < b) != 0) {
+          // stage: this lane's window [w, w + WIN) (entries past n are never read)
+          const uint32_t w = st.p & ~3u;
+          uint32_t before = 0;  // in[w - 1]
+          if (st.p < b) {
+            const uint4* g = reinterpret_cast<const uint4*>(M + w);
+#pragma unroll
+            for (uint32_t j = 0; j < WIN / 2; j++) W.m[j][lane] = w + 2 * j < n ? g[j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t j = 0; j < WIN / 4; j++) W.s[j][lane] = zs_load_word(src, n, w + 4 * j);
+            before = w >= 4 ? zs_load_word(src, n, w - 4) >> 24 : 0u;
           }
-          const uint32_t p = t.p;
-          const uint32_t v = zs_parse_step(t, M[p], p > 0 ? src[p - 1] : 0u, n, good, lazy);
-          if (v != ZS_NONE) {  // gathered four at a time (see pass A)
-            const uint32_t m = nf & 3u;
-            facc.x = m == 0 ? v : facc.x;
-            facc.y = m == 1 ? v : facc.y;
-            facc.z = m == 2 ? v : facc.z;
-            facc.w = m == 3 ? v : facc.w;
-            if (++nf % 4 == 0) *reinterpret_cast<uint4*>(fix + nf - 4) = facc;
+          while (st.p < b && st.p < w + WIN) {
+            const uint32_t o = st.p - w, q = o - 1;  // in[p - 1] is staged byte o - 1 (o > 0)
+            const uint2 e = reinterpret_cast<const uint2*>(&W.m[o >> 1][lane])[o & 1];
+            const uint32_t lb = reinterpret_cast<const uint8_t*>(&W.s[(q >> 2) & (WIN / 4 - 1)][lane])[q & 3];
+            step(e, o == 0 ? before : lb);
           }
         }
-        for (uint32_t i = nf & ~3u; i < nf; i++) fix[i] = (i & 3u) == 0 ? facc.x : (i & 3u) == 1 ? facc.y : facc.z;
-        if (from != ZS_NONE) {  // continue from the speculative end state
-          t.p = seg[j].end;
-          t.ma = seg[j].ma;
-          t.ml = seg[j].ml;
-          t.ms = seg[j].ms;
-        } else if (b == n && t.ma) {
-          fix[nf++] = src[n - 1];  // final deferred literal
-        }
-        seg[j].nfix = nf;
-        seg[j].from = from;
       }
-      sh_tail[0] = t.ma;
+      if (mine) {
+        for (uint32_t i = nsync & ~3u; i < nsync; i++) sync[i] = (i & 3u) == 0 ? yacc.x : (i & 3u) == 1 ? yacc.y : yacc.z;
+        for (uint32_t i = cnt & ~3u; i < cnt; i++) spec[i] = (i & 3u) == 0 ? sacc.x : (i & 3u) == 1 ? sacc.y : sacc.z;
+        sync[nsync] = ZS_NONE;
+        if (b == n && st.ma) spec[cnt++] = src[n - 1];  // final deferred literal (deflate.ts:1429-1432)
+      }
     }
-    __syncthreads();
-    const bool last_round = r0 + nr == nseg;
-    const bool final_lit = last_round && sh_tail[0] != 0;
-    uint32_t round_total = 0;
-    if (last_round) {
-      for (uint32_t j = 0; j < nr; j++)
-        round_total += seg[j].nfix + (seg[j].from == ZS_NONE ? 0u : seg[j].nspec - seg[j].from);
-    }
-    const uint32_t unchecked = final_lit ? total + round_total - 1 : ZS_NONE;  // global index of the final literal
 
-    // ---- pass C: splice and cut blocks.  A segment's run is its catch-up
-    // symbols followed by its speculative symbols from the sync point; they are
-    // read four 64-symbol chunks at a time before any of them is stored (loads
-    // wait for earlier stores on gfx9).
+    // ---- pass B: the true parse across each boundary until it meets a sync
+    // point of the segment.  Every lane does its own boundary at once, entering
+    // with the speculative end state of the segment before (which IS the true
+    // state there whenever that segment synced; lane 0 enters with the true
+    // state); a serial check then redoes, in order, the rare boundary whose
+    // predecessor never synced.
+    uint32_t nf = 0, from = ZS_NONE, start = 0;
+    zs_pstate after;  // true state at the segment's end, given its entry state
+    auto catch_up = [&](zs_pstate c) __attribute__((always_inline)) {
+      uint32_t si = 0, sv = sync[0];
+      uint4 facc = make_uint4(0, 0, 0, 0);
+      nf = 0;
+      from = ZS_NONE;
+      start = c.p - c.ma;  // a pending literal in[c.p - 1] opens the run
+      while (c.p < b) {
+        if (c.ml == ZS_MIN_MATCH - 1) {
+          const uint32_t key = ((c.p - a) << 1) | c.ma;
+          while ((sv >> 16) < key) sv = sync[++si];  // sentinel 0xffffffff stops the scan
+          if ((sv >> 16) == key) { from = sv & 0xffffu; break; }
+        }
+        const uint32_t p = c.p;
+        const uint32_t v = zs_parse_step(c, M[p], p > 0 ? src[p - 1] : 0u, n, good, lazy);
+        if (v != ZS_NONE) {  // gathered four at a time (see pass A)
+          const uint32_t m = nf & 3u;
+          facc.x = m == 0 ? v : facc.x;
+          facc.y = m == 1 ? v : facc.y;
+          facc.z = m == 2 ? v : facc.z;
+          facc.w = m == 3 ? v : facc.w;
+          if (++nf % 4 == 0) *reinterpret_cast<uint4*>(fix + nf - 4) = facc;
+        }
+      }
+      for (uint32_t i = nf & ~3u; i < nf; i++) fix[i] = (i & 3u) == 0 ? facc.x : (i & 3u) == 1 ? facc.y : facc.z;
+      if (from == ZS_NONE && b == n && c.ma) fix[nf++] = src[n - 1];  // final deferred literal
+      after = from != ZS_NONE ? st : c;  // synced: continues as the speculative parse did
+    };
+    {
+      zs_pstate e;  // entry: the speculative end of segment lane - 1
+      const int up = (int)((lane + 63u) & 63u);
+      e.p = (uint32_t)__shfl((int)st.p, up, 64);
+      e.ma = (uint32_t)__shfl((int)st.ma, up, 64);
+      e.ml = (uint32_t)__shfl((int)st.ml, up, 64);
+      e.ms = (uint32_t)__shfl((int)st.ms, up, 64);
+      if (lane == 0) e = t;
+      if (mine) catch_up(e);
+    }
     for (uint32_t j = 0; j < nr; j++) {
-      const zs_seg_info si = seg[j];
-      uint32_t pos = si.start;
-      const uint32_t* base = scr + (size_t)j * ZS_SEG_WORDS;
-      const uint32_t* fx = base + ZS_SPEC_SLOTS + ZS_SYNC_SLOTS;
-      const uint32_t* sp = base + (si.from == ZS_NONE ? 0u : si.from);
-      const uint32_t cnt = si.nfix + (si.from == ZS_NONE ? 0u : si.nspec - si.from);
-      for (uint32_t g0 = 0; g0 < cnt; g0 += 256) {
-        uint32_t vv[4];
+      if (j > 0 && (uint32_t)__builtin_amdgcn_readlane((int)from, (int)(j - 1)) == ZS_NONE) {
+        if (lane == j) catch_up(t);  // segment j - 1 never synced: t is its true end state
+      }
+      t = zs_read_state(after, j);
+    }
+
+    // ---- pass C: splice.  A segment's run is its catch-up symbols followed
+    // by its speculative symbols from the sync point; the round's runs are
+    // concatenated into the stream's symbols by a gather, ZS_GATHER chunks of
+    // 64 loaded before any is stored (loads wait for earlier stores on gfx9).
+    const uint32_t run = mine ? nf + (from == ZS_NONE ? 0u : cnt - from) : 0u;
+    uint32_t incl = run;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uint32_t i = g0 + 64 * q + lane;
-          vv[q] = i < cnt ? (i < si.nfix ? fx[i] : sp[i - si.nfix]) : 0u;
-        }
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    T.off[lane] = incl - run;
+    if (lane == 63) T.off[64] = R;
+    T.nf[lane] = nf;
+    T.from[lane] = from;
+    __syncthreads();
+    uint32_t js = 0, lastv = 0;
+    for (uint32_t g0 = 0; g0 < R; g0 += 64 * ZS_GATHER) {
+      uint32_t v[ZS_GATHER];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uint32_t c0 = g0 + 64 * q;
-          if (c0 >= cnt) break;
-          const uint32_t i = c0 + lane;
-          const uint32_t v = vv[q];
-          const uint32_t len = i < cnt ? ((v & 0x80000000u) ? ((v >> 16) & 0xffu) + ZS_MIN_MATCH : 1u) : 0u;
-          uint32_t x = len;  // inclusive scan of symbol lengths
-#pragma unroll
-          for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if (lane >= (uint32_t)d) x += y;
-          }
-          if (i < cnt) {
-            const uint32_t gi = total + lane;  // `total` already counts the previous chunks
-            sy[gi] = v;
-            if ((gi + 1) % ZS_SYM_END == 0 && gi != unchecked) {
-              // FLUSH_BLOCK after this symbol; remember the window base for the stored-block check
-              const uint32_t bi = (gi + 1) / ZS_SYM_END - 1;
-              const uint32_t st0 = pos + x - len;
-              blk[bi].in_end = pos + x;
-              blk[bi].pad = zs_slides(st0 + 1, n);
-            }
-          }
-          const uint32_t m = min(64u, cnt - c0);
-          last_start = __shfl(pos + x - len, (int)m - 1, 64);
-          pos += __shfl(x, 63, 64);
-          total += m;
+      for (int k = 0; k < ZS_GATHER; k++) {
+        const uint32_t g = g0 + 64 * k + lane;
+        v[k] = 0;
+        if (g < R) {
+          while (T.off[js + 1] <= g) js++;
+          const uint32_t i = g - T.off[js], nfj = T.nf[js];
+          const uint32_t* base = scr + (size_t)js * ZS_SEG_WORDS;
+          v[k] = i < nfj ? base[ZS_SPEC_SLOTS + ZS_SYNC_SLOTS + i] : base[T.from[js] + i - nfj];
         }
       }
+#pragma unroll
+      for (int k = 0; k < ZS_GATHER; k++) {
+        const uint32_t g = g0 + 64 * k + lane;
+        if (g < R) sy[total + g] = v[k];
+        if (g == R - 1) lastv = v[k];
+      }
     }
+    if (R) last_sym = (uint32_t)__shfl((int)lastv, (int)((R - 1) & 63u), 64);
+
+    // block cuts: FLUSH_BLOCK after every 16383rd tallied symbol (deflate.ts:336,
+    // 1120-1124) -- but not after the final deferred literal, which is tallied
+    // after the loop (deflate.ts:1429-1432)
+    const bool final_lit = r0 + nr == nseg && t.ma != 0;
+    const uint32_t unchecked = final_lit ? total + R - 1 : ZS_NONE;
+    for (uint32_t gi = (total / ZS_SYM_END + 1) * ZS_SYM_END - 1; gi < total + R; gi += ZS_SYM_END) {
+      if (gi == unchecked) continue;
+      const uint32_t g = gi - total;
+      uint32_t j = 0;
+      while (T.off[j + 1] <= g) j++;
+      const uint32_t i = g - T.off[j], nfj = T.nf[j], fj = T.from[j];
+      const uint32_t* base = scr + (size_t)j * ZS_SEG_WORDS;
+      uint32_t acc = 0, li = 0;  // run lengths through symbol i, symbol i's length
+      for (uint32_t q = lane; q <= i; q += 64) {
+        const uint32_t l = zs_sym_len(q < nfj ? base[ZS_SPEC_SLOTS + ZS_SYNC_SLOTS + q] : base[fj + q - nfj]);
+        acc += l;
+        li = q == i ? l : li;
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        acc += __shfl_xor(acc, d, 64);
+        li += __shfl_xor(li, d, 64);
+      }
+      const uint32_t end = (uint32_t)__builtin_amdgcn_readlane((int)start, (int)j) + acc;
+      if (lane == 0) {  // the block's input end; its window base for the stored-block check
+        const uint32_t bi = (gi + 1) / ZS_SYM_END - 1;
+        blk[bi].in_end = end;
+        blk[bi].pad = zs_slides(end - li + 1, n);
+      }
+    }
+    total += R;
     __syncthreads();
   }
 
   // ---- block records (deflate.ts:1434-1440: the final block takes the rest, possibly empty)
-  const bool final_lit = nseg > 0 && sh_tail[0] != 0;
+  const bool final_lit = nseg > 0 && t.ma != 0;
   const uint32_t checked = final_lit ? total - 1 : total;
   const uint32_t nflush = checked / ZS_SYM_END;
-  // window base when the final block is flushed: slides up to the last visited position
-  const uint32_t v_last = total == 0 ? 0u : final_lit ? n - 1 : last_start + 1;
+  // window base when the final block is flushed: slides up to the last visited
+  // position (the symbols tile [0, n), so the last one starts at n - its length)
+  const uint32_t v_last = total == 0 ? 0u : final_lit ? n - 1 : n - zs_sym_len(last_sym) + 1;
   const uint32_t final_slides = zs_slides(v_last, n);
   __syncthreads();
   for (uint32_t b0 = 0; b0 <= nflush; b0 += 64) {
@@ -253,3 +338,18 @@ __global__ __launch_bounds__(64) void zs_k_parse(const uint8_t* __restrict__ in,
     streams[s].nblk = nflush + 1;
   }
 }
+
+#define ZS_PARSE_KERNEL(name, WIN)                                                                                   \
+  __global__ __launch_bounds__(64) void name(                                                                        \
+      const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,     \
+      const uint64_t* __restrict__ pos_base, const uint32_t* __restrict__ blk_base, const uint2* __restrict__ mres,  \
+      uint32_t* __restrict__ syms, zs_block* __restrict__ blocks, zs_stream* __restrict__ streams,                  \
+      uint32_t* __restrict__ scratch, int good, int lazy) {                                                         \
+    __shared__ zs_parse_win<WIN> W;                                                                                 \
+    __shared__ zs_seg_tab T;                                                                                        \
+    zs_parse_body<WIN>(W, T, in, in_off, in_len, pos_base, blk_base, mres, syms, blocks, streams, scratch, good,    \
+                       lazy);                                                                                       \
+  }
+ZS_PARSE_KERNEL(zs_k_parse16, 16)
+ZS_PARSE_KERNEL(zs_k_parse, 32)
+ZS_PARSE_KERNEL(zs_k_parse_direct, 0)

@@ -41,9 +41,15 @@ __global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uin
                             uint16_t* members, uint2* mres);
 __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint16_t* members, uint2* mres, int chain, int nice);
-__global__ void zs_k_parse(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                           const uint32_t* blk_base, const uint2* mres, uint32_t* syms, zs_block* blocks,
-                           zs_stream* streams, uint32_t* scratch, int good, int lazy);
+// the one-wave lazy parse (deflate_parse.hip): pass A stages 32 / 16 match-table
+// entries per lane in LDS (zs_k_parse / zs_k_parse16) or loads them directly (zs_k_parse_direct)
+#define ZS_PARSE_DECL(name)                                                                                        \
+  __global__ void name(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base, \
+                       const uint32_t* blk_base, const uint2* mres, uint32_t* syms, zs_block* blocks,              \
+                       zs_stream* streams, uint32_t* scratch, int good, int lazy);
+ZS_PARSE_DECL(zs_k_parse)
+ZS_PARSE_DECL(zs_k_parse16)
+ZS_PARSE_DECL(zs_k_parse_direct)
 // parse scratch words per 1024-position segment (deflate_parse.hip)
 #define ZS_PARSE_SEG 1024u
 #define ZS_PARSE_SEG_WORDS 3596u
