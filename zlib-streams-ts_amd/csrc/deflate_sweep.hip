@@ -65,28 +65,12 @@ static __device__ __forceinline__ uint32_t sw_hash(uint32_t w) {  // SURVEY A1, 
 // 64 per instruction, claiming slots with ONE ds_add_rtn_u32 per lane: gfx950
 // applies same-address LDS atomics of one wave instruction in increasing lane
 // order (zs_selftest checks it, including the 16-bit half form used here), so
-// equal hashes get slots in position order.  Hashes come straight from global
-// memory (a 4-byte window per lane, two aligned loads).  Results of the
+// equal hashes get slots in position order.  Pass 1 hashes input words held
+// in registers, pass 2 a 4 KiB LDS stage of the input.  Results of the
 // positions that are not inserted (the last two) are zeroed.
 #define ZS_BK_THREADS 256u
 #define ZS_BK_INFLIGHT 8  // pass 2: wave instructions (x 64 positions) per wait
-#define ZS_BK_CHUNK 4096u  // pass 2: input bytes staged in LDS at a time
-
-// hash of position p (p + 2 < n); src4 = the stream's bytes as aligned words (a
-// word past n is never used for a valid p: p + 2 < n reads at most word (n-1)/4)
-static __device__ __forceinline__ uint32_t bk_hash_at(const uint8_t* src, uint32_t p, uint32_t n, bool aligned) {
-  uint32_t w;
-  if (aligned) {
-    const uint32_t* s4 = (const uint32_t*)src;
-    const uint32_t i = p >> 2;
-    const uint32_t lo = s4[i];
-    const uint32_t hi = (4 * i + 4 < n) ? s4[i + 1] : 0u;
-    w = __builtin_amdgcn_alignbyte(hi, lo, p & 3u);
-  } else {
-    w = (uint32_t)src[p] | ((uint32_t)src[p + 1] << 8) | ((uint32_t)src[p + 2] << 16);
-  }
-  return sw_hash(w);
-}
+#define ZS_BK_CHUNK 2048u  // pass 2: positions per chunk (input bytes staged in LDS, slots queued)
 
 __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __restrict__ in,
                                                             const uint64_t* __restrict__ in_off,
@@ -96,6 +80,7 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
   __shared__ uint32_t cnt[16384];
   __shared__ uint32_t part[ZS_BK_THREADS];
   __shared__ uint32_t stg[ZS_BK_CHUNK / 4 + 2];
+  __shared__ uint16_t q[2][ZS_BK_CHUNK];
   const int s = blockIdx.x;
   const uint32_t n = in_len[s];
   if (n > ZS_SWEEP_MAX) return;  // zs_k_prev / zs_k_match's stream
@@ -106,20 +91,31 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
   const uint32_t m = n > 2 ? n - 2 : 0u;  // inserted positions (deflate.ts:1367-1370)
   for (uint32_t p = m + tid; p < n; p += ZS_BK_THREADS) out[p] = make_uint2(0, 0);
   if (m == 0) return;
-  for (uint32_t i = tid; i < 16384; i += ZS_BK_THREADS) cnt[i] = 0;
+  for (uint32_t i = tid; i < 16384 / 4; i += ZS_BK_THREADS) reinterpret_cast<uint4*>(cnt)[i] = make_uint4(0, 0, 0, 0);
   const bool aligned = ((uintptr_t)src & 3u) == 0;
   __syncthreads();
-  // pass 1: bucket sizes (unordered adds, all waves)
-  for (uint32_t p0 = 0; p0 < m; p0 += 4 * ZS_BK_THREADS) {
-    uint32_t h[4];
+  // pass 1: bucket sizes (unordered adds, all waves).  Thread t hashes the 16
+  // positions [p0 + 16 t, +16) from 5 input words; the next 4 KiB block's words
+  // are loaded before this block's adds (a load round trip per block, not per
+  // four positions).
+  {
+    uint32_t w[5], nw[5];
+    auto load5 = [&](uint32_t p0, uint32_t* x) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t p = p0 + ZS_BK_THREADS * j + tid;
-      h[j] = p < m ? bk_hash_at(src, p, n, aligned) : 0xffffffffu;
+      for (int k = 0; k < 5; k++) x[k] = zs_load_word(src, n, p0 + 16 * tid + 4 * k);
+    };
+    load5(0, nw);
+    for (uint32_t p0 = 0; p0 < m; p0 += 16 * ZS_BK_THREADS) {
+#pragma unroll
+      for (int k = 0; k < 5; k++) w[k] = nw[k];
+      if (p0 + 16 * ZS_BK_THREADS < m) load5(p0 + 16 * ZS_BK_THREADS, nw);
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j++) {
+        const uint32_t p = p0 + 16 * tid + j;
+        const uint32_t h = sw_hash(__builtin_amdgcn_alignbyte(w[(j >> 2) + 1], w[j >> 2], j & 3u));
+        if (p < m) atomicAdd(&cnt[h >> 1], 1u << (16u * (h & 1u)));
+      }
     }
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (h[j] != 0xffffffffu) atomicAdd(&cnt[h[j] >> 1], 1u << (16u * (h[j] & 1u)));
   }
   __syncthreads();
   // exclusive scan: thread i owns words [64i, 64i + 64) (buckets 128i ...)
@@ -157,12 +153,15 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
     }
   }
   __syncthreads();
-  if (tid >= 64) return;
-  // pass 2: ordered scatter by wave 0.  The input goes through LDS 4 KiB at a
-  // time (stg, the pass-1 partial sums' neighbour), the next chunk's loads in
-  // flight in registers while this chunk's positions are claimed,
-  // ZS_BK_INFLIGHT instructions per wait.
-  const uint32_t lane = tid;
+  // pass 2: wave 0 claims the slots in position order, ZS_BK_CHUNK positions
+  // at a time, into an LDS queue (slot of chunk position o at q[c & 1][o]);
+  // waves 1..3 scatter the previous chunk's positions to their slots while it
+  // claims the next one (stores from one wave alone take longer than the
+  // claims: 64 scattered 2-byte stores per instruction).  The input goes
+  // through LDS a chunk at a time (stg), the next chunk's loads in flight in
+  // registers while this chunk's positions are claimed, ZS_BK_INFLIGHT
+  // instructions per wait.
+  const uint32_t wave = tid >> 6, lane = tid & 63u;
   constexpr uint32_t CW = ZS_BK_CHUNK / 4 / 64;  // words per lane per chunk
   uint32_t nxt[CW + 1];
   auto fetch = [&](uint32_t c0) {
@@ -180,49 +179,59 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
       nxt[i] = v;
     }
   };
-  fetch(0);
-  for (uint32_t c0 = 0; c0 < m; c0 += ZS_BK_CHUNK) {
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+  if (wave == 0) fetch(0);
+  const uint32_t nch = (m + ZS_BK_CHUNK - 1) / ZS_BK_CHUNK;
+  for (uint32_t c = 0; c <= nch; c++) {
+    const uint32_t c0 = c * ZS_BK_CHUNK;
+    if (wave == 0 && c < nch) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (uint32_t i = 0; i <= CW; i++)
-      if (64 * i + lane < ZS_BK_CHUNK / 4 + 2) stg[64 * i + lane] = nxt[i];
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    if (c0 + ZS_BK_CHUNK < m) fetch(c0 + ZS_BK_CHUNK);
-    const uint32_t c1 = min(m, c0 + ZS_BK_CHUNK);
-    for (uint32_t g0 = c0; g0 < c1; g0 += 64 * ZS_BK_INFLIGHT) {
-      uint32_t a[ZS_BK_INFLIGHT], v[ZS_BK_INFLIGHT], sh[ZS_BK_INFLIGHT], e[ZS_BK_INFLIGHT];
+      for (uint32_t i = 0; i <= CW; i++)
+        if (64 * i + lane < ZS_BK_CHUNK / 4 + 2) stg[64 * i + lane] = nxt[i];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      if (c0 + ZS_BK_CHUNK < m) fetch(c0 + ZS_BK_CHUNK);
+      const uint32_t c1 = min(m, c0 + ZS_BK_CHUNK);
+      uint16_t* const qc = q[c & 1u];
+      for (uint32_t g0 = c0; g0 < c1; g0 += 64 * ZS_BK_INFLIGHT) {
+        uint32_t a[ZS_BK_INFLIGHT], v[ZS_BK_INFLIGHT], sh[ZS_BK_INFLIGHT], e[ZS_BK_INFLIGHT];
 #pragma unroll
-      for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
-        const uint32_t p = g0 + 64 * j + lane;
-        const uint32_t o = p - c0;
-        const uint32_t h = sw_hash(__builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u));
-        sh[j] = 16u * (h & 1u);
-        a[j] = sw_lds_addr(&cnt[h >> 1]);
-        v[j] = p < c1 ? 1u << sh[j] : 0u;  // a lane past the chunk adds nothing
+        for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
+          const uint32_t p = g0 + 64 * j + lane;
+          const uint32_t o = p - c0;
+          const uint32_t h = sw_hash(__builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u));
+          sh[j] = 16u * (h & 1u);
+          a[j] = sw_lds_addr(&cnt[h >> 1]);
+          v[j] = p < c1 ? 1u << sh[j] : 0u;  // a lane past the chunk adds nothing
+        }
+        // in order: instruction j's adds land after instruction j-1's (LDS executes a wave's ops in order)
+        asm volatile(
+            "ds_add_rtn_u32 %0, %8, %16\n\t"
+            "ds_add_rtn_u32 %1, %9, %17\n\t"
+            "ds_add_rtn_u32 %2, %10, %18\n\t"
+            "ds_add_rtn_u32 %3, %11, %19\n\t"
+            "ds_add_rtn_u32 %4, %12, %20\n\t"
+            "ds_add_rtn_u32 %5, %13, %21\n\t"
+            "ds_add_rtn_u32 %6, %14, %22\n\t"
+            "ds_add_rtn_u32 %7, %15, %23\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(e[0]), "=&v"(e[1]), "=&v"(e[2]), "=&v"(e[3]), "=&v"(e[4]), "=&v"(e[5]), "=&v"(e[6]), "=&v"(e[7])
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(v[0]),
+              "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7])
+            : "memory");
+#pragma unroll
+        for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
+          const uint32_t p = g0 + 64 * j + lane;
+          if (p < c1) qc[p - c0] = (uint16_t)(e[j] >> sh[j]);
+        }
       }
-      // in order: instruction j's adds land after instruction j-1's (LDS executes a wave's ops in order)
-      asm volatile(
-          "ds_add_rtn_u32 %0, %8, %16\n\t"
-          "ds_add_rtn_u32 %1, %9, %17\n\t"
-          "ds_add_rtn_u32 %2, %10, %18\n\t"
-          "ds_add_rtn_u32 %3, %11, %19\n\t"
-          "ds_add_rtn_u32 %4, %12, %20\n\t"
-          "ds_add_rtn_u32 %5, %13, %21\n\t"
-          "ds_add_rtn_u32 %6, %14, %22\n\t"
-          "ds_add_rtn_u32 %7, %15, %23\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(e[0]), "=&v"(e[1]), "=&v"(e[2]), "=&v"(e[3]), "=&v"(e[4]), "=&v"(e[5]), "=&v"(e[6]), "=&v"(e[7])
-          : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(v[0]),
-            "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7])
-          : "memory");
-#pragma unroll
-      for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
-        const uint32_t p = g0 + 64 * j + lane;
-        if (p < c1) mem[(e[j] >> sh[j]) & 0xffffu] = (uint16_t)p;
-      }
+    } else if (wave != 0 && c > 0) {
+      const uint32_t b0 = c0 - ZS_BK_CHUNK, cnt1 = min(m, c0) - b0;
+      const uint16_t* const qp = q[(c - 1) & 1u];
+      for (uint32_t o = tid - 64u; o < cnt1; o += ZS_BK_THREADS - 64u) mem[qp[o]] = (uint16_t)(b0 + o);
     }
+    __syncthreads();
   }
 }
 

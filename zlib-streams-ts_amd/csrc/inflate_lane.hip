@@ -33,7 +33,11 @@ struct zs_lane_reader {
 };
 
 static __device__ __forceinline__ uint32_t zs_lr_load4(const zs_lane_reader& R, uint32_t at) {
-  return zs_load_word(R.src, R.n, at);  // one load when aligned and inside the input
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++)
+    if (at + k < R.n) v |= (uint32_t)R.src[at + k] << (8 * k);
+  return v;
 }
 // bits < 32 -> bits >= 32: the prefetched word enters hold and the next one is
 // requested, so its latency overlaps the decoding of the bits just added
