@@ -1,12 +1,14 @@
 // deflate_emit.hip -- Huffman tree construction, block layout and bit packing.
 //
 //   zs_k_trees  : one wave per block.  The wave histograms the block's symbols
-//                 with LDS atomics; lane 0 then runs the reference's exact tree
-//                 construction (heap ordered by freq then depth, overflow
-//                 repair, canonical bit-reversed codes -- trees.ts:167-316),
-//                 the tree run-length coding (trees.ts:318-447) and the
-//                 stored/static/dynamic choice (trees.ts:554-583).  The code
-//                 table and the dynamic header bits go to global memory.
+//                 with LDS atomics; lane 0 then runs the serial heart of the
+//                 reference's exact tree construction (heap ordered by freq
+//                 then depth, bit lengths with overflow repair --
+//                 trees.ts:167-316), the tree run-length coding
+//                 (trees.ts:318-447) and the stored/static/dynamic choice
+//                 (trees.ts:554-583); the wave does the rest in parallel
+//                 (frequency set-up, canonical codes by per-length ballots,
+//                 payload bit counts, the code table and header stores).
 //   zs_k_layout : one lane per stream: bit offset of every block (stored
 //                 blocks depend on byte alignment), output length, status, and
 //                 zeroing of the words that two writers share.
@@ -27,10 +29,12 @@ struct zs_tw {  // LDS workspace of one wave, common/types.ts DeflateState tree 
   uint16_t dfreq[2 * ZS_D_CODES + 1], dlen[2 * ZS_D_CODES + 1], ddad[2 * ZS_D_CODES + 1], dcode[2 * ZS_D_CODES + 1];
   uint16_t bfreq[2 * ZS_BL_CODES + 1], blen[2 * ZS_BL_CODES + 1], bdad[2 * ZS_BL_CODES + 1], bcode[2 * ZS_BL_CODES + 1];
   int16_t heap[2 * ZS_L_CODES + 1];
-  uint32_t hk[2 * ZS_L_CODES + 2];  // working heap: freq << 17 | depth << 10 | node
+  uint32_t hk[2 * ZS_L_CODES + 4] __attribute__((aligned(16)));  // working heap: freq << 17 | depth << 10 | node
+                                                                   // (+2: the sift reads grandchildren 2j..2j+3)
   uint16_t bl_count[16];
   uint32_t hist[ZS_L_CODES + ZS_D_CODES];
   uint32_t hdr[ZS_HDR_WORDS];
+  uint32_t bc[4];  // lane 0 -> wave: type, max codes, header bits
 };
 
 struct zs_tdesc {
@@ -57,19 +61,32 @@ struct zs_tstate {
 // end-of-block), below 2^15; depths stay far below 2^7; nodes below 2^10.
 static __device__ __forceinline__ uint32_t zs_hkey(uint32_t e) { return e >> 10; }
 
-static __device__ void zs_pqdownheap(zs_tstate& t, int k) {  // trees.ts:167-185
+// pqdownheap (trees.ts:167-185), two levels per LDS round trip: the children
+// j, j + 1 and all four grandchildren 2j .. 2j + 3 are read together (entries
+// past heap_len are read but never selected: the j < heap_len / j2 <= heap_len
+// tests guard them).
+static __device__ void zs_pqdownheap(zs_tstate& t, int k) {
   uint32_t* hk = t.w->hk;
-  const uint32_t v = hk[k];
+  const uint32_t v = hk[k], kv = zs_hkey(v);
+  const int len = t.heap_len;
   int j = k << 1;
-  while (j <= t.heap_len) {
-    const uint32_t a = hk[j], b = hk[j + 1];  // hk[heap_len + 1] is never selected (j < heap_len test)
-    const bool right = j < t.heap_len && zs_hkey(b) <= zs_hkey(a);
-    const uint32_t c = right ? b : a;
-    j += right ? 1 : 0;
-    if (zs_hkey(v) <= zs_hkey(c)) break;
+  while (j <= len) {
+    const uint2 ch = *reinterpret_cast<const uint2*>(&hk[j]);  // j even: 8-byte aligned
+    const uint4 gc = *reinterpret_cast<const uint4*>(&hk[2 * j]);  // 2j multiple of 4: 16-byte aligned
+    const bool right = j < len && zs_hkey(ch.y) <= zs_hkey(ch.x);
+    const uint32_t c = right ? ch.y : ch.x;
+    if (kv <= zs_hkey(c)) break;
     hk[k] = c;
-    k = j;
-    j <<= 1;
+    k = j + (right ? 1 : 0);
+    const int j2 = k << 1;
+    if (j2 > len) break;
+    const uint32_t a2 = right ? gc.z : gc.x, b2 = right ? gc.w : gc.y;
+    const bool right2 = j2 < len && zs_hkey(b2) <= zs_hkey(a2);
+    const uint32_t c2 = right2 ? b2 : a2;
+    if (kv <= zs_hkey(c2)) break;
+    hk[k] = c2;
+    k = j2 + (right2 ? 1 : 0);
+    j = k << 1;
   }
   hk[k] = v;
 }
@@ -80,18 +97,31 @@ static __device__ void zs_gen_bitlen(zs_tstate& t, zs_tdesc& d) {  // trees.ts:1
   int h, n, m, bits, xbits, overflow = 0;
   for (bits = 0; bits <= 15; bits++) bl_count[bits] = 0;
   d.len[heap[t.heap_max]] = 0;
-  for (h = t.heap_max + 1; h < ZS_HEAP_SIZE; h++) {
-    n = heap[h];
-    bits = d.len[d.dad[n]] + 1;
-    if (bits > d.max_length) { bits = d.max_length; overflow++; }
-    d.len[n] = (uint16_t)bits;
-    if (n > d.max_code) continue;
-    bl_count[bits]++;
-    xbits = n >= d.extra_base ? d.extra[n - d.extra_base] : 0;
-    const uint32_t f = d.freq[n];
-    t.opt_len += f * (uint32_t)(bits + xbits);
-    if (d.stat) t.static_len += f * ((d.stat[n] >> 16) + (uint32_t)xbits);
+  // heap[] and dad[] do not change here: read 8 entries and their parents
+  // ahead, so the loop's only dependent LDS read is len[parent]
+  for (int h0 = t.heap_max + 1; h0 < ZS_HEAP_SIZE; h0 += 8) {
+    int nb[8];
+    uint32_t db[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) nb[u] = h0 + u < ZS_HEAP_SIZE ? heap[h0 + u] : 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) db[u] = d.dad[nb[u]];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (h0 + u >= ZS_HEAP_SIZE) break;
+      n = nb[u];
+      bits = d.len[db[u]] + 1;
+      if (bits > d.max_length) { bits = d.max_length; overflow++; }
+      d.len[n] = (uint16_t)bits;
+      if (n > d.max_code) continue;
+      bl_count[bits]++;
+      xbits = n >= d.extra_base ? d.extra[n - d.extra_base] : 0;
+      const uint32_t f = d.freq[n];
+      t.opt_len += f * (uint32_t)(bits + xbits);
+      if (d.stat) t.static_len += f * ((d.stat[n] >> 16) + (uint32_t)xbits);
+    }
   }
+  h = ZS_HEAP_SIZE;
   if (overflow == 0) return;
   do {
     bits = d.max_length - 1;
@@ -115,19 +145,34 @@ static __device__ void zs_gen_bitlen(zs_tstate& t, zs_tdesc& d) {  // trees.ts:1
   }
 }
 
-static __device__ void zs_gen_codes(zs_tstate& t, zs_tdesc& d) {  // trees.ts:54-76
-  uint16_t next_code[16];
-  uint32_t code = 0;
-  for (int bits = 1; bits <= 15; bits++) { code = (code + t.w->bl_count[bits - 1]) << 1; next_code[bits] = (uint16_t)code; }
-  for (int n = 0; n <= d.max_code; n++) {
-    const int len = d.len[n];
-    if (len == 0) continue;
-    const uint32_t c = next_code[len]++;
-    d.code[n] = (uint16_t)(__builtin_bitreverse32(c) >> (32 - len));
+// gen_codes (trees.ts:54-76) by the wave: symbol n's code is the first code of
+// its length plus the number of symbols m < n of the same length, counted
+// with one ballot per length over 64 symbols at a time.  All lanes call it.
+static __device__ void zs_gen_codes_wave(const uint16_t* bl_count, const uint16_t* len, uint16_t* code, int max_code,
+                                         uint32_t lane) {
+  uint32_t fc[16];
+  uint32_t c = 0;
+#pragma unroll
+  for (int b = 1; b <= 15; b++) {
+    c = (c + bl_count[b - 1]) << 1;
+    fc[b] = c;
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int n0 = 0; n0 <= max_code; n0 += 64) {
+    const int n = n0 + (int)lane;
+    const uint32_t l = n <= max_code ? len[n] : 0u;
+    uint32_t my = 0;
+#pragma unroll
+    for (int b = 1; b <= 15; b++) {
+      const uint64_t mk = __ballot(l == (uint32_t)b);
+      my = l == (uint32_t)b ? fc[b] + (uint32_t)__popcll(mk & below) : my;
+      fc[b] += (uint32_t)__popcll(mk);
+    }
+    if (l) code[n] = (uint16_t)(__builtin_bitreverse32(my) >> (32 - l));
   }
 }
 
-static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:261-316
+static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:261-316, lane 0
   int16_t* heap = t.w->heap;
   uint32_t* hk = t.w->hk;
   int n, max_code = -1, node;
@@ -164,8 +209,7 @@ static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:2
     zs_pqdownheap(t, 1);
   } while (t.heap_len >= 2);
   heap[--t.heap_max] = (int16_t)(hk[1] & 1023u);
-  zs_gen_bitlen(t, d);
-  zs_gen_codes(t, d);
+  zs_gen_bitlen(t, d);  // the codes follow by the wave (zs_gen_codes_wave)
 }
 
 static __device__ void zs_scan_tree(zs_tstate& t, zs_tdesc& d, int max_code) {  // trees.ts:318-363
@@ -261,13 +305,13 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
     }
   }
   __syncthreads();
-  if (lane != 0) return;
-
   // init_block (trees.ts:90-103) + tally counts
-  for (int i = 0; i < ZS_L_CODES; i++) w.lfreq[i] = (uint16_t)w.hist[i];
-  w.lfreq[ZS_END_BLOCK] = 1;
-  for (int i = 0; i < ZS_D_CODES; i++) w.dfreq[i] = (uint16_t)w.hist[ZS_L_CODES + i];
-  for (int i = 0; i < ZS_BL_CODES; i++) w.bfreq[i] = 0;
+  for (uint32_t i = lane; i < ZS_L_CODES; i += 64) w.lfreq[i] = i == ZS_END_BLOCK ? 1 : (uint16_t)w.hist[i];
+  for (uint32_t i = lane; i < ZS_D_CODES; i += 64) w.dfreq[i] = (uint16_t)w.hist[ZS_L_CODES + i];
+  if (lane < ZS_BL_CODES) w.bfreq[lane] = 0;
+  __syncthreads();
+  // the serial parts run in lane 0 (its registers hold t and the max codes),
+  // the code assignment in the whole wave between them
   zs_tstate t;
   t.w = &w;
   t.opt_len = 0;
@@ -277,59 +321,79 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   zs_tdesc D = {w.dfreq, w.dlen, w.ddad, w.dcode, ZS_STATIC_DTREE, ZS_EXTRA_DBITS, 0, ZS_D_CODES, 15, 0};
   zs_tdesc B = {w.bfreq, w.blen, w.bdad, w.bcode, nullptr, nullptr, 0, ZS_BL_CODES, 7, 0};
   B.extra = ZS_EXTRA_BLBITS;
-  zs_build_tree(t, L);
-  zs_build_tree(t, D);
-  // build_bl_tree (trees.ts:416-432)
-  zs_scan_tree(t, L, L.max_code);
-  zs_scan_tree(t, D, D.max_code);
-  zs_build_tree(t, B);
-  int max_blindex;
-  for (max_blindex = ZS_BL_CODES - 1; max_blindex >= 3; max_blindex--)
-    if (w.blen[ZS_BL_ORDER[max_blindex]] != 0) break;
-  t.opt_len += 3u * ((uint32_t)max_blindex + 1) + 5 + 5 + 4;
-  uint32_t opt_lenb = (t.opt_len + 3 + 7) >> 3;
-  const uint32_t static_lenb = (t.static_len + 3 + 7) >> 3;
-  if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
-  const uint32_t stored_len = blk.in_end - blk.in_start;
-  uint32_t type;
-  if (stored_len + 4 <= opt_lenb) type = 0;
-  else if (static_lenb == opt_lenb) type = 1;
-  else type = 2;
+  if (lane == 0) zs_build_tree(t, L);
+  __syncthreads();
+  zs_gen_codes_wave(w.bl_count, w.llen, w.lcode, __builtin_amdgcn_readlane(L.max_code, 0), lane);
+  __syncthreads();
+  if (lane == 0) zs_build_tree(t, D);
+  __syncthreads();
+  zs_gen_codes_wave(w.bl_count, w.dlen, w.dcode, __builtin_amdgcn_readlane(D.max_code, 0), lane);
+  __syncthreads();
+  if (lane == 0) {  // build_bl_tree (trees.ts:416-432)
+    zs_scan_tree(t, L, L.max_code);
+    zs_scan_tree(t, D, D.max_code);
+    zs_build_tree(t, B);
+  }
+  __syncthreads();
+  zs_gen_codes_wave(w.bl_count, w.blen, w.bcode, __builtin_amdgcn_readlane(B.max_code, 0), lane);
+  __syncthreads();
+  if (lane == 0) {
+    int max_blindex;
+    for (max_blindex = ZS_BL_CODES - 1; max_blindex >= 3; max_blindex--)
+      if (w.blen[ZS_BL_ORDER[max_blindex]] != 0) break;
+    t.opt_len += 3u * ((uint32_t)max_blindex + 1) + 5 + 5 + 4;
+    uint32_t opt_lenb = (t.opt_len + 3 + 7) >> 3;
+    const uint32_t static_lenb = (t.static_len + 3 + 7) >> 3;
+    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    const uint32_t stored_len = blk.in_end - blk.in_start;
+    uint32_t type;
+    if (stored_len + 4 <= opt_lenb) type = 0;
+    else if (static_lenb == opt_lenb) type = 1;
+    else type = 2;
+    if (type == 2) {
+      // send_all_trees (trees.ts:434-447)
+      const int lcodes = L.max_code + 1, dcodes = D.max_code + 1, blcodes = max_blindex + 1;
+      zs_hput(t, (uint32_t)(lcodes - 257), 5);
+      zs_hput(t, (uint32_t)(dcodes - 1), 5);
+      zs_hput(t, (uint32_t)(blcodes - 4), 4);
+      for (int rank = 0; rank < blcodes; rank++) zs_hput(t, w.blen[ZS_BL_ORDER[rank]], 3);
+      zs_send_tree(t, L, lcodes - 1);
+      zs_send_tree(t, D, dcodes - 1);
+    }
+    w.bc[0] = type;
+    w.bc[1] = t.hbits;
+  }
+  __syncthreads();
+  const uint32_t type = w.bc[0], hbits = w.bc[1];
   // exact payload bits of the chosen coding, from the true counts
   uint32_t data_bits = 0;
-  uint32_t* cout = codes + (size_t)bi * (ZS_L_CODES + ZS_D_CODES);
   if (type != 0) {
-    for (int i = 0; i < ZS_L_CODES; i++) {
+    for (uint32_t i = lane; i < ZS_L_CODES; i += 64) {
       const uint32_t f = i == ZS_END_BLOCK ? 1u : w.hist[i];
-      if (!f) continue;
       const uint32_t len = type == 1 ? ZS_STATIC_LTREE[i] >> 16 : w.llen[i];
-      data_bits += f * (len + (i >= 257 ? (uint32_t)ZS_EXTRA_LBITS[i - 257] : 0u));
+      if (f) data_bits += f * (len + (i >= 257 ? (uint32_t)ZS_EXTRA_LBITS[i - 257] : 0u));
     }
-    for (int i = 0; i < ZS_D_CODES; i++) {
-      const uint32_t f = w.hist[ZS_L_CODES + i];
-      if (!f) continue;
-      const uint32_t len = type == 1 ? 5u : w.dlen[i];
-      data_bits += f * (len + (uint32_t)ZS_EXTRA_DBITS[i]);
+    if (lane < ZS_D_CODES) {
+      const uint32_t f = w.hist[ZS_L_CODES + lane];
+      const uint32_t len = type == 1 ? 5u : w.dlen[lane];
+      if (f) data_bits += f * (len + (uint32_t)ZS_EXTRA_DBITS[lane]);
     }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) data_bits += __shfl_xor(data_bits, d, 64);
   }
   if (type == 2) {
-    // send_all_trees (trees.ts:434-447)
-    const int lcodes = L.max_code + 1, dcodes = D.max_code + 1, blcodes = max_blindex + 1;
-    zs_hput(t, (uint32_t)(lcodes - 257), 5);
-    zs_hput(t, (uint32_t)(dcodes - 1), 5);
-    zs_hput(t, (uint32_t)(blcodes - 4), 4);
-    for (int rank = 0; rank < blcodes; rank++) zs_hput(t, w.blen[ZS_BL_ORDER[rank]], 3);
-    zs_send_tree(t, L, lcodes - 1);
-    zs_send_tree(t, D, dcodes - 1);
-    for (int i = 0; i < ZS_L_CODES; i++) cout[i] = w.lcode[i] | ((uint32_t)w.llen[i] << 16);
-    for (int i = 0; i < ZS_D_CODES; i++) cout[ZS_L_CODES + i] = w.dcode[i] | ((uint32_t)w.dlen[i] << 16);
+    uint32_t* cout = codes + (size_t)bi * (ZS_L_CODES + ZS_D_CODES);
+    for (uint32_t i = lane; i < ZS_L_CODES; i += 64) cout[i] = w.lcode[i] | ((uint32_t)w.llen[i] << 16);
+    if (lane < ZS_D_CODES) cout[ZS_L_CODES + lane] = w.dcode[lane] | ((uint32_t)w.dlen[lane] << 16);
     uint32_t* hout = hdr + (size_t)bi * ZS_HDR_WORDS;
-    for (uint32_t i = 0; i < (t.hbits + 31) / 32; i++) hout[i] = w.hdr[i];
+    for (uint32_t i = lane; i < (hbits + 31) / 32; i += 64) hout[i] = w.hdr[i];
   }
-  blk.type = type;
-  blk.hdr_bits = type == 2 ? t.hbits : 0;
-  blk.data_bits = data_bits;
-  blocks[bi] = blk;
+  if (lane == 0) {
+    blk.type = type;
+    blk.hdr_bits = type == 2 ? hbits : 0;
+    blk.data_bits = data_bits;
+    blocks[bi] = blk;
+  }
 }
 
 // --------------------------------------------------------------- layout
