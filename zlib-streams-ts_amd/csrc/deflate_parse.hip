@@ -59,6 +59,7 @@ template <uint32_t WIN>
 struct zs_parse_win {
   uint4 m[WIN / 2][64];
   uint32_t s[WIN / 4][64];
+  uint32_t b[64];  // in[w - 1]
 };
 template <>
 struct zs_parse_win<0> {};
@@ -103,6 +104,7 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
   uint32_t* scr = scratch + (size_t)ZS_SEG_WORDS * (pos_base[s] / ZS_SEG + s);
   zs_block* blk = blocks + blk_base[s];
   const uint32_t nseg = (n + ZS_SEG - 1) / ZS_SEG;
+  const bool aligned = ((uintptr_t)src & 3u) == 0;
 
   zs_pstate t = {0, 0, ZS_MIN_MATCH - 1, 0};  // the true parse state entering the round (wave-uniform)
   uint32_t total = 0;     // symbols written (wave-uniform)
@@ -154,20 +156,46 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
         while (__ballot(st.p < b) != 0) {
           // stage: this lane's window [w, w + WIN) (entries past n are never read)
           const uint32_t w = st.p & ~3u;
-          uint32_t before = 0;  // in[w - 1]
           if (st.p < b) {
-            const uint4* g = reinterpret_cast<const uint4*>(M + w);
+            // every load is issued before the first is waited for: indices are
+            // clamped into the stream instead of branched around (entries past
+            // n are never read; the table's rows are 8-entry aligned, pos_base)
+            const uint4* g = reinterpret_cast<const uint4*>(M);
+            const uint32_t glast = ((n + 7u) >> 1) & ~3u;  // the stream's uint4s (two entries each)
+            uint4 mv[WIN / 2];
+            auto load_m = [&]() __attribute__((always_inline)) {
 #pragma unroll
-            for (uint32_t j = 0; j < WIN / 2; j++) W.m[j][lane] = w + 2 * j < n ? g[j] : make_uint4(0, 0, 0, 0);
+              for (uint32_t j = 0; j < WIN / 2; j++) mv[j] = g[min(w / 2 + j, glast - 1u)];
+            };
+            auto store_m = [&]() __attribute__((always_inline)) {
 #pragma unroll
-            for (uint32_t j = 0; j < WIN / 4; j++) W.s[j][lane] = zs_load_word(src, n, w + 4 * j);
-            before = w >= 4 ? zs_load_word(src, n, w - 4) >> 24 : 0u;
+              for (uint32_t j = 0; j < WIN / 2; j++) W.m[j][lane] = mv[j];
+            };
+            if (aligned) {  // aligned words holding at least one byte of the stream never leave its pages
+              load_m();
+              const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+              const uint32_t slast = (n - 1u) >> 2;
+              uint32_t sv[WIN / 4];
+#pragma unroll
+              for (uint32_t j = 0; j < WIN / 4; j++) sv[j] = s4[min(w / 4 + j, slast)];
+              const uint32_t bw = s4[w ? w / 4 - 1 : 0u] >> 24;
+              store_m();
+#pragma unroll
+              for (uint32_t j = 0; j < WIN / 4; j++) W.s[j][lane] = sv[j];
+              W.b[lane] = w ? bw : 0u;
+            } else {
+              load_m();
+#pragma unroll
+              for (uint32_t j = 0; j < WIN / 4; j++) W.s[j][lane] = zs_load_word(src, n, w + 4 * j);
+              W.b[lane] = w ? (uint32_t)src[w - 1] : 0u;
+              store_m();
+            }
           }
           while (st.p < b && st.p < w + WIN) {
             const uint32_t o = st.p - w, q = o - 1;  // in[p - 1] is staged byte o - 1 (o > 0)
             const uint2 e = reinterpret_cast<const uint2*>(&W.m[o >> 1][lane])[o & 1];
             const uint32_t lb = reinterpret_cast<const uint8_t*>(&W.s[(q >> 2) & (WIN / 4 - 1)][lane])[q & 3];
-            step(e, o == 0 ? before : lb);
+            step(e, o == 0 ? W.b[lane] : lb);
           }
         }
       }
