@@ -24,4 +24,8 @@ struct zs_dim3 {
 extern zs_dim3 threadIdx, blockIdx, blockDim;
 using std::max;
 using std::min;
+static inline uint32_t zs_host_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (s & 3u)));
+}
+#define __builtin_amdgcn_alignbyte(hi, lo, s) zs_host_alignbyte(hi, lo, s)
 typedef int hipError_t;

@@ -25,19 +25,24 @@ struct zs_lane_tabs {
 };
 
 struct zs_lane_reader {
-  const uint8_t* src;
+  const uint32_t* w4;  // the aligned words holding the member's bytes
+  uint32_t sh, last;   // the member's offset in its first word; index of the word holding its last byte
   uint32_t n, pos;  // bytes moved into hold so far
   uint64_t hold;
   uint32_t bits;
   uint32_t pf;      // input bytes [pos, pos + 4), loaded one refill ahead (zero past the end)
 };
 
+// input bytes [at, at + 4), zero past the end: two aligned word loads with
+// clamped indices and a funnel shift -- no branch, so the load stays in flight
+// until the refill that uses it (a branch per byte made the compiler wait on
+// each byte in turn)
 static __device__ __forceinline__ uint32_t zs_lr_load4(const zs_lane_reader& R, uint32_t at) {
-  uint32_t v = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++)
-    if (at + k < R.n) v |= (uint32_t)R.src[at + k] << (8 * k);
-  return v;
+  const uint32_t q = (at + R.sh) >> 2;
+  const uint32_t lo = R.w4[min(q, R.last)], hi = R.w4[min(q + 1u, R.last)];
+  const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, R.sh);
+  const uint32_t valid = at < R.n ? R.n - at : 0u;
+  return valid >= 4u ? v : v & ((1u << (8u * valid)) - 1u);
 }
 // bits < 32 -> bits >= 32: the prefetched word enters hold and the next one is
 // requested, so its latency overlaps the decoding of the bits just added
@@ -148,8 +153,14 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   zs_lane_tabs& T = tabs[s];
   zs_lane_lds& F = LL[threadIdx.x];
   zs_lane_reader R;
-  R.src = in + in_off[s];
-  R.n = in_len[s];
+  {
+    const uint8_t* src = in + in_off[s];
+    R.n = in_len[s];
+    R.sh = (uint32_t)((uintptr_t)src & 3u);
+    // an empty member reads (and masks off) a word of in_len[] instead: its own address may be past the buffer
+    R.w4 = R.n ? reinterpret_cast<const uint32_t*>(src - R.sh) : in_len;
+    R.last = R.n ? (R.sh + R.n - 1u) >> 2 : 0u;
+  }
   R.pos = 0;
   R.hold = 0;
   R.bits = 0;
