@@ -2,9 +2,11 @@
 // gzip wrappers (deflate.ts:155-159 update them in read_buf; the trailer is
 // written at deflate.ts:971-983).
 //
-// One wave per stream; lane i owns the i-th contiguous 1/64 of the stream.
+// One wave per stream; lane i owns the i-th contiguous 1/64 of the stream
+// (rounded up to 16 bytes), read 16 bytes at a time with the next 16 in flight.
 //   CRC-32 (common/crc32.ts:26-58): each lane computes the standard CRC of its
-//   segment from an LDS byte table; lane 0 then folds the 64 segment CRCs with
+//   segment, four bytes per step from slice-by-4 LDS tables (the same CRC as the
+//   reference's byte table, four table steps folded); lane 0 then folds the 64 segment CRCs with
 //   crc32_combine arithmetic (multiplication by x^(8*len) modulo the reflected
 //   polynomial 0xedb88320).
 //   Adler-32 (common/adler32.ts:4-25): A = 1 + sum x_j, B = n + sum (n-j) x_j
@@ -43,26 +45,75 @@ static __device__ uint32_t zs_x8nmodp(uint64_t len) {
   return p;
 }
 
+// Input bytes [i, i + 16) of the lane's segment as four words: five aligned
+// word loads (indices clamped to the word holding the stream's last byte, so
+// nothing outside the stream's pages is touched) and funnel shifts.
+struct zs_ck_src {
+  const uint32_t* w4;
+  uint32_t sh, last;
+};
+static __device__ __forceinline__ uint4 zs_ck_load16(const zs_ck_src& S, uint32_t i) {
+  const uint32_t q = (i + S.sh) >> 2;
+  uint32_t x[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) x[k] = S.w4[min(q + (uint32_t)k, S.last)];
+  return make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], S.sh), __builtin_amdgcn_alignbyte(x[2], x[1], S.sh),
+                    __builtin_amdgcn_alignbyte(x[3], x[2], S.sh), __builtin_amdgcn_alignbyte(x[4], x[3], S.sh));
+}
+static __device__ __forceinline__ uint32_t zs_ck_word(const uint4& d, uint32_t j) {
+  return j == 0 ? d.x : j == 1 ? d.y : j == 2 ? d.z : d.w;
+}
+
 __global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                     const uint32_t* __restrict__ in_len, uint32_t* __restrict__ check,
                                                     int kind, const uint32_t* __restrict__ seeds) {
-  __shared__ uint32_t T[256];
+  __shared__ uint32_t T[4][256];  // slice-by-4 tables: T[k][b] = CRC of byte b followed by k zero bytes
   __shared__ uint32_t seg_crc[64];
   const int s = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint32_t n = in_len[s];
   const uint8_t* src = in + in_off[s];
-  const uint32_t per = (n + 63) / 64;
+  // lane i owns bytes [i per, (i + 1) per), per a multiple of 16
+  const uint32_t per = (((n + 63) / 64) + 15u) & ~15u;
   const uint32_t b0 = min(n, lane * per), b1 = min(n, b0 + per);
+  zs_ck_src S;
+  S.sh = (uint32_t)((uintptr_t)src & 3u);
+  S.w4 = n ? reinterpret_cast<const uint32_t*>(src - S.sh) : in_len;  // an empty stream reads nothing it uses
+  S.last = n ? (S.sh + n - 1u) >> 2 : 0u;
   if (kind == 2) {
     for (uint32_t i = lane; i < 256; i += 64) {
       uint32_t c = i;
       for (int k = 0; k < 8; k++) c = (c & 1) ? 0xedb88320u ^ (c >> 1) : c >> 1;
-      T[i] = c;
+      T[0][i] = c;
+    }
+    __syncthreads();
+    for (uint32_t i = lane; i < 256; i += 64) {
+      uint32_t c = T[0][i];
+      for (int k = 1; k < 4; k++) {
+        c = (c >> 8) ^ T[0][c & 0xff];
+        T[k][i] = c;
+      }
     }
     __syncthreads();
     uint32_t c = 0xffffffffu;
-    for (uint32_t i = b0; i < b1; i++) c = (c >> 8) ^ T[(c ^ src[i]) & 0xff];
+    if (b0 < b1) {
+      uint4 d = zs_ck_load16(S, b0);
+      for (uint32_t i = b0; i < b1; i += 16) {
+        const uint4 cur = d;
+        if (i + 16 < b1) d = zs_ck_load16(S, i + 16);  // the next 16 bytes in flight
+        const uint32_t m = b1 - i;
+        if (m >= 16) {
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            c ^= zs_ck_word(cur, (uint32_t)j);
+            c = T[3][c & 0xff] ^ T[2][(c >> 8) & 0xff] ^ T[1][(c >> 16) & 0xff] ^ T[0][c >> 24];
+          }
+        } else {
+          for (uint32_t j = 0; j < m; j++)
+            c = (c >> 8) ^ T[0][(c ^ (zs_ck_word(cur, j >> 2) >> (8 * (j & 3)))) & 0xff];
+        }
+      }
+    }
     seg_crc[lane] = c ^ 0xffffffffu;
     __syncthreads();
     if (lane == 0) {
@@ -83,10 +134,20 @@ __global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ 
     }
   } else {
     uint64_t a = 0, w = 0;
-    for (uint32_t i = b0; i < b1; i++) {
-      a += src[i];
-      w += (uint64_t)(n - i) * src[i];
-      if (((i - b0) & 4095) == 4095) { a %= 65521; w %= 65521; }
+    if (b0 < b1) {
+      uint4 d = zs_ck_load16(S, b0);
+      uint32_t since = 0;
+      for (uint32_t i = b0; i < b1; i += 16) {
+        const uint4 cur = d;
+        if (i + 16 < b1) d = zs_ck_load16(S, i + 16);
+        const uint32_t m = min(16u, b1 - i);
+        for (uint32_t j = 0; j < m; j++) {
+          const uint32_t x = (zs_ck_word(cur, j >> 2) >> (8 * (j & 3))) & 0xffu;
+          a += x;
+          w += (uint64_t)(n - (i + j)) * x;
+        }
+        if (++since == 256) { a %= 65521; w %= 65521; since = 0; }  // 4 KiB between reductions
+      }
     }
     a %= 65521;
     w %= 65521;
