@@ -145,7 +145,9 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * "match_sweep" (default 1): levels 4..9, streams <= 65,537 B find matches by
  * a counting sort by hash + lock-step sweep (0: chain links + per-tile walk);
  * "parse_split" (default 0): levels 4..9 parse as per-range + per-stream
- * kernels (0: one wave per stream); "lane_block" (default 0 = by batch size;
+ * kernels (0: one wave per stream); "parse_win" (default 32; 16, or 0 for
+ * direct loads): match-table entries the one-wave parse stages per lane in
+ * LDS; "lane_block" (default 0 = by batch size;
  * else 1..64, a power of two): members per workgroup of the inflate lane path.
  * These options never change output bytes.  "inflate_ref_wrap" (default 1)
  * does: 1 reproduces the reference's inflate_fast window-wrap copy

@@ -53,8 +53,8 @@ static_assert(ZS_SEG == ZS_PARSE_SEG && ZS_SEG_WORDS == ZS_PARSE_SEG_WORDS, "scr
 // apart from its neighbours': conflict-free), bytes in[w + 4 j, +4) at s[j][l].
 // WIN = 32 (the default, 19 KiB of LDS: 8 workgroups per CU) halves the
 // stages of WIN = 16 (10 KiB: all 16 workgroups a CU gets at 4096 streams
-// fit) and measures faster: 2.10 vs 2.26 ms at 4096 streams, 3.2 ms with
-// direct loads (profiles/r02).
+// fit) and measures faster: 1.54 vs 1.77 ms at 4096 streams, 2.99 ms with
+// direct loads (WIN = 0); 0.40 / 0.42 / 0.54 ms at 512 (tools/ab_parse.sh).
 template <uint32_t WIN>
 struct zs_parse_win {
   uint4 m[WIN / 2][64];
