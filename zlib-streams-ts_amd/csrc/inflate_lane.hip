@@ -309,7 +309,25 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
       const uint8_t* from = dst + total - dist;
       uint8_t* to = dst + total;
-      if (dist >= 8) {  // 8 independent loads, then 8 stores: one memory round trip per 8 bytes
+      // A copy waits for its source bytes once per chunk (loads after the
+      // stores of the chunk before), so the chunk is as wide as the distance
+      // allows.  Source words are aligned loads funnel-shifted into place; a
+      // word that is read always holds at least one byte of the output region
+      // (so never leaves its pages), and only bytes below `to` are used.
+      const uint32_t fsh = (uint32_t)((uintptr_t)from & 3u);
+      const uint32_t* fw = reinterpret_cast<const uint32_t*>(from - fsh);
+      if (dist >= 16) {  // 16 bytes per round trip
+        for (uint32_t i = 0; i < len; i += 16) {
+          uint32_t x[5];
+#pragma unroll
+          for (int k = 0; k < 5; k++) x[k] = fw[(i >> 2) + (uint32_t)k];
+#pragma unroll
+          for (uint32_t j = 0; j < 16; j++) {
+            const uint32_t wd = __builtin_amdgcn_alignbyte(x[(j >> 2) + 1], x[j >> 2], fsh);
+            if (i + j < len) to[i + j] = (uint8_t)(wd >> (8 * (j & 3)));
+          }
+        }
+      } else if (dist >= 8) {  // 8 independent loads, then 8 stores: one memory round trip per 8 bytes
         for (uint32_t i = 0; i < len; i += 8) {
           uint8_t b[8];
 #pragma unroll
@@ -318,8 +336,18 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
           for (int k = 0; k < 8; k++)
             if (i + k < len) to[i + k] = b[k];
         }
-      } else {  // overlapping copy: the source is being written
-        for (uint32_t i = 0; i < len; i++) to[i] = from[i];
+      } else {
+        // overlapping copy, period dist < 8: the dist bytes before `to` are
+        // read once (three words, clamped to the last written one) and the
+        // run is stored from registers -- not a round trip per byte
+        const uint32_t last = (uint32_t)((to - 1) - (from - fsh)) >> 2;
+        const uint32_t x0 = fw[0], x1 = fw[min(1u, last)], x2 = fw[min(2u, last)];
+        const uint32_t p0 = __builtin_amdgcn_alignbyte(x1, x0, fsh), p1 = __builtin_amdgcn_alignbyte(x2, x1, fsh);
+        uint32_t j = 0;
+        for (uint32_t i = 0; i < len; i++) {
+          to[i] = (uint8_t)((j < 4 ? p0 >> (8 * j) : p1 >> (8 * (j - 4))) & 0xffu);
+          j = j + 1 == dist ? 0u : j + 1;
+        }
       }
       total += len;
     }
