@@ -260,3 +260,77 @@ def test_lane_path_decodes_clean_members(engine, fmt):
     for (s, c), (st, ph, msg, out, cons) in zip(keep, res):
         assert st == 1 and out == s
     assert engine.last_lane_count() == len(keep)
+
+
+def _decode_with(engine, items, fmt, caps, **opts):
+    try:
+        for k, v in opts.items():
+            engine.set_option(k, v)
+        return engine.decompress_batch_raw(items, fmt, out_caps=caps)
+    finally:
+        engine.set_option("inflate_wave_min", 32768)
+        engine.set_option("inflate_ref_wrap", 1)
+        engine.set_option("inflate_fast", 1)
+
+
+def test_wave_path_deflate64_fixtures(engine):
+    """Large members decode one per wave (inflate_wave.hip) beside the lane
+    kernel: the reference's deflate64 fixtures (>32 KiB distances, codes 30/31,
+    length 285) at every threshold -- all on the wave path (1), the default
+    split, none (0) -- against the reference's output hashes."""
+    names = sorted(os.listdir(os.path.join(golden_io.GOLDEN, "d64")))
+    data = [open(os.path.join(golden_io.GOLDEN, "d64", f), "rb").read() for f in names]
+    data.append(bytes.fromhex("4b1cfdff07a3e5030000"))  # test-inflate9-length-code-285.spec.ts:9-15
+    cases = {c["name"]: c for c, _ in golden_io.inflate_cases()}
+    caps = [3 << 20] * len(data)
+    for wmin in (1, 4096, 32768, 0):
+        res = _decode_with(engine, data, "deflate64-raw", caps, inflate_wave_min=wmin)
+        assert engine.last_lane_count() == len(data), wmin  # every member ended on a fast path
+        for k, (st, ph, msg, out, cons) in enumerate(res):
+            if k == len(names):
+                assert st == 1 and out == b"a" * 66539 and cons == len(data[k])
+            else:
+                c = cases["d64_" + names[k]]
+                assert st == 1 and corpus.sha256(out) == c["out_sha256"], (wmin, names[k])
+                assert cons == len(data[k])
+
+
+@pytest.mark.parametrize("fmt", ["deflate-raw", "deflate", "gzip"])
+def test_wave_path_large_members_zlib_semantics(engine, fmt):
+    """With the window-wrap reproduction off (inflate_ref_wrap=0), large members
+    of the three formats -- text, mixed, runs, incompressible (stored blocks),
+    fixed-Huffman -- decode on the wave path to their sources, and damaged ones
+    (flipped bit, truncation, short capacity) report exactly what the exact
+    state machine reports."""
+    rng = random.Random(11)
+    srcs = [corpus.make({"kind": k, "n": n, "seed": rng.randrange(1 << 32)})
+            for k, n in (("text", 262144), ("mixed", 1 << 20), ("zeros", 2 << 20), ("rand", 300000),
+                         ("ramp", 500000), ("text", 40000))]
+    comps = [oracle.compress(s, lvl, fmt)[1] for s, lvl in zip(srcs, (6, 6, 9, 6, 1, 6))]
+    comps.append(zlib_fixed(srcs[0], fmt))
+    srcs.append(srcs[0])
+    caps = [len(s) + 64 for s in srcs]
+    res = _decode_with(engine, comps, fmt, caps, inflate_ref_wrap=0, inflate_wave_min=1)
+    assert engine.last_lane_count() == len(comps)
+    for i, (s, (st, ph, msg, out, cons)) in enumerate(zip(srcs, res)):
+        assert st == 1 and out == s and cons == len(comps[i]), (fmt, i, st, msg)
+    bad = []
+    for c in comps[:3]:
+        flip = bytearray(c)
+        flip[len(c) // 2] ^= 0x10
+        bad += [bytes(flip), c[: len(c) * 2 // 3]]
+    bcaps = [len(srcs[0]) + 64, len(srcs[0]) + 64, len(srcs[1]) + 64, len(srcs[1]) + 64, 1 << 20, 1 << 20]
+    bad.append(comps[0])
+    bcaps.append(len(srcs[0]) // 2)  # output capacity too small
+    wave = _decode_with(engine, bad, fmt, bcaps, inflate_ref_wrap=0, inflate_wave_min=1)
+    exact = _decode_with(engine, bad, fmt, bcaps, inflate_ref_wrap=0, inflate_fast=0)
+    for i, (a, b) in enumerate(zip(wave, exact)):
+        assert a == b, (fmt, i, a[:3], b[:3], len(a[3]), len(b[3]), a[4], b[4])
+
+
+def zlib_fixed(data, fmt):
+    """A fixed-Huffman stream of `data` (Python's zlib with Z_FIXED): block type 1 at size."""
+    import zlib
+    wb = {"deflate-raw": -15, "deflate": 15, "gzip": 31}[fmt]
+    co = zlib.compressobj(6, zlib.DEFLATED, wb, 8, zlib.Z_FIXED)
+    return co.compress(data) + co.flush()

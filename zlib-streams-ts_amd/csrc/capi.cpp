@@ -91,6 +91,11 @@ struct zs_ctx {
   bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)
   int parse_win = 32;        // L4..9 parse: match-table entries staged per lane in LDS (32, 16; 0: direct loads)
   int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
+  uint32_t inflate_wave_min = 32768;  // members with more input bytes decode one per wave (inflate_wave.hip); 0: never
+  hipStream_t side = nullptr;         // second stream: the wave-per-member kernel runs beside the lane kernel
+  hipEvent_t fork = nullptr, join = nullptr;
+  Buf wlist;
+  std::vector<uint32_t> hwlist;
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res, d_pack;
   HostBuf h_in, h_out;
@@ -165,6 +170,12 @@ int zs_ctx_create(int device, zs_ctx** out) {
     delete c;
     return fail(ZS_MEM_ERROR, "%s", hipGetErrorString(e));
   }
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) {
+    zs_ctx_destroy(c);
+    return fail(ZS_MEM_ERROR, "%s", "cannot create the side stream");
+  }
   // the chain builder relies on lane-ordered LDS atomics: check before any use
   uint64_t bad = 0;
   const int st = zs_selftest(c, &bad);
@@ -203,10 +214,14 @@ void zs_ctx_destroy(zs_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (Buf* b : {&c->lstat, &c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
-                 &c->istate, &c->d_in, &c->d_out, &c->d_res, &c->d_pack})
+                 &c->istate, &c->d_in, &c->d_out, &c->d_res, &c->d_pack, &c->wlist})
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&c->h_in, &c->h_out})
     if (b->p) (void)hipHostFree(b->p);
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->fork) (void)hipEventDestroy(c->fork);
+  if (c->join) (void)hipEventDestroy(c->join);
+  if (c->side) (void)hipStreamDestroy(c->side);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -228,6 +243,9 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
     if (value != 0 && (value < 1 || value > 64 || (value & (value - 1))))
       return fail(ZS_STREAM_ERROR, "lane_block must be 0 or a power of two <= 64");
     c->lane_block = value;
+  } else if (!strcmp(name, "inflate_wave_min")) {
+    if (value < 0) return fail(ZS_STREAM_ERROR, "inflate_wave_min must be >= 0");
+    c->inflate_wave_min = (uint32_t)value;
   } else return fail(ZS_STREAM_ERROR, "unknown option %s", name);
   return ZS_OK;
 }
@@ -812,9 +830,35 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
     while (B > 1 && B * zs_inflate_lane_lds_bytes() > 160u * 1024u) B >>= 1;  // one CU's LDS
     const size_t lsm = B * zs_inflate_lane_lds_bytes();
     HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate_lane, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm));
+    // Large members (more than inflate_wave_min input bytes) decode one per wave
+    // on the side stream, beside the lane kernel: one lane would take the
+    // batch's whole time on such a member.  Only where the lane path's
+    // straight-through decode is the reference's (deflate64, or no window-wrap
+    // reproduction); the lane kernel skips exactly these members.
+    uint32_t wave_min = 0;
+    c->hwlist.clear();
+    if (c->inflate_wave_min && (wbits == -16 || !c->inflate_ref_wrap)) {
+      for (uint32_t i = 0; i < n; i++)
+        if (in_len[i] > c->inflate_wave_min) c->hwlist.push_back(i);
+      if (!c->hwlist.empty()) wave_min = c->inflate_wave_min;
+    }
+    if (wave_min) {
+      const uint32_t nw = (uint32_t)c->hwlist.size();
+      HIPCHK(c->wlist.ensure(4ull * nw));
+      HIPCHK(hipMemcpyAsync(c->wlist.p, c->hwlist.data(), 4ull * nw, hipMemcpyHostToDevice, st));
+      HIPCHK(hipEventRecord(c->fork, st));
+      HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
+      const size_t wsm = zs_inflate_wave_lds_bytes();
+      HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wsm));
+      zs_k_inflate_wave<<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
+                                                  c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(c->join, c->side));
+    }
     zs_k_inflate_lane<<<(n + B - 1) / B, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
                                                     (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
-                                                    c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0);
+                                                    c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min);
+    if (wave_min) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
     MARK("inflate_lane");
     if (wbits > 0) {  // trailer checks over the decoded bytes: adler32 (zlib) / crc32 (gzip)
       uint32_t* chk = c->llen.as<uint32_t>() + n;

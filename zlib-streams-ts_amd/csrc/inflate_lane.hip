@@ -146,10 +146,12 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
                                                         const uint64_t* __restrict__ out_off,
                                                         const uint32_t* __restrict__ out_cap, int wbits, uint32_t n_members,
                                                         zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
-                                                        uint32_t* __restrict__ lens_out, int flags) {
+                                                        uint32_t* __restrict__ lens_out, int flags,
+                                                        uint32_t wave_min) {
   extern __shared__ zs_lane_lds LL[];  // blockDim.x entries
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_members) return;
+  if (wave_min && in_len[s] > wave_min) return;  // a large member: zs_k_inflate_wave decodes it (inflate_wave.hip)
   zs_lane_tabs& T = tabs[s];
   zs_lane_lds& F = LL[threadIdx.x];
   zs_lane_reader R;
