@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
     uint8_t* ob8 = (uint8_t*)ob.data();
     const size_t obn = ob.size() * sizeof(uint4);
     for (size_t k = 0; k < obn; k++) ob8[k] = 0xa5;  // guard pattern around the member's output
-    zs_k_inflate_lane(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags);
+    zs_k_inflate_lane(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u);
     for (size_t k = 0; k < obn; k++)
       if ((k < ooff || k >= ooff + cap) && ob8[k] != 0xa5) {
         fprintf(stderr, "lane_host: member %u wrote byte %zu outside [%lu, %lu)\n", i, k, (unsigned long)ooff,
