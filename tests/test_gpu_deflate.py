@@ -158,6 +158,62 @@ def test_c2_full_batch_matches_reference_goldens(engine):
     assert sum(len(o) for _, o in res) == 91855591
 
 
+@pytest.mark.parametrize("level", [1, 2, 3])
+def test_group_fast_parser_equals_serial_replay(engine, level):
+    """zs_k_fast (group-speculative, default) against zs_k_fast_serial (step by step): same bytes on
+    streams that slide several times, all-zero and random streams, and sizes around the group and
+    slide boundaries; both also against the oracle on the short ones."""
+    specs = [("text", 262144), ("mixed", 200000), ("rand", 40000), ("zeros", 100000), ("ramp", 70000),
+             ("text", 0), ("text", 1), ("text", 3), ("text", 4), ("text", 59), ("text", 64), ("text", 259),
+             ("text", 32769), ("text", 65535), ("text", 65536), ("text", 65537), ("zeros", 65537),
+             ("text", 98304 + 300), ("mixed", 131072 + 17)]
+    inputs = [corpus.make({"kind": k, "n": n, "seed": 9300 + i}) for i, (k, n) in enumerate(specs)]
+    b = bytearray(corpus.rand(78, 90000))  # a candidate at exactly MAX_DIST
+    b[40000:40020] = b[40000 - 32506:40000 - 32506 + 20]
+    inputs.append(bytes(b))
+    try:
+        engine.set_option("fast_group", 0)
+        ref = engine.compress_batch_raw(inputs, "deflate-raw", level)
+        engine.set_option("fast_group", 1)
+        res = engine.compress_batch_raw(inputs, "deflate-raw", level)
+    finally:
+        engine.set_option("fast_group", 1)
+    bad = [i for i in range(len(inputs)) if res[i] != ref[i]]
+    assert not bad, [(specs[i] if i < len(specs) else "dist", len(res[i][1]), len(ref[i][1])) for i in bad]
+    for d, (st, out) in zip(inputs, res):
+        if len(d) <= 65536:
+            assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1]
+
+
+@pytest.mark.parametrize("chunks", [2, 3, 7])
+def test_chunked_pipeline_matches_goldens(engine, chunks):
+    """The batch pipelined as K chunks over two HIP streams (option chunks) gives the same bytes:
+    the small goldens of every level/format (mixed sizes, so chunks are ragged) and 1,000 C2 streams."""
+    import zsamd
+
+    engine.set_option("chunks", chunks)
+    try:
+        test_small_goldens(engine)
+        recs = golden_io.batch("t64_l6_raw")
+        buf = bytes(zsamd.corpus("text", 0, 1000, 65536))
+        inputs = [buf[i * 65536:(i + 1) * 65536] for i in range(1000)]
+        # a mixed batch: the 64 KiB streams interleaved with short and empty ones
+        mixed = []
+        for i, d in enumerate(inputs):
+            mixed.append(d)
+            if i % 97 == 0:
+                mixed.append(d[: i % 5000])
+        res = engine.compress_batch_raw(mixed, "deflate-raw", 6)
+        engine.set_option("chunks", 1)
+        ref = engine.compress_batch_raw(mixed, "deflate-raw", 6)
+        assert res == ref
+        full = [out for d, (st, out) in zip(mixed, res) if len(d) == 65536]
+        bad = [i for i, out in enumerate(full) if (len(out), hashlib.sha256(out).digest()[:16]) != recs[i]]
+        assert not bad, bad[:10]
+    finally:
+        engine.set_option("chunks", 0)
+
+
 @pytest.mark.slow
 def test_c5_gzip_batch_matches_reference_goldens(engine):
     import zsamd

@@ -91,6 +91,8 @@ struct zs_ctx {
   bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)
   int parse_win = 32;        // L4..9 parse: match-table entries staged per lane in LDS (32, 16; 0: direct loads)
   int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
+  bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
+  int chunks = 0;             // deflate: chunks of the batch pipelined over two streams (0: chosen from the batch)
   uint32_t inflate_wave_min = 32768;  // members with more input bytes decode one per wave (inflate_wave.hip); 0: never
   hipStream_t side = nullptr;         // second stream: the wave-per-member kernel runs beside the lane kernel
   hipEvent_t fork = nullptr, join = nullptr;
@@ -102,7 +104,12 @@ struct zs_ctx {
   std::vector<uint8_t> hmeta;
   size_t last_n = 0;
   // timing
-  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  struct Mark {
+    std::string name;
+    hipEvent_t ev;
+    hipStream_t st;
+  };
+  std::vector<Mark> marks;  // a phase = the time between consecutive marks on the same stream
   std::vector<std::pair<std::string, double>> phase_ms;
   double total_ms = -1;
 };
@@ -122,7 +129,7 @@ static int mark(zs_ctx* c, hipStream_t st, const char* name) {
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return ZS_OK;
   (void)hipEventRecord(e, st);
-  c->marks.emplace_back(name, e);
+  c->marks.push_back({name, e, st});
   return ZS_OK;
 }
 #define MARK(name)                              \
@@ -135,20 +142,23 @@ static void collect_marks(zs_ctx* c) {
   c->phase_ms.clear();
   c->total_ms = -1;
   if (c->marks.size() < 2) {
-    for (auto& m : c->marks) (void)hipEventDestroy(m.second);
+    for (auto& m : c->marks) (void)hipEventDestroy(m.ev);
     c->marks.clear();
     return;
   }
-  (void)hipEventSynchronize(c->marks.back().second);
+  (void)hipEventSynchronize(c->marks.back().ev);
   for (size_t i = 1; i < c->marks.size(); i++) {
+    size_t j = i;  // the previous mark on the same stream
+    while (j-- > 0 && c->marks[j].st != c->marks[i].st) {}
+    if (j == (size_t)-1) continue;
     float ms = 0;
-    (void)hipEventElapsedTime(&ms, c->marks[i - 1].second, c->marks[i].second);
-    c->phase_ms.emplace_back(c->marks[i].first, ms);
+    (void)hipEventElapsedTime(&ms, c->marks[j].ev, c->marks[i].ev);
+    c->phase_ms.emplace_back(c->marks[i].name, ms);
   }
   float tot = 0;
-  (void)hipEventElapsedTime(&tot, c->marks.front().second, c->marks.back().second);
+  (void)hipEventElapsedTime(&tot, c->marks.front().ev, c->marks.back().ev);
   c->total_ms = tot;
-  for (auto& m : c->marks) (void)hipEventDestroy(m.second);
+  for (auto& m : c->marks) (void)hipEventDestroy(m.ev);
   c->marks.clear();
 }
 
@@ -236,6 +246,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "parse_split")) c->parse_split = value != 0;
+  else if (!strcmp(name, "fast_group")) c->fast_group = value != 0;
   else if (!strcmp(name, "parse_win")) {
     if (value != 0 && value != 16 && value != 32) return fail(ZS_STREAM_ERROR, "parse_win must be 0, 16 or 32");
     c->parse_win = value;
@@ -243,6 +254,9 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
     if (value != 0 && (value < 1 || value > 64 || (value & (value - 1))))
       return fail(ZS_STREAM_ERROR, "lane_block must be 0 or a power of two <= 64");
     c->lane_block = value;
+  } else if (!strcmp(name, "chunks")) {
+    if (value < 0 || value > 64) return fail(ZS_STREAM_ERROR, "chunks must be in 0..64");
+    c->chunks = value;
   } else if (!strcmp(name, "inflate_wave_min")) {
     if (value < 0) return fail(ZS_STREAM_ERROR, "inflate_wave_min must be >= 0");
     c->inflate_wave_min = (uint32_t)value;
@@ -340,6 +354,87 @@ static int deflate_stored_batch(zs_ctx* c, int wrap, uint32_t n, const uint8_t* 
   return ZS_OK;
 }
 
+// Chunks a deflate batch of n streams is pipelined in (option chunks = 0).
+static uint32_t auto_chunks(uint32_t n, int level) {
+  (void)n;
+  (void)level;
+  return 1;
+}
+
+// One chunk of a deflate batch (streams [a, a + n) of the caller's batch, every
+// per-stream array already offset to a): the whole kernel sequence on stream st.
+static int deflate_chunk(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
+                         uint32_t max_len, uint32_t max_blk, const uint8_t* d_in, const uint64_t* d_in_off,
+                         const uint32_t* d_in_len, uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                         const uint64_t* d_pos, const uint32_t* d_blk, const uint32_t* d_rng, zs_stream* d_st,
+                         uint32_t* syms, uint32_t* pscr, uint32_t* check, int32_t* d_status, uint32_t* d_out_len) {
+  zs_block* d_bk = c->blocks.as<zs_block>();
+  const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
+  MARK("start");
+  if (wrap) {
+    zs_k_checksum<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, check, wrap == 1 ? 1 : 2);
+    zs_k_copy_check<<<nblocks_s, nthreads_s, 0, st>>>(check, d_st, (int)n);
+    MARK("checksum");
+  }
+  if (level >= 4) {
+    const dim3 g((max_len + 8191) / 8192, n);
+    if (c->match_sweep) {
+      // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
+      // longer ones: chain links + per-tile chain walk (deflate_match.hip)
+      zs_k_bucket<<<n, 256, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
+      if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+      MARK("bucket");
+      zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
+                                     cfg.chain, cfg.nice);
+      if (max_len > 65537u)
+        zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
+                                       cfg.chain, cfg.nice, 65537u);
+      MARK("sweep");
+    } else {
+      // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
+      zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+      if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+      MARK("prev");
+      if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
+                                                   c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
+      MARK("match");
+    }
+    if (c->parse_split) {
+      // the lazy parse: per-range speculative parse + merges, then per-stream joins and splice (deflate_parse.hip)
+      if (max_len)
+        zs_k_parse_a<<<dim3((max_len + ZS_PARSE_RANGE - 1) / ZS_PARSE_RANGE, n), 64, 0, st>>>(
+            d_in, d_in_off, d_in_len, d_pos, d_rng, c->mres.as<uint2>(), pscr, cfg.good, cfg.lazy);
+      zs_k_parse_b<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, d_rng, c->mres.as<uint2>(),
+                                     syms, d_bk, d_st, pscr, cfg.good, cfg.lazy);
+    } else {
+      auto parse = c->parse_win == 32 ? zs_k_parse : c->parse_win == 16 ? zs_k_parse16 : zs_k_parse_direct;
+      parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(),
+                              syms, d_bk, d_st, pscr, cfg.good, cfg.lazy);
+    }
+    MARK("parse");
+  } else {
+    const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
+    // levels 1..3: the group-speculative replay (default) or the step-by-step one (fast_group = 0)
+    auto fast = c->fast_group ? zs_k_fast : zs_k_fast_serial;
+    HIPCHK(hipFuncSetAttribute((const void*)fast, hipFuncAttributeMaxDynamicSharedMemorySize, fast_smem));
+    fast<<<n, 64, fast_smem, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, syms, d_bk, d_st,
+                                        cfg.chain, cfg.lazy, cfg.nice);
+    MARK("fast");
+  }
+  zs_k_trees<<<dim3(max_blk, n), 64, 0, st>>>(d_in, d_in_off, d_pos, d_blk, syms, d_bk, d_st,
+                                              c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), (int)n);
+  MARK("trees");
+  zs_k_layout<<<nblocks_s, nthreads_s, 0, st>>>(d_blk, d_bk, d_st, d_out_cap, d_out, d_out_off, wrap, (int)n);
+  MARK("layout");
+  zs_k_emit<<<dim3(max_blk, n), 256, 0, st>>>(d_in, d_in_off, d_pos, d_blk, syms, d_bk, d_st,
+                                              c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), d_out, d_out_off, wrap);
+  MARK("emit");
+  if (wrap) zs_k_wrap<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_out, d_out_off, d_in_len, wrap, level, (int)n);
+  zs_k_finish<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_status, d_out_len, (int)n);
+  MARK("finish");
+  return ZS_OK;
+}
+
 extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* d_in,
                                        const uint64_t* in_off, const uint32_t* in_len, uint8_t* d_out,
                                        const uint64_t* out_off, const uint32_t* out_cap, int32_t* d_status,
@@ -405,70 +500,39 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   const uint32_t* d_blk = (const uint32_t*)(dm + ml.blk_base);
   const uint32_t* d_rng = (const uint32_t*)(dm + ml.range_base);
   zs_stream* d_st = c->streams.as<zs_stream>();
-  zs_block* d_bk = c->blocks.as<zs_block>();
   const zs_level_cfg cfg = kLevels[level];
-  const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
-
-  MARK("start");
-  if (wrap) {
-    zs_k_checksum<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, c->check.as<uint32_t>(), wrap == 1 ? 1 : 2);
-    zs_k_copy_check<<<nblocks_s, nthreads_s, 0, st>>>(c->check.as<uint32_t>(), d_st, (int)n);
-    MARK("checksum");
+  // The batch runs as K contiguous chunks of streams, alternating between the
+  // context's two HIP streams: chunk j+1's match finding (which fills the chip)
+  // runs while chunk j's parse, trees and emit (one wave per stream or block,
+  // latency-bound) finish.  Every kernel indexes its workspace through the
+  // per-stream bases, so a chunk is the same launch sequence over offset
+  // per-stream arrays.
+  uint32_t K = c->chunks ? (uint32_t)c->chunks : auto_chunks(n, level);
+  K = std::max(1u, std::min(K, n));
+  if (K > 1) {  // the side stream starts after the caller's prior work and the metadata upload
+    HIPCHK(hipEventRecord(c->fork, st));
+    HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
   }
-  if (level >= 4) {
-    const dim3 g((max_len + 8191) / 8192, n);
-    if (c->match_sweep) {
-      // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
-      // longer ones: chain links + per-tile chain walk (deflate_match.hip)
-      zs_k_bucket<<<n, 256, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
-      if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
-      MARK("bucket");
-      zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
-                                     cfg.chain, cfg.nice);
-      if (max_len > 65537u)
-        zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
-                                       cfg.chain, cfg.nice, 65537u);
-      MARK("sweep");
-    } else {
-      // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
-      zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
-      if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
-      MARK("prev");
-      if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
-                                                   c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
-      MARK("match");
+  for (uint32_t j = 0; j < K; j++) {
+    const uint32_t a = (uint32_t)((uint64_t)n * j / K), e = (uint32_t)((uint64_t)n * (j + 1) / K);
+    uint32_t cmax_len = 0, cmax_blk = 0;
+    for (uint32_t i = a; i < e; i++) {
+      cmax_len = std::max(cmax_len, in_len[i]);
+      cmax_blk = std::max(cmax_blk, in_len[i] / ZS_SYM_END + 2);
     }
-    if (c->parse_split) {
-      // the lazy parse: per-range speculative parse + merges, then per-stream joins and splice (deflate_parse.hip)
-      if (max_len)
-        zs_k_parse_a<<<dim3((max_len + ZS_PARSE_RANGE - 1) / ZS_PARSE_RANGE, n), 64, 0, st>>>(
-            d_in, d_in_off, d_in_len, d_pos, d_rng, c->mres.as<uint2>(), c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
-      zs_k_parse_b<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, d_rng, c->mres.as<uint2>(),
-                                     c->syms.as<uint32_t>(), d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
-    } else {
-      auto parse = c->parse_win == 32 ? zs_k_parse : c->parse_win == 16 ? zs_k_parse16 : zs_k_parse_direct;
-      parse<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(),
-                              c->syms.as<uint32_t>(), d_bk, d_st, c->pscr.as<uint32_t>(), cfg.good, cfg.lazy);
-    }
-    MARK("parse");
-  } else {
-    const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
-    HIPCHK(hipFuncSetAttribute((const void*)zs_k_fast, hipFuncAttributeMaxDynamicSharedMemorySize, fast_smem));
-    zs_k_fast<<<n, 64, fast_smem, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
-                                        cfg.chain, cfg.lazy, cfg.nice);
-    MARK("fast");
+    hipStream_t X = (j & 1) ? c->side : st;
+    const int r = deflate_chunk(c, X, level, wrap, cfg, e - a, cmax_len, cmax_blk, d_in, d_in_off + a, d_in_len + a,
+                                d_out, d_out_off + a, d_out_cap + a, d_pos + a, d_blk + a, d_rng + a, d_st + a,
+                                c->syms.as<uint32_t>() + a,
+                                c->pscr.as<uint32_t>() + (c->parse_split ? 0 : (size_t)ZS_PARSE_SEG_WORDS * a),
+                                c->check.as<uint32_t>() + a, d_status + a, d_out_len + a);
+    if (r != ZS_OK) return r;
   }
-  zs_k_trees<<<dim3(max_blk, n), 64, 0, st>>>(d_in, d_in_off, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
-                                              c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), (int)n);
-  MARK("trees");
-  zs_k_layout<<<nblocks_s, nthreads_s, 0, st>>>(d_blk, d_bk, d_st, d_out_cap, d_out, d_out_off, wrap, (int)n);
-  MARK("layout");
-  zs_k_emit<<<dim3(max_blk, n), 256, 0, st>>>(d_in, d_in_off, d_pos, d_blk, c->syms.as<uint32_t>(), d_bk, d_st,
-                                              c->codes.as<uint32_t>(), c->hdr.as<uint32_t>(), d_out, d_out_off, wrap);
-  MARK("emit");
-  if (wrap) zs_k_wrap<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_out, d_out_off, d_in_len, wrap, level, (int)n);
-  zs_k_finish<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_status, d_out_len, (int)n);
-  MARK("finish");
+  if (K > 1) {
+    HIPCHK(hipEventRecord(c->join, c->side));
+    HIPCHK(hipStreamWaitEvent(st, c->join, 0));
+  }
+  MARK("end");
   HIPCHK(hipGetLastError());
   collect_marks(c);
   return ZS_OK;

@@ -1,6 +1,12 @@
 // deflate_fast.hip -- the greedy parser of levels 1..3 (deflate_fast,
 // deflate.ts:1281-1350) on gfx950.
 //
+// Two kernels.  zs_k_fast_serial (below) is the first design: one wave replays
+// the reference step by step.  zs_k_fast (at the end of the file, the default)
+// replays it a group of 64 positions at a time from speculative per-lane chain
+// walks; option fast_group = 0 selects the serial one.
+//
+// zs_k_fast_serial:
 // Unlike levels 4..9, deflate_fast does not insert the positions inside a
 // match longer than max_lazy (deflate.ts:1310-1322), so its hash chains depend
 // on the parse and cannot be precomputed per position.  One
@@ -25,7 +31,7 @@ struct zs_fast_lds {
   uint32_t ring[8192];  // input byte x (x < 256 c) at byte (x & 32767)
 };
 
-__global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+__global__ __launch_bounds__(64) void zs_k_fast_serial(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                 const uint32_t* __restrict__ in_len,
                                                 const uint64_t* __restrict__ pos_base,
                                                 const uint32_t* __restrict__ blk_base, uint32_t* __restrict__ syms,
@@ -191,6 +197,281 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
   }
   close_block(n, 1);
   drain();
+  if (lane == 0) {
+    streams[s].nsym = nsym;
+    streams[s].nblk = nflush;
+  }
+}
+
+// ---------------------------------------------------------------- zs_k_fast
+// The group-speculative replay (CPU model: tools/emu/emu_fast_group.c,
+// tests/test_emu_fast.py).  One wave per stream keeps the reference's exact
+// window-relative head[] / prev[] (u16, LDS, slid on the reference schedule)
+// and works on groups of 64 consecutive positions [g0, g0 + 64), lane i
+// holding position g0 + i:
+//   1. every lane inserts its position speculatively -- the superset of what
+//      deflate_fast inserts, which skips the inside of matches longer than
+//      max_lazy (deflate.ts:1310-1322) -- through one lane-ordered
+//      ds_mskor_rtn_b32 on its head[] half-word (gfx950 applies same-address
+//      LDS atomics of one instruction in lane order; zs_selftest checks it):
+//      each lane gets its superset chain's first link; the first lane of each
+//      hash then puts the original head back;
+//   2. every lane walks its superset chain (budget, MAX_DIST limit and nice
+//      as longest_match, deflate.ts:1053-1115; lengths compared 4 bytes at a
+//      time up to nice) and records which in-group positions it visited;
+//   3. the serial parse replays the group from the lane results with scalar
+//      control flow: a step's result is exact iff every in-group position its
+//      walk met was truly inserted (the true chain is the superset chain minus
+//      the skipped positions); the ~3 % of steps whose walk met a skipped one
+//      re-walk the true chain (in-group links from ballots over the truly
+//      inserted lanes), and a result at nice is extended to its exact length;
+//   4. the truly inserted positions enter head[] / prev[] in lane order (one
+//      more exchange).
+// Steps start below g0 + 58 (the inside of a short match, <= max_lazy <= 6,
+// stays inside the group) and below the position at which fill_window's next
+// slide is due (deflate.ts:180-190), so a group never straddles a slide.
+// The input sits in a 32 KiB LDS ring holding [E - 32768, E) with
+// g0 + 160 <= E <= g0 + 262: every candidate (distance <= MAX_DIST) and every
+// scan byte up to g0 + 122 + 32; 256-byte chunks are prefetched in registers
+// one chunk ahead and appended 64 bytes at a time.
+#define ZS_FG_STEPS 58u
+
+struct zs_fastg_lds {
+  uint32_t head[16384];   // u16 head[h] at half (h & 1) of word h >> 1
+  uint16_t prev[32768];
+  uint32_t ring[8192];    // input byte x at byte (x & 32767)
+};
+
+typedef __attribute__((address_space(3))) uint32_t zs_fg_lds_u32;
+static __device__ __forceinline__ uint32_t zs_fg_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const zs_fg_lds_u32*)p;
+}
+static __device__ __forceinline__ uint32_t zs_fg_mskor(uint32_t addr, uint32_t mask, uint32_t val) {
+  uint32_t old;
+  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(old)
+               : "v"(addr), "v"(mask), "v"(val)
+               : "memory");
+  return old;
+}
+
+__global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                const uint32_t* __restrict__ in_len,
+                                                const uint64_t* __restrict__ pos_base,
+                                                const uint32_t* __restrict__ blk_base, uint32_t* __restrict__ syms,
+                                                zs_block* __restrict__ blocks, zs_stream* __restrict__ streams,
+                                                int chain, int lazy, int nice_cfg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t zs_fastg_smem[];
+  zs_fastg_lds& L = *reinterpret_cast<zs_fastg_lds*>(zs_fastg_smem);
+  const int s = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = in_len[s];
+  const uint8_t* src = in + in_off[s];
+  uint32_t* sy = syms + pos_base[s] + s;
+  zs_block* blk = blocks + blk_base[s];
+  for (uint32_t i = lane; i < 16384; i += 64) { L.head[i] = 0; reinterpret_cast<uint32_t*>(L.prev)[i] = 0; }
+  const uint8_t* ringb = reinterpret_cast<const uint8_t*>(L.ring);
+  auto rword = [&](uint32_t x) -> uint32_t {  // input bytes [x, x + 4) from the ring
+    const uint32_t w = x >> 2;
+    return __builtin_amdgcn_alignbyte(L.ring[(w + 1) & 8191u], L.ring[w & 8191u], x & 3u);
+  };
+
+  // ring fill: E = end of the ring's bytes; pf = bytes [P, P + 256) (4 per lane), nx = [P + 256, P + 512) in flight
+  uint32_t E = 0, P = 0;
+  uint32_t pf = zs_load_word(src, n, 4 * lane), nx = zs_load_word(src, n, 256 + 4 * lane);
+  auto fill_to = [&](uint32_t want) {
+    while (E < want) {
+      if ((lane >> 4) == ((E - P) >> 6)) L.ring[((P >> 2) + lane) & 8191u] = pf;
+      E += 64;
+      if (E == P + 256) {
+        P += 256;
+        pf = nx;
+        nx = zs_load_word(src, n, P + 256 + 4 * lane);
+      }
+    }
+  };
+
+  uint32_t base = 0, p = 0;
+  uint32_t nsym = 0, in_blk = 0, nflush = 0, blk_start = 0;
+  uint32_t sbuf = 0;
+  auto emit = [&](uint32_t v) {
+    sbuf = lane == (nsym & 63u) ? v : sbuf;
+    nsym++;
+    in_blk++;
+    if ((nsym & 63u) == 0) sy[nsym - 64 + lane] = sbuf;
+  };
+  auto close_block = [&](uint32_t end, uint32_t last) {
+    if (lane == 0) {
+      zs_block b;
+      b.sym_start = nsym - in_blk;
+      b.sym_count = in_blk;
+      b.in_start = blk_start;
+      b.in_end = end;
+      b.type = 0; b.hdr_bits = 0; b.data_bits = 0; b.pad = 0; b.bit_off = 0; b.bit_end = 0;
+      b.last = last | (blk_start < base ? 2u : 0u);
+      blk[nflush] = b;
+    }
+    nflush++;
+    in_blk = 0;
+    blk_start = end;
+  };
+  // exact match length at scan position a (wave-uniform) against candidate c < a, capped at maxc:
+  // 64 bytes per ballot, the first 64 from the ring, further ones from memory
+  auto exact_len = [&](uint32_t a, uint32_t c, uint32_t maxc) -> uint32_t {
+    uint32_t k = 0;
+    uint64_t neq = __ballot(ringb[(a + lane) & 32767u] != ringb[(c + lane) & 32767u] || lane >= maxc);
+    while (neq == 0 && k + 64 < maxc) {
+      k += 64;
+      const uint32_t sb = a + k + lane < n ? src[a + k + lane] : 0x100u;
+      const uint32_t mb = c + k + lane < n ? src[c + k + lane] : 0x1ffu;
+      neq = __ballot(mb != sb || k + lane >= maxc);
+    }
+    k += neq ? (uint32_t)__builtin_ctzll(neq) : 64u;
+    return k < maxc ? k : maxc;
+  };
+
+  while (p < n) {
+    // fill_window slide (deflate.ts:180-190), same schedule as deflate_slow
+    const uint32_t m = min(n, base + 65536u);
+    if (p - base >= ZS_SLIDE_AT && m - p < ZS_MIN_LOOKAHEAD) {
+      for (uint32_t i = lane; i < 16384; i += 64) {
+        const uint32_t a = L.head[i];
+        const uint32_t b = reinterpret_cast<uint32_t*>(L.prev)[i];
+        const uint32_t a0 = a & 0xffffu, a1 = a >> 16, b0 = b & 0xffffu, b1 = b >> 16;
+        L.head[i] = (a0 >= 32768u ? a0 - 32768u : 0u) | ((a1 >= 32768u ? a1 - 32768u : 0u) << 16);
+        reinterpret_cast<uint32_t*>(L.prev)[i] = (b0 >= 32768u ? b0 - 32768u : 0u) |
+                                                 ((b1 >= 32768u ? b1 - 32768u : 0u) << 16);
+      }
+      base += 32768u;
+      continue;  // re-evaluate the group bounds against the new base
+    }
+    const uint32_t g0 = p, rg0 = g0 - base;
+    uint32_t tslide = base + ZS_SLIDE_AT;
+    if (m >= ZS_MIN_LOOKAHEAD - 1 && m - (ZS_MIN_LOOKAHEAD - 1) > tslide) tslide = m - (ZS_MIN_LOOKAHEAD - 1);
+    const uint32_t g1 = min(min(g0 + ZS_FG_STEPS, tslide), n);
+    fill_to(g0 + 160u);
+
+    // ---- 1. speculative insertion of every lane's position
+    const uint32_t q = g0 + lane;
+    const bool ok = q + 2 < n;  // INSERT_STRING needs lookahead >= MIN_MATCH (deflate.ts:1296)
+    const uint32_t hw = rword(q);
+    const uint32_t h = (((hw & 0xffu) << 10) ^ (((hw >> 8) & 0xffu) << 5) ^ ((hw >> 16) & 0xffu)) & ZS_HASH_MASK;
+    const uint32_t ha = zs_fg_addr(&L.head[h >> 1]), sh = 16u * (h & 1u);
+    const uint32_t hm = ok ? 0xffffu << sh : 0u;
+    const uint32_t sp = (zs_fg_mskor(ha, hm, ok ? (rg0 + lane) << sh : 0u) >> sh) & 0xffffu;
+    const bool spin = sp != 0u && sp >= rg0;  // the link is an earlier lane of the group
+    // the first lane of each hash restores the original head, which every lane then reads
+    (void)zs_fg_mskor(ha, ok && !spin ? hm : 0u, ok && !spin ? sp << sh : 0u);
+    const uint32_t orig = ok ? (L.head[h >> 1] >> sh) & 0xffffu : 0u;
+
+    // ---- 2. superset-chain walks, lengths up to nice (4 bytes per compare)
+    const uint32_t look = n - q;  // wraps for lanes past the end; they are inactive
+    const uint32_t srel = q - base;
+    const uint32_t maxc = min(look, ZS_MAX_MATCH), nice = min(look, (uint32_t)nice_cfg);
+    const uint32_t capn = min(nice, maxc);
+    const uint32_t limit = srel > ZS_MAX_DIST ? srel - ZS_MAX_DIST : 0u;
+    bool act = ok && q < g1 && sp != 0u && srel - sp <= ZS_MAX_DIST;
+    uint32_t best = ZS_MIN_MATCH - 1, bms = 0, cur = sp;
+    uint64_t vis = 0;
+    uint32_t sw[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) sw[j] = rword(q + 4 * j);
+    for (int t = 0; t < chain; t++) {
+      if (__ballot(act) == 0) break;
+      const bool cin = cur != 0u && cur >= rg0;
+      uint32_t nxt = 0;
+      if (act) {
+        if (cin) vis |= 1ull << (cur - rg0);
+        const uint32_t c = base + cur;
+        uint32_t len = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          if (len == 4u * j && len < capn) {
+            const uint32_t x = rword(c + 4 * j) ^ sw[j];
+            len += x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
+          }
+        }
+        len = min(len, capn);
+        if (len > best) {
+          best = len;
+          bms = cur;
+          if (len >= nice) act = false;
+        }
+        nxt = L.prev[cur & 0x7fffu];
+      }
+      // an in-group link is the speculative link of that lane (read by every lane)
+      const uint32_t lsp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((cur - rg0) & 63u) * 4u), (int)sp);
+      nxt = cin ? lsp : nxt;
+      cur = nxt;
+      act = act && cur > limit;
+    }
+
+    // ---- 3. serial replay of the group (wave-uniform)
+    const uint64_t okm = __ballot(ok);
+    const uint32_t vlo = (uint32_t)vis, vhi = (uint32_t)(vis >> 32);
+    uint64_t tm = 0;  // truly inserted lanes
+    while (p < g1) {
+      const uint32_t i = p - g0;
+      const uint32_t lk = n - p, sr = p - base;
+      tm |= okm & (1ull << i);
+      const uint64_t vi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vhi, (int)i) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)vlo, (int)i);
+      uint32_t ml = 0, ms = 0;
+      const uint32_t mx = min(lk, ZS_MAX_MATCH), nc = min(lk, (uint32_t)nice_cfg);
+      if ((vi & ~tm) == 0) {
+        ml = (uint32_t)__builtin_amdgcn_readlane((int)best, (int)i);
+        ms = (uint32_t)__builtin_amdgcn_readlane((int)bms, (int)i);
+        if (ml < ZS_MIN_MATCH) ml = 0;
+        else if (ml >= nc) ml = exact_len(p, base + ms, mx);
+      } else {
+        // re-walk the true chain: in-group links through the truly inserted lanes of the same hash
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)h, (int)i);
+        auto true_link = [&](uint32_t l, uint32_t hl) -> uint32_t {
+          const uint64_t c = __ballot(h == hl) & tm & ((1ull << l) - 1ull);
+          return c ? rg0 + 63u - (uint32_t)__builtin_clzll(c) : (uint32_t)__builtin_amdgcn_readlane((int)orig, (int)l);
+        };
+        const uint32_t hh = true_link(i, hi);
+        if (hh != 0u && sr - hh <= ZS_MAX_DIST) {
+          const uint32_t lim = sr > ZS_MAX_DIST ? sr - ZS_MAX_DIST : 0u;
+          uint32_t cl = (uint32_t)chain, b2 = ZS_MIN_MATCH - 1, c = hh;
+          do {
+            const uint32_t len = exact_len(p, base + c, mx);
+            if (len > b2) {
+              ms = c;
+              b2 = len;
+              if (len >= nc) break;
+            }
+            if (c != 0u && c >= rg0) {
+              const uint32_t l = c - rg0;
+              c = true_link(l, (uint32_t)__builtin_amdgcn_readlane((int)h, (int)l));
+            } else {
+              c = L.prev[c & 0x7fffu];
+            }
+          } while (c > lim && --cl != 0);
+          ml = b2 >= ZS_MIN_MATCH ? b2 : 0u;
+        }
+      }
+      if (ml >= ZS_MIN_MATCH) {
+        emit(0x80000000u | ((ml - ZS_MIN_MATCH) << 16) | (sr - ms));
+        const uint32_t after = p + ml;
+        if (ml <= (uint32_t)lazy && n - after >= ZS_MIN_MATCH)  // insert inside short matches
+          tm |= ((1ull << (after - g0)) - 1ull) & ~((2ull << i) - 1ull);
+        p = after;
+      } else {
+        emit((uint32_t)ringb[p & 32767u]);
+        p++;
+      }
+      if (in_blk == ZS_SYM_END) close_block(p, 0);
+    }
+
+    // ---- 4. the truly inserted positions enter head[] / prev[] in lane order
+    const bool ins = (tm >> lane) & 1ull;
+    const uint32_t tp = (zs_fg_mskor(ha, ins ? hm : 0u, ins ? (rg0 + lane) << sh : 0u) >> sh) & 0xffffu;
+    if (ins) L.prev[(rg0 + lane) & 0x7fffu] = (uint16_t)tp;
+  }
+  close_block(n, 1);
+  const uint32_t k = nsym & 63u;
+  if (lane < k) sy[nsym - k + lane] = sbuf;
   if (lane == 0) {
     streams[s].nsym = nsym;
     streams[s].nblk = nflush;
