@@ -415,7 +415,7 @@ static int deflate_chunk(zs_ctx* c, hipStream_t st, int level, int wrap, const z
   } else {
     const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
     // levels 1..3: the group-speculative replay (default) or the step-by-step one (fast_group = 0)
-    auto fast = c->fast_group ? zs_k_fast : zs_k_fast_serial;
+    auto fast = !c->fast_group ? zs_k_fast_serial : cfg.nice <= 8 ? zs_k_fast<2> : cfg.nice <= 16 ? zs_k_fast<4> : zs_k_fast<8>;
     HIPCHK(hipFuncSetAttribute((const void*)fast, hipFuncAttributeMaxDynamicSharedMemorySize, fast_smem));
     fast<<<n, 64, fast_smem, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, syms, d_bk, d_st,
                                         cfg.chain, cfg.lazy, cfg.nice);

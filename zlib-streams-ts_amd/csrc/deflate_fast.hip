@@ -22,6 +22,7 @@
 // bytes, the literals), the next-but-one chunk's load in flight as the parse
 // enters a chunk.  head + prev + ring fill the CU's 160 KiB of LDS.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "zs_common.h"
 #include "zs_kernels.h"
 
@@ -235,6 +236,7 @@ __global__ __launch_bounds__(64) void zs_k_fast_serial(const uint8_t* __restrict
 // scan byte up to g0 + 122 + 32; 256-byte chunks are prefetched in registers
 // one chunk ahead and appended 64 bytes at a time.
 #define ZS_FG_STEPS 58u
+#define ZS_FG_LONG 0xffffu  // a lane result longer than nice + 32: extended by the serial replay
 
 struct zs_fastg_lds {
   uint32_t head[16384];   // u16 head[h] at half (h & 1) of word h >> 1
@@ -255,6 +257,7 @@ static __device__ __forceinline__ uint32_t zs_fg_mskor(uint32_t addr, uint32_t m
   return old;
 }
 
+template <int NW>  // words compared per walk candidate: nice / 4 (2 / 4 / 8 at levels 1 / 2 / 3)
 __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                 const uint32_t* __restrict__ in_len,
                                                 const uint64_t* __restrict__ pos_base,
@@ -293,13 +296,20 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
 
   uint32_t base = 0, p = 0;
   uint32_t nsym = 0, in_blk = 0, nflush = 0, blk_start = 0;
-  uint32_t sbuf = 0;
-  auto emit = [&](uint32_t v) {
-    sbuf = lane == (nsym & 63u) ? v : sbuf;
-    nsym++;
-    in_blk++;
-    if ((nsym & 63u) == 0) sy[nsym - 64 + lane] = sbuf;
-  };
+#ifdef ZS_FG_PROF
+  unsigned long long fg_acc[5] = {0, 0, 0, 0, 0}, fg_last = __builtin_readcyclecounter();
+  uint32_t fg_rw = 0, fg_lg = 0;
+#define FG_T(k)                                              \
+  do {                                                       \
+    const unsigned long long t_ = __builtin_readcyclecounter(); \
+    fg_acc[k] += t_ - fg_last;                               \
+    fg_last = t_;                                            \
+  } while (0)
+#define FG_C(v) (v)++
+#else
+#define FG_T(k) do {} while (0)
+#define FG_C(v) do {} while (0)
+#endif
   auto close_block = [&](uint32_t end, uint32_t last) {
     if (lane == 0) {
       zs_block b;
@@ -345,6 +355,7 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
       base += 32768u;
       continue;  // re-evaluate the group bounds against the new base
     }
+    FG_T(0);
     const uint32_t g0 = p, rg0 = g0 - base;
     uint32_t tslide = base + ZS_SLIDE_AT;
     if (m >= ZS_MIN_LOOKAHEAD - 1 && m - (ZS_MIN_LOOKAHEAD - 1) > tslide) tslide = m - (ZS_MIN_LOOKAHEAD - 1);
@@ -364,67 +375,156 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
     (void)zs_fg_mskor(ha, ok && !spin ? hm : 0u, ok && !spin ? sp << sh : 0u);
     const uint32_t orig = ok ? (L.head[h >> 1] >> sh) & 0xffffu : 0u;
 
-    // ---- 2. superset-chain walks, lengths up to nice (4 bytes per compare)
+    FG_T(1);
+    // ---- 2. superset-chain walks, lengths up to nice: nw = nice / 4 words per candidate, all
+    //         loaded before the first compare (2 / 4 / 8 at levels 1 / 2 / 3)
     const uint32_t look = n - q;  // wraps for lanes past the end; they are inactive
     const uint32_t srel = q - base;
-    const uint32_t maxc = min(look, ZS_MAX_MATCH), nice = min(look, (uint32_t)nice_cfg);
+    const uint32_t maxc = min(look, (uint32_t)ZS_MAX_MATCH), nice = min(look, (uint32_t)nice_cfg);
     const uint32_t capn = min(nice, maxc);
     const uint32_t limit = srel > ZS_MAX_DIST ? srel - ZS_MAX_DIST : 0u;
     bool act = ok && q < g1 && sp != 0u && srel - sp <= ZS_MAX_DIST;
     uint32_t best = ZS_MIN_MATCH - 1, bms = 0, cur = sp;
     uint64_t vis = 0;
-    uint32_t sw[8];
+    uint32_t sw[NW];
+    {
+      uint32_t A[NW + 1];
 #pragma unroll
-    for (int j = 0; j < 8; j++) sw[j] = rword(q + 4 * j);
+      for (int j = 0; j <= NW; j++) A[j] = L.ring[((q >> 2) + j) & 8191u];
+#pragma unroll
+      for (int j = 0; j < NW; j++) sw[j] = __builtin_amdgcn_alignbyte(A[j + 1], A[j], q & 3u);
+    }
+    // first differing byte of the W words at scan S and candidate c, 4 W if none (all loads issued first)
+    auto diff_at = [&](uint32_t c, const uint32_t* S, auto Wc) -> uint32_t {
+      constexpr int W = decltype(Wc)::value;
+      uint32_t A[W + 1];
+#pragma unroll
+      for (int j = 0; j <= W; j++) A[j] = L.ring[((c >> 2) + j) & 8191u];
+      uint32_t len = 4u * W;
+#pragma unroll
+      for (int j = W - 1; j >= 0; j--) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(A[j + 1], A[j], c & 3u) ^ S[j];
+        len = x ? 4u * j + ((uint32_t)__builtin_ctz(x) >> 3) : len;
+      }
+      return len;
+    };
+    using NWc = std::integral_constant<int, NW>;
     for (int t = 0; t < chain; t++) {
       if (__ballot(act) == 0) break;
+      // straight-line: the link, the candidate's words and the in-group link issue together
       const bool cin = cur != 0u && cur >= rg0;
-      uint32_t nxt = 0;
-      if (act) {
-        if (cin) vis |= 1ull << (cur - rg0);
-        const uint32_t c = base + cur;
-        uint32_t len = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          if (len == 4u * j && len < capn) {
-            const uint32_t x = rword(c + 4 * j) ^ sw[j];
-            len += x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
-          }
-        }
-        len = min(len, capn);
-        if (len > best) {
-          best = len;
-          bms = cur;
-          if (len >= nice) act = false;
-        }
-        nxt = L.prev[cur & 0x7fffu];
-      }
-      // an in-group link is the speculative link of that lane (read by every lane)
+      const uint32_t pl = L.prev[cur & 0x7fffu];
       const uint32_t lsp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((cur - rg0) & 63u) * 4u), (int)sp);
-      nxt = cin ? lsp : nxt;
-      cur = nxt;
+      const uint32_t len = min(diff_at(base + cur, sw, NWc{}), capn);
+      vis |= act && cin ? 1ull << ((cur - rg0) & 63u) : 0ull;
+      const bool better = act && len > best;
+      best = better ? len : best;
+      bms = better ? cur : bms;
+      act = act && !(better && len >= nice);
+      cur = cin ? lsp : pl;
       act = act && cur > limit;
     }
+    // a result at nice: its exact length from 32 more bytes per lane; ZS_FG_LONG if they all match too
+    if (best >= nice && best >= ZS_MIN_MATCH && nice < maxc) {
+      const uint32_t o = 4u * NW;
+      uint32_t S2[8], A2[9];
+#pragma unroll
+      for (int j = 0; j < 9; j++) A2[j] = L.ring[(((q + o) >> 2) + j) & 8191u];
+#pragma unroll
+      for (int j = 0; j < 8; j++) S2[j] = __builtin_amdgcn_alignbyte(A2[j + 1], A2[j], (q + o) & 3u);
+      const uint32_t e = o + diff_at(base + bms + o, S2, std::integral_constant<int, 8>{});
+      best = e >= maxc ? maxc : (e < o + 32u ? e : ZS_FG_LONG);
+    }
 
-    // ---- 3. serial replay of the group (wave-uniform)
-    const uint64_t okm = __ballot(ok);
+    FG_T(2);
+    // ---- 3. replay of the group.  Each lane's step is precomputed: its symbol, the lane after
+    //         it, and what it inserts (its own position, the inside of a short match).  A scalar
+    //         loop chases the next-lane links to the group's end; then, in parallel, the path's
+    //         insertions give each step's truly inserted set (a step only sees positions below
+    //         it, all decided by earlier steps), and the first step whose walk met a position the
+    //         path skipped -- or whose match needs more than nice + 32 bytes compared -- is found
+    //         by one ballot.  The steps before it are exact and stored in one go (rank = earlier
+    //         steps); it runs the slow path, and the chase resumes after it.
+    const bool isM = best >= ZS_MIN_MATCH;
+    const uint32_t sym = isM ? 0x80000000u | ((best - ZS_MIN_MATCH) << 16) | (srel - bms) : (hw & 0xffu);
+    const uint32_t shortc = isM && best != ZS_FG_LONG && best <= (uint32_t)lazy && n - (q + best) >= ZS_MIN_MATCH
+                                ? best - 1u : 0u;
+    const uint32_t pk = min(lane + (isM ? best : 1u), 511u) | (ok ? 512u : 0u) | (shortc << 10) |
+                        (best == ZS_FG_LONG ? 0x4000u : 0u);
     const uint32_t vlo = (uint32_t)vis, vhi = (uint32_t)(vis >> 32);
+    const uint64_t okm = __ballot(ok);
     uint64_t tm = 0;  // truly inserted lanes
-    while (p < g1) {
-      const uint32_t i = p - g0;
+    const uint32_t j1 = g1 - g0;
+    const uint32_t nextv = pk & 511u, shc = (pk >> 10) & 15u;
+    auto put = [&](uint32_t v) {  // one symbol of a slow step
+      if (lane == 0) sy[nsym] = v;
+      nsym++;
+      in_blk++;
+    };
+    auto flush = [&](uint64_t path) {  // store the path's symbols in order; close a block on its 16383rd
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(path);
+      if (cnt == 0) return;
+      const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(path >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)path, 0u));
+      if ((path >> lane) & 1ull) sy[nsym + rk] = sym;
+      if (in_blk + cnt >= ZS_SYM_END) {
+        const uint32_t k = ZS_SYM_END - in_blk;  // symbols up to and including the cut
+        uint64_t m = path;
+        for (uint32_t t = 1; t < k; t++) m &= m - 1;
+        const uint32_t c = (uint32_t)__builtin_ctzll(m);
+        nsym += k;
+        in_blk += k;
+        close_block(g0 + (uint32_t)__builtin_amdgcn_readlane((int)nextv, (int)c), 0);
+        nsym += cnt - k;
+        in_blk += cnt - k;
+      } else {
+        nsym += cnt;
+        in_blk += cnt;
+      }
+    };
+    uint32_t j = p - g0;
+    while (j < j1) {
+      // chase the lane results' next-lane links (scalar)
+      uint64_t path = 0;
+      uint32_t jj = j;
+      while (jj < j1) {
+        path |= 1ull << jj;
+        jj = (uint32_t)__builtin_amdgcn_readlane((int)nextv, (int)jj);
+      }
+      // in parallel: what the path inserts (its own positions, the inside of its short matches),
+      // then the first step whose walk met a position the path skips (or that needs the slow extension)
+      const bool onp = (path >> lane) & 1ull;
+      const uint64_t le = path & (lane == 63u ? ~0ull : (2ull << lane) - 1ull);
+      const uint32_t owner = le ? 63u - (uint32_t)__builtin_clzll(le) : 0u;
+      const uint32_t osc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(owner * 4u), (int)shc);
+      const bool inside = !onp && le != 0 && lane - owner <= osc;
+      const uint64_t tmn = tm | __ballot((onp && ok) || inside);
+      const uint64_t bad = __ballot(onp && ((best == ZS_FG_LONG) || (vis & ~tmn) != 0));
+      if (bad == 0) {
+        flush(path);
+        tm = tmn;
+        j = jj;
+        break;
+      }
+      const uint32_t f = (uint32_t)__builtin_ctzll(bad);
+      const uint64_t below = (1ull << f) - 1ull;
+      flush(path & below);
+      tm = tmn & below;
+      // slow step at lane f
+      const uint32_t i = f;
+      p = g0 + i;
       const uint32_t lk = n - p, sr = p - base;
       tm |= okm & (1ull << i);
       const uint64_t vi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vhi, (int)i) << 32) |
                           (uint32_t)__builtin_amdgcn_readlane((int)vlo, (int)i);
       uint32_t ml = 0, ms = 0;
-      const uint32_t mx = min(lk, ZS_MAX_MATCH), nc = min(lk, (uint32_t)nice_cfg);
+      const uint32_t mx = min(lk, (uint32_t)ZS_MAX_MATCH), nc = min(lk, (uint32_t)nice_cfg);
       if ((vi & ~tm) == 0) {
-        ml = (uint32_t)__builtin_amdgcn_readlane((int)best, (int)i);
+        FG_C(fg_lg);
         ms = (uint32_t)__builtin_amdgcn_readlane((int)bms, (int)i);
-        if (ml < ZS_MIN_MATCH) ml = 0;
-        else if (ml >= nc) ml = exact_len(p, base + ms, mx);
+        ml = exact_len(p, base + ms, mx);
       } else {
         // re-walk the true chain: in-group links through the truly inserted lanes of the same hash
+        FG_C(fg_rw);
         const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)h, (int)i);
         auto true_link = [&](uint32_t l, uint32_t hl) -> uint32_t {
           const uint64_t c = __ballot(h == hl) & tm & ((1ull << l) - 1ull);
@@ -452,28 +552,41 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
         }
       }
       if (ml >= ZS_MIN_MATCH) {
-        emit(0x80000000u | ((ml - ZS_MIN_MATCH) << 16) | (sr - ms));
+        put(0x80000000u | ((ml - ZS_MIN_MATCH) << 16) | (sr - ms));
         const uint32_t after = p + ml;
         if (ml <= (uint32_t)lazy && n - after >= ZS_MIN_MATCH)  // insert inside short matches
           tm |= ((1ull << (after - g0)) - 1ull) & ~((2ull << i) - 1ull);
-        p = after;
+        j = after - g0;
       } else {
-        emit((uint32_t)ringb[p & 32767u]);
-        p++;
+        put((uint32_t)__builtin_amdgcn_readlane((int)hw, (int)i) & 0xffu);
+        j = i + 1;
       }
-      if (in_blk == ZS_SYM_END) close_block(p, 0);
+      if (in_blk == ZS_SYM_END) close_block(g0 + j, 0);
     }
+    p = g0 + j;
 
+    FG_T(3);
     // ---- 4. the truly inserted positions enter head[] / prev[] in lane order
     const bool ins = (tm >> lane) & 1ull;
     const uint32_t tp = (zs_fg_mskor(ha, ins ? hm : 0u, ins ? (rg0 + lane) << sh : 0u) >> sh) & 0xffffu;
     if (ins) L.prev[(rg0 + lane) & 0x7fffu] = (uint16_t)tp;
+    FG_T(4);
   }
+#ifdef ZS_FG_PROF
+  if (lane == 0 && s < 4)
+    printf("fgprof s=%d n=%u t1=%llu t2=%llu t3=%llu t4=%llu t0=%llu rw=%u lg=%u\n", s, n, fg_acc[1], fg_acc[2], fg_acc[3],
+           fg_acc[4], fg_acc[0], fg_rw, fg_lg);
+#endif
   close_block(n, 1);
-  const uint32_t k = nsym & 63u;
-  if (lane < k) sy[nsym - k + lane] = sbuf;
   if (lane == 0) {
     streams[s].nsym = nsym;
     streams[s].nblk = nflush;
   }
 }
+
+template __global__ void zs_k_fast<2>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+                                      uint32_t*, zs_block*, zs_stream*, int, int, int);
+template __global__ void zs_k_fast<4>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+                                      uint32_t*, zs_block*, zs_stream*, int, int, int);
+template __global__ void zs_k_fast<8>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+                                      uint32_t*, zs_block*, zs_stream*, int, int, int);

@@ -61,6 +61,7 @@ __global__ void zs_k_parse_a(const uint8_t* in, const uint64_t* in_off, const ui
 __global__ void zs_k_parse_b(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                              const uint32_t* blk_base, const uint32_t* range_base, const uint2* mres, uint32_t* syms,
                              zs_block* blocks, zs_stream* streams, uint32_t* scratch, int good, int lazy);
+template <int NW>
 __global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,
                           int lazy, int nice);
