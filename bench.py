@@ -133,7 +133,8 @@ def profiled_traffic(kernel, kernel_ms):
     within 10 % (i.e. it profiled this build); otherwise (None, reason)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")), key=os.path.getmtime)
-    for f in reversed(files):
+    stale = None
+    for f in reversed(files):  # newest first; the first whose duration matches this run (same build and config)
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
@@ -143,9 +144,10 @@ def profiled_traffic(kernel, kernel_ms):
         prof_ms = e["avg_ns"] / 1e6
         src = os.path.relpath(f, ROOT)
         if abs(prof_ms - kernel_ms) > 0.1 * kernel_ms:
-            return None, "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
+            stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
+            continue
         return int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms)
-    return None, "no committed profile for %s" % kernel
+    return None, stale or "no committed profile for %s" % kernel
 
 
 def profiled_ceilings(kernel, kernel_ms):
@@ -159,7 +161,8 @@ def profiled_ceilings(kernel, kernel_ms):
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_summary*.json")) +
                    glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")), key=os.path.getmtime)
-    for f in reversed(files):
+    stale = None
+    for f in reversed(files):  # newest first; the first whose duration matches this run
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
@@ -169,12 +172,13 @@ def profiled_ceilings(kernel, kernel_ms):
         src = os.path.relpath(f, ROOT)
         prof_ms = e["avg_ns"] / 1e6
         if abs(prof_ms - kernel_ms) > 0.15 * kernel_ms:
-            return {"source": "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)}
+            stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
+            continue
         out = {k: e[k] for k in ("lds_bank_conflict_frac", "valu_busy", "active_frac_of_wave_cycles",
                                  "wait_frac_of_wave_cycles", "wait_inst_frac_of_wave_cycles") if k in e}
         out["source"] = "%s (%s avg %.3f ms under --pmc)" % (src, kernel, prof_ms)
         return out
-    return {"source": "no committed SQ summary for %s" % kernel}
+    return {"source": stale or "no committed SQ summary for %s" % kernel}
 
 
 def timed_port(fn, items, seconds, threads):

@@ -10,7 +10,7 @@ ratios that bound an integer/LDS kernel:
                            (disjoint; they sum to ~1)
 
 usage: python tools/sq_summary.py DIR [kernel-substring] [--json OUT.json]"""
-import collections, csv, glob, json, os, sys
+import collections, csv, glob, json, os, re, sys
 
 args = [a for a in sys.argv[1:]]
 out_json = None
@@ -25,7 +25,7 @@ dur = collections.defaultdict(list)
 for f in sorted(glob.glob(os.path.join(d, "sq*", "run_counter_collection.csv"))):
     seen = set()
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        k = re.sub(r"<[^>]*>", "", r["Kernel_Name"].split("(")[0].replace("void ", ""))
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         if (f, r["Dispatch_Id"]) not in seen:
             seen.add((f, r["Dispatch_Id"]))

@@ -3,12 +3,17 @@ per kernel: calls, average duration (kernel trace), FETCH_SIZE / WRITE_SIZE
 (KiB per dispatch as rocprofv3 reports them) and the HBM bytes per launch.
 gfx950 FETCH_SIZE counts half of the bytes of wide coalesced reads
 (MI355X_MICROARCH.md, HBM): hbm_bytes_corrected doubles the read side."""
-import collections, csv, json, os, sys
+import collections, csv, json, os, re, sys
+
+
+def kname(name):  # "void zs_k_fast<2>(...)" -> "zs_k_fast"
+    return re.sub(r"<[^>]*>", "", name.split("(")[0].replace("void ", "")).strip()
+
 
 src, dst = sys.argv[1], sys.argv[2]
 stats = {}
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
-    stats[r["Name"].split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+    stats[kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                        "total_ns": float(r["TotalDurationNs"])}
 cnt = collections.defaultdict(lambda: collections.defaultdict(list))
 for kind in ("fetch", "write"):
@@ -16,7 +21,7 @@ for kind in ("fetch", "write"):
     if not os.path.exists(p):
         continue
     for r in csv.DictReader(open(p)):
-        cnt[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        cnt[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
 for k, v in stats.items():
     e = dict(v)
