@@ -132,7 +132,7 @@ def profiled_traffic(kernel, kernel_ms):
     profile's average kernel duration agrees with this run's HIP-event time
     within 10 % (i.e. it profiled this build); otherwise (None, reason)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")))  # round directories sort in order
     stale = None
     for f in reversed(files):  # newest first; the first whose duration matches this run (same build and config)
         try:
@@ -160,7 +160,7 @@ def profiled_ceilings(kernel, kernel_ms):
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_summary*.json")) +
-                   glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")), key=os.path.getmtime)
+                   glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")))
     stale = None
     for f in reversed(files):  # newest first; the first whose duration matches this run
         try:

@@ -148,8 +148,14 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * kernels (0: one wave per stream); "parse_win" (default 32; 16, or 0 for
  * direct loads): match-table entries the one-wave parse stages per lane in
  * LDS; "lane_block" (default 0 = by batch size;
- * else 1..64, a power of two): members per workgroup of the inflate lane path.
- * These options never change output bytes.  "inflate_ref_wrap" (default 1)
+ * else 1..64, a power of two): members per workgroup of the inflate lane path;
+ * "inflate_wave_min" (default 32768; 0 = never): members with more input bytes
+ * decode one per wave (inflate_wave.hip) beside the lane kernel;
+ * "fast_group" (default 1): levels 1..3 replay deflate_fast a group of 64
+ * positions at a time from speculative per-lane chain walks (0: step by step);
+ * "chunks" (default 0 = chosen from the batch, 1 today; else 1..64): deflate
+ * batches run as that many contiguous chunks of streams pipelined over two
+ * HIP streams.  These options never change output bytes.  "inflate_ref_wrap" (default 1)
  * does: 1 reproduces the reference's inflate_fast window-wrap copy
  * (inffast.ts:133-147), which changes the output of members whose match
  * crosses the reference's window wrap between inflate() calls; 0 decodes with
