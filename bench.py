@@ -493,7 +493,7 @@ def main_inflate(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        for ph in ("inflate_lane", "inflate_check", "inflate", "finish"):
+        for ph in ("inflate_lane", "inflate_wave", "inflate_join", "inflate_check", "inflate", "finish"):
             v = eng.last_ms(ph)
             if v >= 0:
                 phases[ph] = phases.get(ph, 0.0) + v
@@ -525,6 +525,11 @@ def main_inflate(args):
         dom = max(phase_avg, key=phase_avg.get)
         k_ms = phase_avg[dom]
         alg = in_local + out_local  # compressed_in + uncompressed_out per member
+        if dom == "inflate_wave":  # the wave kernel decodes only the members with more input than inflate_wave_min
+            opts = dict(o.split("=", 1) for o in args.option)
+            wmin = int(opts.get("inflate_wave_min", 32768))
+            olen = d_len.cpu().tolist()
+            alg = sum(len(m) + olen[i] for i, m in enumerate(members) if len(m) > wmin)
         achieved = alg / (k_ms / 1e3) / 1e9
         traffic, tsrc = profiled_traffic("zs_k_" + dom, k_ms)
         cpu = None

@@ -386,10 +386,12 @@ static int deflate_chunk(zs_ctx* c, hipStream_t st, int level, int wrap, const z
       MARK("bucket");
       zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
                                      cfg.chain, cfg.nice);
-      if (max_len > 65537u)
+      MARK("sweep");
+      if (max_len > 65537u) {
         zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
                                        cfg.chain, cfg.nice, 65537u);
-      MARK("sweep");
+        MARK("match");
+      }
     } else {
       // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
       zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
@@ -914,16 +916,21 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
       HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
       const size_t wsm = zs_inflate_wave_lds_bytes();
       HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wsm));
+      if (int r = mark(c, c->side, "start")) return r;
       zs_k_inflate_wave<<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
                                                   c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
       HIPCHK(hipGetLastError());
+      if (int r = mark(c, c->side, "inflate_wave")) return r;
       HIPCHK(hipEventRecord(c->join, c->side));
     }
     zs_k_inflate_lane<<<(n + B - 1) / B, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
                                                     (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
                                                     c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min);
-    if (wave_min) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
     MARK("inflate_lane");
+    if (wave_min) {
+      HIPCHK(hipStreamWaitEvent(st, c->join, 0));
+      MARK("inflate_join");  // the caller's stream waiting for the wave kernel beyond the lane kernel
+    }
     if (wbits > 0) {  // trailer checks over the decoded bytes: adler32 (zlib) / crc32 (gzip)
       uint32_t* chk = c->llen.as<uint32_t>() + n;
       zs_k_checksum<<<n, 64, 0, st>>>(d_out, d_ooff, c->llen.as<uint32_t>(), chk, wbits == 31 ? 2 : 1);
