@@ -185,6 +185,37 @@ def test_group_fast_parser_equals_serial_replay(engine, level):
             assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1]
 
 
+@pytest.mark.parametrize("level", [4, 6, 9])
+def test_two_wave_parse_equals_one_wave_parse(engine, level):
+    """zs_k_parse_2w (two waves per stream, 512-position segments; the default below 2048 streams) against
+    zs_k_parse (one wave, 1 KiB segments): same bytes on 64 KiB, 256 KiB (slides, several super-rounds) and
+    ragged streams, and the C2 goldens of 1,000 streams with two waves forced."""
+    import zsamd
+
+    specs = [("text", 65536), ("mixed", 65536), ("text", 262144), ("mixed", 200000 + 13), ("zeros", 131072),
+             ("rand", 40000), ("text", 32768), ("text", 32769), ("text", 511), ("text", 512), ("text", 513),
+             ("text", 0), ("text", 5), ("text", 98304 + 300)]
+    inputs = [corpus.make({"kind": k, "n": n, "seed": 9500 + i}) for i, (k, n) in enumerate(specs)]
+    outs = []
+    try:
+        for w in (1, 2):
+            engine.set_option("parse_waves", w)
+            outs.append(engine.compress_batch_raw(inputs, "deflate-raw", level))
+        assert outs[0] == outs[1]
+        if level == 6:
+            recs = golden_io.batch("t64_l6_raw")
+            buf = bytes(zsamd.corpus("text", 0, 1000, 65536))
+            res = engine.compress_batch_raw([buf[i * 65536:(i + 1) * 65536] for i in range(1000)], "deflate-raw", 6)
+            bad = [i for i, (st, out) in enumerate(res)
+                   if st != 1 or (len(out), hashlib.sha256(out).digest()[:16]) != recs[i]]
+            assert not bad, bad[:10]
+    finally:
+        engine.set_option("parse_waves", 0)
+    for d, (st, out) in zip(inputs, outs[1]):
+        if len(d) <= 65536:
+            assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1]
+
+
 @pytest.mark.parametrize("chunks", [2, 3, 7])
 def test_chunked_pipeline_matches_goldens(engine, chunks):
     """The batch pipelined as K chunks over two HIP streams (option chunks) gives the same bytes:

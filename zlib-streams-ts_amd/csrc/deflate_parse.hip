@@ -36,13 +36,31 @@
 #include "zs_kernels.h"
 #include "zs_parse.h"
 
-#define ZS_SEG 1024u                        // positions per speculative segment
-#define ZS_SPEC_SLOTS 1284u                 // >= ZS_SEG + MAX_MATCH - 1 symbols
-#define ZS_SYNC_SLOTS 1028u                 // >= ZS_SEG sync points + sentinel
-#define ZS_FIX_SLOTS 1284u
-#define ZS_SEG_WORDS (ZS_SPEC_SLOTS + ZS_SYNC_SLOTS + ZS_FIX_SLOTS)
-static_assert(ZS_SPEC_SLOTS % 4 == 0 && ZS_SEG_WORDS % 4 == 0, "16-byte aligned scratch regions");
-static_assert(ZS_SEG == ZS_PARSE_SEG && ZS_SEG_WORDS == ZS_PARSE_SEG_WORDS, "scratch layout shared with capi.cpp");
+// Scratch per speculative segment of SEG positions: its speculative symbols,
+// its sync points (+ sentinel) and its catch-up symbols.
+template <uint32_t SEG>
+struct zs_seg_cfg {
+  static constexpr uint32_t SPEC = (SEG + 260u + 3u) & ~3u;  // >= SEG + MAX_MATCH - 1 symbols + final literal
+  static constexpr uint32_t SYNC = SEG + 4u;                 // >= SEG sync points + sentinel
+  static constexpr uint32_t FIX = SPEC;
+  static constexpr uint32_t WORDS = SPEC + SYNC + FIX;
+};
+static_assert(zs_seg_cfg<ZS_PARSE_SEG>::WORDS == ZS_PARSE_SEG_WORDS, "scratch layout shared with capi.cpp");
+static_assert(zs_seg_cfg<ZS_PARSE2W_SEG>::WORDS == ZS_PARSE2W_SEG_WORDS, "scratch layout shared with capi.cpp");
+
+// LDS-visible ordering among the lanes of ONE wave (the splice runs on one wave
+// while the workgroup's other wave may be elsewhere: no s_barrier)
+#define ZS_WAVE_SYNC()                                   \
+  do {                                                   \
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); \
+    __builtin_amdgcn_wave_barrier();                     \
+  } while (0)
+
+// the true parse entering a round, handed from wave to wave (two-wave parse)
+struct zs_round_state {
+  zs_pstate t;
+  uint32_t total, last_sym;
+};
 
 // Per-lane match-table windows of pass A (WIN > 0): the wave stages, for every
 // lane, the WIN table entries from its position (and the input bytes there) in
@@ -85,8 +103,8 @@ static __device__ __forceinline__ zs_pstate zs_read_state(const zs_pstate& x, ui
 
 #define ZS_GATHER 16  // pass C: 64-symbol chunks loaded before any is stored
 
-template <uint32_t WIN>
-static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_seg_tab& T,
+template <uint32_t WIN, uint32_t SEG, uint32_t NWV>
+static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_seg_tab& T, zs_round_state& RS,
                                                      const uint8_t* __restrict__ in,
                                                      const uint64_t* __restrict__ in_off,
                                                      const uint32_t* __restrict__ in_len,
@@ -95,28 +113,38 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
                                                      const uint2* __restrict__ mres, uint32_t* __restrict__ syms,
                                                      zs_block* __restrict__ blocks, zs_stream* __restrict__ streams,
                                                      uint32_t* __restrict__ scratch, int good, int lazy) {
+  using CF = zs_seg_cfg<SEG>;
   const int s = blockIdx.x;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t n = in_len[s];
   const uint8_t* src = in + in_off[s];
   const uint2* M = mres + pos_base[s];
   uint32_t* sy = syms + pos_base[s] + s;  // each stream owns n+1 symbol slots
-  uint32_t* scr = scratch + (size_t)ZS_SEG_WORDS * (pos_base[s] / ZS_SEG + s);
+  // this wave's 64 segment slots (a stream owns >= min(nseg, 64 NWV) slots)
+  uint32_t* scr = scratch + (size_t)CF::WORDS * (pos_base[s] / SEG + s + 64u * wave);
   zs_block* blk = blocks + blk_base[s];
-  const uint32_t nseg = (n + ZS_SEG - 1) / ZS_SEG;
+  const uint32_t nseg = (n + SEG - 1) / SEG;
   const bool aligned = ((uintptr_t)src & 3u) == 0;
 
   zs_pstate t = {0, 0, ZS_MIN_MATCH - 1, 0};  // the true parse state entering the round (wave-uniform)
   uint32_t total = 0;     // symbols written (wave-uniform)
   uint32_t last_sym = 0;  // the last symbol written (wave-uniform)
+  if (NWV > 1) {
+    if (threadIdx.x == 0) RS = {t, 0u, 0u};
+    __syncthreads();
+  }
 
-  for (uint32_t r0 = 0; r0 < nseg; r0 += 64) {
-    const uint32_t nr = min(64u, nseg - r0);
+  // NWV waves take NWV consecutive rounds of 64 segments at once: every wave
+  // runs pass A on its round in parallel, then the waves run passes B and C in
+  // round order, handing the true state over through RS.
+  for (uint32_t sr = 0; sr < nseg; sr += 64u * NWV) {
+    const uint32_t r0 = sr + 64u * wave;
+    const uint32_t nr = r0 < nseg ? min(64u, nseg - r0) : 0u;
     const bool mine = lane < nr;  // lane owns segment r0 + lane
-    const uint32_t a = mine ? (r0 + lane) * ZS_SEG : n, b = mine ? min(n, a + ZS_SEG) : n;
-    uint32_t* spec = scr + (size_t)lane * ZS_SEG_WORDS;
-    uint32_t* sync = spec + ZS_SPEC_SLOTS;
-    uint32_t* fix = sync + ZS_SYNC_SLOTS;
+    const uint32_t a = mine ? (r0 + lane) * SEG : n, b = mine ? min(n, a + SEG) : n;
+    uint32_t* spec = scr + (size_t)lane * CF::WORDS;
+    uint32_t* sync = spec + CF::SPEC;
+    uint32_t* fix = sync + CF::SYNC;
 
     // ---- pass A: speculative parse of the lane's segment from the position-0 state
     zs_pstate st = {a, 0, ZS_MIN_MATCH - 1, 0};
@@ -207,13 +235,25 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
       }
     }
 
+    // Phase 1 (pass B + the round's symbol count) needs the true state entering
+    // the round: the waves run it in round order.  Phase 2 (the splice) needs
+    // only this round's results, so a wave's phase 2 overlaps the next wave's
+    // phase 1.
+    uint32_t nf = 0, from = ZS_NONE, start = 0, R = 0, tot0 = 0;
+    bool final_lit_r = false;
+    for (uint32_t k = 0; k < NWV + (NWV > 1 ? 1u : 0u); k++) {
+    if (NWV > 1) __syncthreads();
+    if (nr != 0 && k == wave) {
+    if (NWV > 1) {
+      t = RS.t;
+      total = RS.total;
+    }
     // ---- pass B: the true parse across each boundary until it meets a sync
     // point of the segment.  Every lane does its own boundary at once, entering
     // with the speculative end state of the segment before (which IS the true
     // state there whenever that segment synced; lane 0 enters with the true
     // state); a serial check then redoes, in order, the rare boundary whose
     // predecessor never synced.
-    uint32_t nf = 0, from = ZS_NONE, start = 0;
     zs_pstate after;  // true state at the segment's end, given its entry state
     auto catch_up = [&](zs_pstate c) __attribute__((always_inline)) {
       uint32_t si = 0, sv = sync[0];
@@ -270,12 +310,21 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
       const uint32_t y = __shfl_up(incl, d, 64);
       if (lane >= (uint32_t)d) incl += y;
     }
-    const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     T.off[lane] = incl - run;
     if (lane == 63) T.off[64] = R;
     T.nf[lane] = nf;
     T.from[lane] = from;
-    __syncthreads();
+    tot0 = total;
+    final_lit_r = r0 + nr == nseg && t.ma != 0;
+    total += R;
+    if (NWV > 1 && lane == 0) {
+      RS.t = t;
+      RS.total = total;
+    }
+    }  // phase 1
+    if (nr != 0 && k == wave + (NWV > 1 ? 1u : 0u)) {
+    ZS_WAVE_SYNC();
     uint32_t js = 0, lastv = 0;
     for (uint32_t g0 = 0; g0 < R; g0 += 64 * ZS_GATHER) {
       uint32_t v[ZS_GATHER];
@@ -286,34 +335,36 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
         if (g < R) {
           while (T.off[js + 1] <= g) js++;
           const uint32_t i = g - T.off[js], nfj = T.nf[js];
-          const uint32_t* base = scr + (size_t)js * ZS_SEG_WORDS;
-          v[k] = i < nfj ? base[ZS_SPEC_SLOTS + ZS_SYNC_SLOTS + i] : base[T.from[js] + i - nfj];
+          const uint32_t* base = scr + (size_t)js * CF::WORDS;
+          v[k] = i < nfj ? base[CF::SPEC + CF::SYNC + i] : base[T.from[js] + i - nfj];
         }
       }
 #pragma unroll
       for (int k = 0; k < ZS_GATHER; k++) {
         const uint32_t g = g0 + 64 * k + lane;
-        if (g < R) sy[total + g] = v[k];
+        if (g < R) sy[tot0 + g] = v[k];
         if (g == R - 1) lastv = v[k];
       }
     }
-    if (R) last_sym = (uint32_t)__shfl((int)lastv, (int)((R - 1) & 63u), 64);
+    if (R) {
+      last_sym = (uint32_t)__shfl((int)lastv, (int)((R - 1) & 63u), 64);
+      if (NWV > 1 && lane == 0) RS.last_sym = last_sym;  // rounds' phases 2 run in order
+    }
 
     // block cuts: FLUSH_BLOCK after every 16383rd tallied symbol (deflate.ts:336,
     // 1120-1124) -- but not after the final deferred literal, which is tallied
     // after the loop (deflate.ts:1429-1432)
-    const bool final_lit = r0 + nr == nseg && t.ma != 0;
-    const uint32_t unchecked = final_lit ? total + R - 1 : ZS_NONE;
-    for (uint32_t gi = (total / ZS_SYM_END + 1) * ZS_SYM_END - 1; gi < total + R; gi += ZS_SYM_END) {
+    const uint32_t unchecked = final_lit_r ? tot0 + R - 1 : ZS_NONE;
+    for (uint32_t gi = (tot0 / ZS_SYM_END + 1) * ZS_SYM_END - 1; gi < tot0 + R; gi += ZS_SYM_END) {
       if (gi == unchecked) continue;
-      const uint32_t g = gi - total;
+      const uint32_t g = gi - tot0;
       uint32_t j = 0;
       while (T.off[j + 1] <= g) j++;
       const uint32_t i = g - T.off[j], nfj = T.nf[j], fj = T.from[j];
-      const uint32_t* base = scr + (size_t)j * ZS_SEG_WORDS;
+      const uint32_t* base = scr + (size_t)j * CF::WORDS;
       uint32_t acc = 0, li = 0;  // run lengths through symbol i, symbol i's length
       for (uint32_t q = lane; q <= i; q += 64) {
-        const uint32_t l = zs_sym_len(q < nfj ? base[ZS_SPEC_SLOTS + ZS_SYNC_SLOTS + q] : base[fj + q - nfj]);
+        const uint32_t l = zs_sym_len(q < nfj ? base[CF::SPEC + CF::SYNC + q] : base[fj + q - nfj]);
         acc += l;
         li = q == i ? l : li;
       }
@@ -329,8 +380,16 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
         blk[bi].pad = zs_slides(end - li + 1, n);
       }
     }
-    total += R;
+    ZS_WAVE_SYNC();
+    }  // phase 2
+    }  // handoff
+  }
+  if (NWV > 1) {
     __syncthreads();
+    if (wave != 0) return;
+    t = RS.t;
+    total = RS.total;
+    last_sym = RS.last_sym;
   }
 
   // ---- block records (deflate.ts:1434-1440: the final block takes the rest, possibly empty)
@@ -341,7 +400,7 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
   // position (the symbols tile [0, n), so the last one starts at n - its length)
   const uint32_t v_last = total == 0 ? 0u : final_lit ? n - 1 : n - zs_sym_len(last_sym) + 1;
   const uint32_t final_slides = zs_slides(v_last, n);
-  __syncthreads();
+  ZS_WAVE_SYNC();
   for (uint32_t b0 = 0; b0 <= nflush; b0 += 64) {
     const uint32_t b = b0 + lane;
     zs_block k;
@@ -357,9 +416,9 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
       // bit 1: the block began before the slid window (matters for stored blocks)
       k.last = (b == nflush ? 1u : 0u) | ((uint64_t)in_start < 32768ull * slides ? 2u : 0u);
     }
-    __syncthreads();  // every read of in_end / pad in this chunk precedes the writes
+    ZS_WAVE_SYNC();  // every read of in_end / pad in this chunk precedes the writes
     if (b <= nflush) blk[b] = k;
-    __syncthreads();
+    ZS_WAVE_SYNC();
   }
   if (lane == 0) {
     streams[s].nsym = total;
@@ -367,17 +426,21 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
   }
 }
 
-#define ZS_PARSE_KERNEL(name, WIN)                                                                                   \
-  __global__ __launch_bounds__(64) void name(                                                                        \
+#define ZS_PARSE_KERNEL(name, WIN, SEG, NWV)                                                                        \
+  __global__ __launch_bounds__(64 * NWV) void name(                                                                  \
       const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ in_len,     \
       const uint64_t* __restrict__ pos_base, const uint32_t* __restrict__ blk_base, const uint2* __restrict__ mres,  \
       uint32_t* __restrict__ syms, zs_block* __restrict__ blocks, zs_stream* __restrict__ streams,                  \
       uint32_t* __restrict__ scratch, int good, int lazy) {                                                         \
-    __shared__ zs_parse_win<WIN> W;                                                                                 \
-    __shared__ zs_seg_tab T;                                                                                        \
-    zs_parse_body<WIN>(W, T, in, in_off, in_len, pos_base, blk_base, mres, syms, blocks, streams, scratch, good,    \
-                       lazy);                                                                                       \
+    __shared__ zs_parse_win<WIN> W[NWV];                                                                            \
+    __shared__ zs_seg_tab T[NWV];                                                                                   \
+    __shared__ zs_round_state RS;                                                                                   \
+    const uint32_t w_ = threadIdx.x >> 6;                                                                           \
+    zs_parse_body<WIN, SEG, NWV>(W[w_], T[w_], RS, in, in_off, in_len, pos_base, blk_base, mres, syms, blocks,      \
+                                 streams, scratch, good, lazy);                                                     \
   }
-ZS_PARSE_KERNEL(zs_k_parse16, 16)
-ZS_PARSE_KERNEL(zs_k_parse, 32)
-ZS_PARSE_KERNEL(zs_k_parse_direct, 0)
+ZS_PARSE_KERNEL(zs_k_parse16, 16, ZS_PARSE_SEG, 1)
+ZS_PARSE_KERNEL(zs_k_parse, 32, ZS_PARSE_SEG, 1)
+ZS_PARSE_KERNEL(zs_k_parse_direct, 0, ZS_PARSE_SEG, 1)
+// two waves per stream, 512-position segments: half the speculative pass per lane (small batches)
+ZS_PARSE_KERNEL(zs_k_parse_2w, 32, ZS_PARSE2W_SEG, 2)
