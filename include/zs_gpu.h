@@ -151,6 +151,9 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * else 1..64, a power of two): members per workgroup of the inflate lane path;
  * "inflate_wave_min" (default 32768; 0 = never): members with more input bytes
  * decode one per wave (inflate_wave.hip) beside the lane kernel;
+ * "parse_waves" (default 0 = two below 2048 streams, else one; 1 or 2): waves
+ * per stream of the levels 4..9 one-wave-family parse (two: 512-position
+ * segments, two rounds' speculative passes at once);
  * "fast_group" (default 1): levels 1..3 replay deflate_fast a group of 64
  * positions at a time from speculative per-lane chain walks (0: step by step);
  * "chunks" (default 0 = chosen from the batch, 1 today; else 1..64): deflate
