@@ -35,6 +35,7 @@ struct zs_tw {  // LDS workspace of one wave, common/types.ts DeflateState tree 
   uint32_t hist[ZS_L_CODES + ZS_D_CODES];
   uint32_t hdr[ZS_HDR_WORDS];
   uint32_t bc[4];  // lane 0 -> wave: type, max codes, header bits
+  uint32_t b32[32];  // scan_tree's bl_tree frequencies (LDS atomics)
 };
 
 struct zs_tdesc {
@@ -212,27 +213,6 @@ static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:2
   zs_gen_bitlen(t, d);  // the codes follow by the wave (zs_gen_codes_wave)
 }
 
-static __device__ void zs_scan_tree(zs_tstate& t, zs_tdesc& d, int max_code) {  // trees.ts:318-363
-  uint16_t* bf = t.w->bfreq;
-  int prevlen = -1, curlen, nextlen = d.len[0], count = 0, max_count = 7, min_count = 4;
-  if (nextlen == 0) { max_count = 138; min_count = 3; }
-  d.len[max_code + 1] = 0xffff;
-  for (int n = 0; n <= max_code; n++) {
-    curlen = nextlen;
-    nextlen = d.len[n + 1];
-    if (++count < max_count && curlen == nextlen) continue;
-    else if (count < min_count) bf[curlen] = (uint16_t)(bf[curlen] + count);
-    else if (curlen != 0) { if (curlen != prevlen) bf[curlen]++; bf[16]++; }
-    else if (count <= 10) bf[17]++;
-    else bf[18]++;
-    count = 0;
-    prevlen = curlen;
-    if (nextlen == 0) { max_count = 138; min_count = 3; }
-    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
-    else { max_count = 7; min_count = 4; }
-  }
-}
-
 static __device__ __forceinline__ void zs_hput(zs_tstate& t, uint32_t v, int n) {
   uint32_t* h = t.w->hdr;
   const uint32_t pos = t.hbits;
@@ -241,28 +221,86 @@ static __device__ __forceinline__ void zs_hput(zs_tstate& t, uint32_t v, int n) 
   t.hbits += n;
 }
 
-static __device__ void zs_send_tree(zs_tstate& t, zs_tdesc& d, int max_code) {  // trees.ts:365-414
-  const uint16_t* bc = t.w->bcode;
-  const uint16_t* bl = t.w->blen;
-  int prevlen = -1, curlen, nextlen = d.len[0], count = 0, max_count = 7, min_count = 4;
-  if (nextlen == 0) { max_count = 138; min_count = 3; }
-  for (int n = 0; n <= max_code; n++) {
-    curlen = nextlen;
-    nextlen = d.len[n + 1];
-    if (++count < max_count && curlen == nextlen) continue;
-    else if (count < min_count) { do zs_hput(t, bc[curlen], bl[curlen]); while (--count != 0); }
-    else if (curlen != 0) {
-      if (curlen != prevlen) { zs_hput(t, bc[curlen], bl[curlen]); count--; }
-      zs_hput(t, bc[16], bl[16]);
-      zs_hput(t, (uint32_t)(count - 3), 2);
-    } else if (count <= 10) { zs_hput(t, bc[17], bl[17]); zs_hput(t, (uint32_t)(count - 3), 3); }
-    else { zs_hput(t, bc[18], bl[18]); zs_hput(t, (uint32_t)(count - 11), 7); }
-    count = 0;
-    prevlen = curlen;
-    if (nextlen == 0) { max_count = 138; min_count = 3; }
-    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
-    else { max_count = 7; min_count = 4; }
+// ---- scan_tree / send_tree (trees.ts:318-414) over maximal runs, one lane per
+// run.  The serial automaton's chunking of a run of r equal lengths v depends
+// on (v, r) alone: entering a run the state is always (max, min) = (138, 3)
+// for v = 0 and (7, 4) otherwise (the previous length differs), and inside a
+// run it is (138, 3) for zeros and (6, 3) otherwise, with prevlen = v after
+// the first chunk.  So each run's codes (symbol, extra value, extra bits) are
+// enumerated by its own lane: frequencies by LDS atomics, the header bits at
+// the run's offset from a prefix sum over the runs in index order.
+template <class F>
+static __device__ __forceinline__ void zs_run_codes(uint32_t v, uint32_t r, F&& f) {
+  if (v == 0) {
+    while (r) {
+      const uint32_t c = r < 138u ? r : 138u;
+      r -= c;
+      if (c < 3) for (uint32_t k = 0; k < c; k++) f(0u, 0u, 0u);
+      else if (c <= 10) f(17u, c - 3u, 3u);
+      else f(18u, c - 11u, 7u);
+    }
+  } else {
+    uint32_t c = r < 7u ? r : 7u;
+    r -= c;
+    if (c < 4) for (uint32_t k = 0; k < c; k++) f(v, 0u, 0u);
+    else { f(v, 0u, 0u); f(16u, c - 4u, 2u); }
+    while (r) {
+      c = r < 6u ? r : 6u;
+      r -= c;
+      if (c < 3) for (uint32_t k = 0; k < c; k++) f(v, 0u, 0u);
+      else f(16u, c - 3u, 2u);
+    }
   }
+}
+// lane's run in the 64-index chunk at n0 of len[0..max_code] (guard len[max_code + 1] = 0xffff already
+// set): returns true with (v, r) if index n0 + lane starts a run
+static __device__ __forceinline__ bool zs_run_at(const uint16_t* len, int max_code, int n0, uint32_t lane,
+                                                 uint32_t& v, uint32_t& r) {
+  const int n = n0 + (int)lane;
+  if (n > max_code) return false;
+  v = len[n];
+  if (n > 0 && len[n - 1] == v) return false;
+  int m = n + 1;
+  while (len[m] == v) m++;  // the guard ends every run
+  r = (uint32_t)(m - n);
+  return true;
+}
+// all lanes: scan_tree's bl_tree frequencies of one tree, added to b32[]
+static __device__ void zs_scan_tree_wave(const uint16_t* len, int max_code, uint32_t* b32, uint32_t lane) {
+  for (int n0 = 0; n0 <= max_code; n0 += 64) {
+    uint32_t v = 0, r = 0;
+    if (zs_run_at(len, max_code, n0, lane, v, r))
+      zs_run_codes(v, r, [&](uint32_t sym, uint32_t, uint32_t) { atomicAdd(&b32[sym], 1u); });
+  }
+}
+// all lanes: send_tree's header bits of one tree at bit `base` of hdr[] (zeroed); returns the end bit
+static __device__ uint32_t zs_send_tree_wave(const uint16_t* len, int max_code, const uint16_t* bc, const uint16_t* bl,
+                                             uint32_t* hdr, uint32_t base, uint32_t lane) {
+  for (int n0 = 0; n0 <= max_code; n0 += 64) {
+    uint32_t v = 0, r = 0, bits = 0;
+    const bool st = zs_run_at(len, max_code, n0, lane, v, r);
+    if (st) zs_run_codes(v, r, [&](uint32_t sym, uint32_t, uint32_t xb) { bits += bl[sym] + xb; });
+    uint32_t incl = bits;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    uint32_t pos = base + incl - bits;
+    auto put = [&](uint32_t val, uint32_t nb) {
+      if (nb == 0) return;
+      atomicOr(&hdr[pos >> 5], val << (pos & 31u));
+      if ((pos & 31u) + nb > 32u) atomicOr(&hdr[(pos >> 5) + 1], val >> (32u - (pos & 31u)));
+      pos += nb;
+    };
+    if (st)
+      zs_run_codes(v, r, [&](uint32_t sym, uint32_t xv, uint32_t xb) {
+        put(bc[sym], bl[sym]);
+        put(xv, xb);
+      });
+    base += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  }
+  return base;
 }
 
 __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
@@ -329,11 +367,20 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   __syncthreads();
   zs_gen_codes_wave(w.bl_count, w.dlen, w.dcode, __builtin_amdgcn_readlane(D.max_code, 0), lane);
   __syncthreads();
-  if (lane == 0) {  // build_bl_tree (trees.ts:416-432)
-    zs_scan_tree(t, L, L.max_code);
-    zs_scan_tree(t, D, D.max_code);
-    zs_build_tree(t, B);
+  // build_bl_tree (trees.ts:416-432): scan_tree of both trees by runs (all lanes), then the tree (lane 0)
+  const int lmax = __builtin_amdgcn_readlane(L.max_code, 0), dmax = __builtin_amdgcn_readlane(D.max_code, 0);
+  if (lane < 32) w.b32[lane] = 0;
+  if (lane == 0) {
+    w.llen[lmax + 1] = 0xffff;  // scan_tree's guards (trees.ts:328), read by send_tree too
+    w.dlen[dmax + 1] = 0xffff;
   }
+  __syncthreads();
+  zs_scan_tree_wave(w.llen, lmax, w.b32, lane);
+  zs_scan_tree_wave(w.dlen, dmax, w.b32, lane);
+  __syncthreads();
+  if (lane < ZS_BL_CODES) w.bfreq[lane] = (uint16_t)(w.bfreq[lane] + w.b32[lane]);
+  __syncthreads();
+  if (lane == 0) zs_build_tree(t, B);
   __syncthreads();
   zs_gen_codes_wave(w.bl_count, w.blen, w.bcode, __builtin_amdgcn_readlane(B.max_code, 0), lane);
   __syncthreads();
@@ -351,20 +398,24 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
     else if (static_lenb == opt_lenb) type = 1;
     else type = 2;
     if (type == 2) {
-      // send_all_trees (trees.ts:434-447)
+      // send_all_trees (trees.ts:434-447): the counts and the bl_tree lengths here, the two trees by all lanes
       const int lcodes = L.max_code + 1, dcodes = D.max_code + 1, blcodes = max_blindex + 1;
       zs_hput(t, (uint32_t)(lcodes - 257), 5);
       zs_hput(t, (uint32_t)(dcodes - 1), 5);
       zs_hput(t, (uint32_t)(blcodes - 4), 4);
       for (int rank = 0; rank < blcodes; rank++) zs_hput(t, w.blen[ZS_BL_ORDER[rank]], 3);
-      zs_send_tree(t, L, lcodes - 1);
-      zs_send_tree(t, D, dcodes - 1);
     }
     w.bc[0] = type;
     w.bc[1] = t.hbits;
   }
   __syncthreads();
-  const uint32_t type = w.bc[0], hbits = w.bc[1];
+  const uint32_t type = w.bc[0];
+  uint32_t hbits = w.bc[1];
+  if (type == 2) {
+    hbits = zs_send_tree_wave(w.llen, lmax, w.bcode, w.blen, w.hdr, hbits, lane);
+    hbits = zs_send_tree_wave(w.dlen, dmax, w.bcode, w.blen, w.hdr, hbits, lane);
+    __syncthreads();
+  }
   // exact payload bits of the chosen coding, from the true counts
   uint32_t data_bits = 0;
   if (type != 0) {
