@@ -303,6 +303,7 @@ static __device__ uint32_t zs_send_tree_wave(const uint16_t* len, int max_code, 
   return base;
 }
 
+#define ZS_HIST_INFLIGHT 32u
 __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                  const uint64_t* __restrict__ pos_base,
                                                  const uint32_t* __restrict__ blk_base,
@@ -320,18 +321,18 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   for (uint32_t i = lane; i < ZS_L_CODES + ZS_D_CODES; i += 64) w.hist[i] = 0;
   for (uint32_t i = lane; i < ZS_HDR_WORDS; i += 64) w.hdr[i] = 0;
   __syncthreads();
-  // histogram (deflate/utils.ts:55-81 tallies, done in parallel); eight symbol
-  // loads in flight per lane before their atomics, so the wave waits for
-  // memory once per 512 symbols rather than once per 64
-  for (uint32_t i0 = 0; i0 < blk.sym_count; i0 += 512) {
-    uint32_t v[8];
+  // histogram (deflate/utils.ts:55-81 tallies, done in parallel); ZS_HIST_INFLIGHT
+  // symbol loads in flight per lane before their atomics, so the wave waits for
+  // memory once per 64 * ZS_HIST_INFLIGHT symbols rather than once per 64
+  for (uint32_t i0 = 0; i0 < blk.sym_count; i0 += 64 * ZS_HIST_INFLIGHT) {
+    uint32_t v[ZS_HIST_INFLIGHT];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
+    for (uint32_t k = 0; k < ZS_HIST_INFLIGHT; k++) {
       const uint32_t i = i0 + 64 * k + lane;
       v[k] = i < blk.sym_count ? sy[i] : 0xffffffffu;
     }
 #pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
+    for (uint32_t k = 0; k < ZS_HIST_INFLIGHT; k++) {
       if (v[k] == 0xffffffffu) continue;
       if (v[k] & 0x80000000u) {
         const uint32_t lc = (v[k] >> 16) & 0xff, dist = (v[k] & 0xffffu) - 1;
