@@ -187,8 +187,8 @@ def test_group_fast_parser_equals_serial_replay(engine, level):
 
 @pytest.mark.parametrize("level", [4, 6, 9])
 def test_two_wave_parse_equals_one_wave_parse(engine, level):
-    """zs_k_parse_2w (two waves per stream, 512-position segments; the default below 2048 streams) against
-    zs_k_parse (one wave, 1 KiB segments): same bytes on 64 KiB, 256 KiB (slides, several super-rounds) and
+    """zs_k_parse_2w / _4w (two / four waves per stream, 512 / 256-position segments; two waves are the default
+    below 2048 streams) against zs_k_parse (one wave, 1 KiB segments): same bytes on 64 KiB, 256 KiB (slides, several super-rounds) and
     ragged streams, and the C2 goldens of 1,000 streams with two waves forced."""
     import zsamd
 
@@ -198,10 +198,10 @@ def test_two_wave_parse_equals_one_wave_parse(engine, level):
     inputs = [corpus.make({"kind": k, "n": n, "seed": 9500 + i}) for i, (k, n) in enumerate(specs)]
     outs = []
     try:
-        for w in (1, 2):
+        for w in (1, 2, 4):
             engine.set_option("parse_waves", w)
             outs.append(engine.compress_batch_raw(inputs, "deflate-raw", level))
-        assert outs[0] == outs[1]
+        assert outs[0] == outs[1] == outs[2]
         if level == 6:
             recs = golden_io.batch("t64_l6_raw")
             buf = bytes(zsamd.corpus("text", 0, 1000, 65536))

@@ -93,7 +93,7 @@ struct zs_ctx {
   bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)
   int parse_win = 32;        // L4..9 parse: match-table entries staged per lane in LDS (32, 16; 0: direct loads)
   int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
-  bool cur_parse2w = false;  // the current deflate batch parses with zs_k_parse_2w
+  int cur_pw = 1;            // waves per stream of the current deflate batch's parse (zs_k_parse / _2w / _4w)
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
   int chunks = 0;             // deflate: chunks of the batch pipelined over two streams (0: chosen from the batch)
@@ -252,7 +252,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "parse_split")) c->parse_split = value != 0;
   else if (!strcmp(name, "fast_group")) c->fast_group = value != 0;
   else if (!strcmp(name, "parse_waves")) {
-    if (value < 0 || value > 2) return fail(ZS_STREAM_ERROR, "parse_waves must be 0, 1 or 2");
+    if (value < 0 || value > 4 || value == 3) return fail(ZS_STREAM_ERROR, "parse_waves must be 0, 1, 2 or 4");
     c->parse_waves = value;
   }
   else if (!strcmp(name, "parse_win")) {
@@ -365,9 +365,14 @@ static int deflate_stored_batch(zs_ctx* c, int wrap, uint32_t n, const uint8_t* 
 // The L4..9 parse runs two waves per stream (zs_k_parse_2w: 512-position
 // segments, two rounds' speculative passes at once) for a batch of n streams?
 // The whole batch decides (chunks of one batch share the scratch layout).
-static bool parse_two_waves(const zs_ctx* c, uint32_t n) {
-  if (c->parse_waves) return c->parse_waves == 2 && c->parse_win == 32;
-  return n < ZS_PARSE2W_AUTO && c->parse_win == 32;
+static int parse_waves_for(const zs_ctx* c, uint32_t n) {
+  if (c->parse_win != 32) return 1;
+  if (c->parse_waves) return c->parse_waves;
+  return n < ZS_PARSE2W_AUTO ? 2 : 1;
+}
+static uint32_t parse_seg(int w) { return w == 4 ? ZS_PARSE4W_SEG : w == 2 ? ZS_PARSE2W_SEG : ZS_PARSE_SEG; }
+static uint32_t parse_seg_words(int w) {
+  return w == 4 ? ZS_PARSE4W_SEG_WORDS : w == 2 ? ZS_PARSE2W_SEG_WORDS : ZS_PARSE_SEG_WORDS;
 }
 
 // Chunks a deflate batch of n streams is pipelined in (option chunks = 0).
@@ -426,9 +431,10 @@ static int deflate_chunk(zs_ctx* c, hipStream_t st, int level, int wrap, const z
                                      syms, d_bk, d_st, pscr, cfg.good, cfg.lazy);
     } else {
       auto parse = c->parse_win == 32 ? zs_k_parse : c->parse_win == 16 ? zs_k_parse16 : zs_k_parse_direct;
-      const bool two = c->cur_parse2w;  // decided for the whole batch (scratch layout)
-      if (two) parse = zs_k_parse_2w;
-      parse<<<n, two ? 128 : 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(),
+      const int pw = c->cur_pw;  // decided for the whole batch (scratch layout)
+      if (pw == 2) parse = zs_k_parse_2w;
+      if (pw == 4) parse = zs_k_parse_4w;
+      parse<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(),
                               syms, d_bk, d_st, pscr, cfg.good, cfg.lazy);
     }
     MARK("parse");
@@ -502,12 +508,10 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   HIPCHK(c->prevd.ensure(2 * P + 64));
   HIPCHK(c->mres.ensure(8 * P + 64));
   HIPCHK(c->syms.ensure(4 * (P + n) + 64));
-  c->cur_parse2w = level >= 4 && !c->parse_split && parse_two_waves(c, n);
+  c->cur_pw = level >= 4 && !c->parse_split ? parse_waves_for(c, n) : 1;
   if (level >= 4)
     HIPCHK(c->pscr.ensure(c->parse_split ? 4ull * ZS_PARSE_RANGE_WORDS * (NR + 1)
-                                         : c->cur_parse2w
-                                               ? 4ull * ZS_PARSE2W_SEG_WORDS * (P / ZS_PARSE2W_SEG + n + 1)
-                                               : 4ull * ZS_PARSE_SEG_WORDS * (P / ZS_PARSE_SEG + n + 1)));
+                                         : 4ull * parse_seg_words(c->cur_pw) * (P / parse_seg(c->cur_pw) + n + 1)));
   HIPCHK(c->blocks.ensure(sizeof(zs_block) * (size_t)B));
   HIPCHK(c->streams.ensure(sizeof(zs_stream) * (size_t)n));
   HIPCHK(c->codes.ensure(4ull * (ZS_L_CODES + ZS_D_CODES) * B));
@@ -548,8 +552,7 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
                                 d_out, d_out_off + a, d_out_cap + a, d_pos + a, d_blk + a, d_rng + a, d_st + a,
                                 c->syms.as<uint32_t>() + a,
                                 c->pscr.as<uint32_t>() + (c->parse_split ? 0
-                                                          : (size_t)(c->cur_parse2w ? ZS_PARSE2W_SEG_WORDS
-                                                                                           : ZS_PARSE_SEG_WORDS) * a),
+                                                          : (size_t)parse_seg_words(c->cur_pw) * a),
                                 c->check.as<uint32_t>() + a, d_status + a, d_out_len + a);
     if (r != ZS_OK) return r;
   }

@@ -47,6 +47,7 @@ struct zs_seg_cfg {
 };
 static_assert(zs_seg_cfg<ZS_PARSE_SEG>::WORDS == ZS_PARSE_SEG_WORDS, "scratch layout shared with capi.cpp");
 static_assert(zs_seg_cfg<ZS_PARSE2W_SEG>::WORDS == ZS_PARSE2W_SEG_WORDS, "scratch layout shared with capi.cpp");
+static_assert(zs_seg_cfg<ZS_PARSE4W_SEG>::WORDS == ZS_PARSE4W_SEG_WORDS, "scratch layout shared with capi.cpp");
 
 // LDS-visible ordering among the lanes of ONE wave (the splice runs on one wave
 // while the workgroup's other wave may be elsewhere: no s_barrier)
@@ -444,3 +445,5 @@ ZS_PARSE_KERNEL(zs_k_parse, 32, ZS_PARSE_SEG, 1)
 ZS_PARSE_KERNEL(zs_k_parse_direct, 0, ZS_PARSE_SEG, 1)
 // two waves per stream, 512-position segments: half the speculative pass per lane (small batches)
 ZS_PARSE_KERNEL(zs_k_parse_2w, 32, ZS_PARSE2W_SEG, 2)
+// four waves per stream, 256-position segments
+ZS_PARSE_KERNEL(zs_k_parse_4w, 32, ZS_PARSE4W_SEG, 4)

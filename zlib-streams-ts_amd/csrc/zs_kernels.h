@@ -51,11 +51,14 @@ ZS_PARSE_DECL(zs_k_parse)
 ZS_PARSE_DECL(zs_k_parse16)
 ZS_PARSE_DECL(zs_k_parse_direct)
 ZS_PARSE_DECL(zs_k_parse_2w)  // two waves per stream, ZS_PARSE2W_SEG-position segments
+ZS_PARSE_DECL(zs_k_parse_4w)  // four waves per stream, ZS_PARSE4W_SEG-position segments
 // parse scratch words per 1024-position segment (deflate_parse.hip)
 #define ZS_PARSE_SEG 1024u
 #define ZS_PARSE_SEG_WORDS 3596u
 #define ZS_PARSE2W_SEG 512u
 #define ZS_PARSE2W_SEG_WORDS 2060u
+#define ZS_PARSE4W_SEG 256u
+#define ZS_PARSE4W_SEG_WORDS 1292u
 // the two-kernel parse (deflate_parse2.hip): positions per range, scratch words per range
 #define ZS_PARSE_RANGE 2048u
 #define ZS_PARSE_RANGE_WORDS 5376u
