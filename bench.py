@@ -96,9 +96,17 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # ZS_BENCH_BACKEND=gloo + more ranks than GPUs: a functional rehearsal of the multi-rank path on a
+        # one-GPU box (ranks share the device); the driver's runs use RCCL, one rank per GPU
+        backend = os.environ.get("ZS_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            self.local %= max(1, torch.cuda.device_count())
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            else:
+                dist.init_process_group(backend)
         torch.cuda.set_device(self.local)
         self.dev = torch.device("cuda", self.local)
 
