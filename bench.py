@@ -141,8 +141,8 @@ def profiled_traffic(kernel, kernel_ms):
     within 10 % (i.e. it profiled this build); otherwise (None, reason)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")))  # round directories sort in order
-    stale = None
-    for f in reversed(files):  # newest first; the first whose duration matches this run (same build and config)
+    stale, hit = None, None
+    for f in reversed(files):  # newest round first; among matching durations, the profile with the most launches
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
@@ -154,7 +154,10 @@ def profiled_traffic(kernel, kernel_ms):
         if abs(prof_ms - kernel_ms) > 0.1 * kernel_ms:
             stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
             continue
-        return int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms)
+        if hit is None or e.get("calls", 0) > hit[0]:
+            hit = (e.get("calls", 0), int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms))
+    if hit:
+        return hit[1], hit[2]
     return None, stale or "no committed profile for %s" % kernel
 
 
@@ -169,8 +172,8 @@ def profiled_ceilings(kernel, kernel_ms):
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_summary*.json")) +
                    glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")))
-    stale = None
-    for f in reversed(files):  # newest first; the first whose duration matches this run
+    stale, hit = None, None
+    for f in reversed(files):  # newest round first; among matching durations, the summary with the most launches
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
@@ -182,10 +185,13 @@ def profiled_ceilings(kernel, kernel_ms):
         if abs(prof_ms - kernel_ms) > 0.15 * kernel_ms:
             stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
             continue
-        out = {k: e[k] for k in ("lds_bank_conflict_frac", "valu_busy", "active_frac_of_wave_cycles",
-                                 "wait_frac_of_wave_cycles", "wait_inst_frac_of_wave_cycles") if k in e}
-        out["source"] = "%s (%s avg %.3f ms under --pmc)" % (src, kernel, prof_ms)
-        return out
+        if hit is None or e.get("dispatches", 0) > hit[0]:
+            out = {k: e[k] for k in ("lds_bank_conflict_frac", "valu_busy", "active_frac_of_wave_cycles",
+                                     "wait_frac_of_wave_cycles", "wait_inst_frac_of_wave_cycles") if k in e}
+            out["source"] = "%s (%s avg %.3f ms under --pmc)" % (src, kernel, prof_ms)
+            hit = (e.get("dispatches", 0), out)
+    if hit:
+        return hit[1]
     return {"source": stale or "no committed SQ summary for %s" % kernel}
 
 
