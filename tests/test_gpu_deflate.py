@@ -262,16 +262,21 @@ def test_c5_gzip_batch_matches_reference_goldens(engine):
 @pytest.mark.slow
 @pytest.mark.parametrize("name,level", [("t256_l1_raw", 1), ("t256_l9_raw", 9)])
 def test_c4_256k_streams_match_reference_goldens(engine, name, level):
-    """BASELINE.json configs[3]: 256 KiB T-corpus streams at L1 (deflate_fast) and L9 (slides, chain 4096)."""
+    """BASELINE.json configs[3]: 4096 x 256 KiB T-corpus streams at L1 (deflate_fast) and L9 (slides, chain 4096)."""
     import zsamd
 
     recs = golden_io.batch(name)
-    n = 512
-    buf = bytes(zsamd.corpus("text", 0, n, 262144))
-    inputs = [buf[i * 262144:(i + 1) * 262144] for i in range(n)]
-    res = engine.compress_batch_raw(inputs, "deflate-raw", level)
-    bad = [i for i, (st, out) in enumerate(res) if st != 1 or (len(out), hashlib.sha256(out).digest()[:16]) != recs[i]]
-    assert not bad, bad[:10]
+    # all 4096 streams of the config, in four batches of 1024 (the per-GPU share at 8 GPUs is 512)
+    total = 0
+    for lo in range(0, 4096, 1024):
+        buf = bytes(zsamd.corpus("text", lo, 1024, 262144))
+        inputs = [buf[i * 262144:(i + 1) * 262144] for i in range(1024)]
+        res = engine.compress_batch_raw(inputs, "deflate-raw", level)
+        bad = [lo + i for i, (st, out) in enumerate(res)
+               if st != 1 or (len(out), hashlib.sha256(out).digest()[:16]) != recs[lo + i]]
+        assert not bad, bad[:10]
+        total += sum(len(o) for _, o in res)
+    assert total == {1: 419870313, 9: 351529571}[level]  # SURVEY 8(d) C4 totals
 
 
 @pytest.mark.gpu
