@@ -28,7 +28,7 @@
 #define SLIDE_AT 65274u
 #define SYM_END 16383u
 #define HMASK 0x7fffu
-#define GROUP_STEPS 58u  // step starts in [g0, g0 + 58): short-match insides stay below g0 + 64
+// step starts in [g0, g0 + 64 - max_lazy): short-match insides stay below g0 + 64
 
 static uint32_t hash3(const uint8_t* s, uint32_t q) {
   return (((uint32_t)s[q] << 10) ^ ((uint32_t)s[q + 1] << 5) ^ s[q + 2]) & HMASK;
@@ -135,7 +135,7 @@ static void grouped(const uint8_t* s, uint32_t n, uint32_t chain, uint32_t lazy,
     const uint32_t m = n < base + 65536u ? n : base + 65536u;
     uint32_t tslide = base + SLIDE_AT;  // first position at which the next slide is due
     if (m >= MIN_LOOKAHEAD - 1 && m - (MIN_LOOKAHEAD - 1) > tslide) tslide = m - (MIN_LOOKAHEAD - 1);
-    uint32_t g1 = g0 + GROUP_STEPS;
+    uint32_t g1 = g0 + 64u - lazy;
     if (g1 > tslide) g1 = tslide;
     if (g1 > n) g1 = n;
     // ---- lanes (parallel in the kernel)

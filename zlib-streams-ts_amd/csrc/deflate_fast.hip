@@ -228,14 +228,13 @@ __global__ __launch_bounds__(64) void zs_k_fast_serial(const uint8_t* __restrict
 //      inserted lanes), and a result at nice is extended to its exact length;
 //   4. the truly inserted positions enter head[] / prev[] in lane order (one
 //      more exchange).
-// Steps start below g0 + 58 (the inside of a short match, <= max_lazy <= 6,
-// stays inside the group) and below the position at which fill_window's next
+// Steps start below g0 + 64 - max_lazy (the inside of a short match, <= max_lazy
+// positions, stays inside the group) and below the position at which fill_window's next
 // slide is due (deflate.ts:180-190), so a group never straddles a slide.
 // The input sits in a 32 KiB LDS ring holding [E - 32768, E) with
 // g0 + 160 <= E <= g0 + 262: every candidate (distance <= MAX_DIST) and every
 // scan byte up to g0 + 122 + 32; 256-byte chunks are prefetched in registers
 // one chunk ahead and appended 64 bytes at a time.
-#define ZS_FG_STEPS 58u
 #define ZS_FG_LONG 0xffffu  // a lane result longer than nice + 32: extended by the serial replay
 
 struct zs_fastg_lds {
@@ -359,7 +358,7 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
     const uint32_t g0 = p, rg0 = g0 - base;
     uint32_t tslide = base + ZS_SLIDE_AT;
     if (m >= ZS_MIN_LOOKAHEAD - 1 && m - (ZS_MIN_LOOKAHEAD - 1) > tslide) tslide = m - (ZS_MIN_LOOKAHEAD - 1);
-    const uint32_t g1 = min(min(g0 + ZS_FG_STEPS, tslide), n);
+    const uint32_t g1 = min(min(g0 + 64u - (uint32_t)lazy, tslide), n);
     fill_to(g0 + 160u);
 
     // ---- 1. speculative insertion of every lane's position
