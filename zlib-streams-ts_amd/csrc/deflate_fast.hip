@@ -437,8 +437,8 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
 
     FG_T(2);
     // ---- 3. replay of the group.  Each lane's step is precomputed: its symbol, the lane after
-    //         it, and what it inserts (its own position, the inside of a short match).  A scalar
-    //         loop chases the next-lane links to the group's end; then, in parallel, the path's
+    //         it, and what it inserts (its own position, the inside of a short match).  Pointer
+    //         doubling gives every lane's chain of next-lane links to the group's end; then, in parallel, the path's
     //         insertions give each step's truly inserted set (a step only sees positions below
     //         it, all decided by earlier steps), and the first step whose walk met a position the
     //         path skipped -- or whose match needs more than nice + 32 bytes compared -- is found
@@ -480,15 +480,30 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
         in_blk += cnt;
       }
     };
+    // every lane's path to the group's end (the lanes its step chain visits), by pointer doubling:
+    // S(l) = {l, nx(l), nx(nx(l)), ...} with nx absorbing at the end; six ds_bpermute levels instead of a
+    // chain of dependent readlanes, and a restart after a slow step is one more lookup
+    uint32_t slo, shi;
+    {
+      uint64_t S = 1ull << lane;
+      uint32_t J = nextv < j1 ? nextv : lane;
+#pragma unroll
+      for (int k = 0; k < 6; k++) {
+        const int a = (int)(J * 4u);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)S);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(S >> 32));
+        J = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)J);
+        S |= ((uint64_t)hi << 32) | lo;
+      }
+      slo = (uint32_t)S;
+      shi = (uint32_t)(S >> 32);
+    }
     uint32_t j = p - g0;
     while (j < j1) {
-      // chase the lane results' next-lane links (scalar)
-      uint64_t path = 0;
-      uint32_t jj = j;
-      while (jj < j1) {
-        path |= 1ull << jj;
-        jj = (uint32_t)__builtin_amdgcn_readlane((int)nextv, (int)jj);
-      }
+      // the steps from lane j to the group's end, if every lane result on the way holds
+      const uint64_t path = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)shi, (int)j) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)slo, (int)j);
+      const uint32_t jj = (uint32_t)__builtin_amdgcn_readlane((int)nextv, (int)(63u - (uint32_t)__builtin_clzll(path)));
       // in parallel: what the path inserts (its own positions, the inside of its short matches),
       // then the first step whose walk met a position the path skips (or that needs the slow extension)
       const bool onp = (path >> lane) & 1ull;
