@@ -126,10 +126,12 @@ int zs_crc32_batch(zs_ctx *ctx, uint32_t n_streams, const uint8_t *in, const uin
 int zs_adler32_batch(zs_ctx *ctx, uint32_t n_streams, const uint8_t *in, const uint64_t *in_off,
                      const uint32_t *in_len, const uint32_t *seeds, uint32_t *check);
 
-/* Kernel timing of the last batch call on this context (HIP events on the
- * stream the kernels ran on): total device milliseconds and the duration of
- * the named phase ("match", "parse", "trees", "emit", "prev", "inflate", ...).
- * Returns -1 when no timing is available. */
+/* Kernel timing of the batch calls made on this context since the last query
+ * (HIP events on the streams the kernels ran on; the calls themselves never
+ * wait for them, the query does): device milliseconds from the first call's
+ * start to the last call's end, and the summed duration of the named phase
+ * ("sweep", "parse", "trees", "emit", "fast", "inflate_lane", ...).  Returns -1
+ * when no timing is available. */
 double zs_last_batch_ms(zs_ctx *ctx);
 /* Members of the last inflate batch that the lane-per-member path decoded
  * (the rest went through the exact stream-layer state machine).  Synchronizes

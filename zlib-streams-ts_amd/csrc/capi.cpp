@@ -142,7 +142,11 @@ static int mark(zs_ctx* c, hipStream_t st, const char* name) {
     if (r_ != ZS_OK) return r_;                 \
   } while (0)
 
+// Turns the pending marks (of every batch since the last query) into phase
+// times: waits for the last one.  Batch calls never wait for their marks, so a
+// timed sequence of batches runs back to back.
 static void collect_marks(zs_ctx* c) {
+  if (c->marks.empty()) return;  // nothing new: keep the last results
   c->phase_ms.clear();
   c->total_ms = -1;
   if (c->marks.size() < 2) {
@@ -271,7 +275,10 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   } else return fail(ZS_STREAM_ERROR, "unknown option %s", name);
   return ZS_OK;
 }
-double zs_last_batch_ms(zs_ctx* c) { return c->total_ms; }
+double zs_last_batch_ms(zs_ctx* c) {
+  collect_marks(c);
+  return c->total_ms;
+}
 uint32_t zs_last_inflate_lane_count(zs_ctx* c) {
   uint32_t v = 0;
   if (!c || !c->lstat.p || hipStreamSynchronize(c->last_stream) != hipSuccess ||
@@ -280,6 +287,7 @@ uint32_t zs_last_inflate_lane_count(zs_ctx* c) {
   return v;
 }
 double zs_last_phase_ms(zs_ctx* c, const char* phase) {
+  collect_marks(c);
   double t = -1;
   for (auto& p : c->phase_ms)
     if (p.first == phase) t = (t < 0 ? 0 : t) + p.second;
@@ -358,8 +366,7 @@ static int deflate_stored_batch(zs_ctx* c, int wrap, uint32_t n, const uint8_t* 
                                  d_out_len);
   MARK("stored");
   HIPCHK(hipGetLastError());
-  collect_marks(c);
-  return ZS_OK;
+  return ZS_OK;  // timing marks are collected when queried (no wait here)
 }
 
 // The L4..9 parse runs two waves per stream (zs_k_parse_2w: 512-position
@@ -562,8 +569,7 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   }
   MARK("end");
   HIPCHK(hipGetLastError());
-  collect_marks(c);
-  return ZS_OK;
+  return ZS_OK;  // timing marks are collected when queried (no wait here)
 }
 
 // ---------------------------------------------------------- host buffers
@@ -679,8 +685,7 @@ static int checksum_batch(zs_ctx* c, int kind, uint32_t n, const uint8_t* d_in, 
                                   seeds ? (const uint32_t*)(c->meta.as<uint8_t>() + ml.bytes) : nullptr);
   MARK("checksum");
   HIPCHK(hipGetLastError());
-  collect_marks(c);
-  return ZS_OK;
+  return ZS_OK;  // timing marks are collected when queried (no wait here)
 }
 
 extern "C" int zs_crc32_batch_device(zs_ctx* c, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
@@ -974,8 +979,7 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
   c->last_stream = st;
   MARK("finish");
   HIPCHK(hipGetLastError());
-  collect_marks(c);
-  return ZS_OK;
+  return ZS_OK;  // timing marks are collected when queried (no wait here)
 }
 
 extern "C" int zs_inflate_batch(zs_ctx* c, int wbits, uint32_t n, const uint8_t* in, const uint64_t* in_off,
