@@ -447,8 +447,18 @@ def main_inflate(args):
     eng = zsamd.Engine(D.local)
     set_options(eng, args)
     N_glob = S * R
-    lo, hi = shard.shard_range(N_glob, D.world, D.rank)
-    uniq = sorted({i % S for i in range(lo, hi)})
+    # the global member list: the corpus members, with (C5-ii) the reference's deflate64 fixtures
+    # interleaved at fixed places -- sharded as one list, so each fixture is decoded by exactly one rank
+    fx = d64_fixtures() if dec_fmt == "deflate64-raw" else []
+    gstep = max(1, N_glob // max(1, len(fx)))
+    entries = []
+    for i in range(N_glob):
+        if fx and i % gstep == gstep // 2 and i // gstep < len(fx):
+            entries.append(("f", i // gstep))
+        entries.append(("u", i))
+    lo, hi = shard.shard_range(len(entries), D.world, D.rank)
+    mine = entries[lo:hi]
+    uniq = sorted({e[1] % S for e in mine if e[0] == "u"})
     umap = {u: k for k, u in enumerate(uniq)}
     host = bytearray()
     for u in uniq:
@@ -463,16 +473,9 @@ def main_inflate(args):
             if u < len(recs):
                 assert (len(comp[k]), hashlib.sha256(comp[k]).digest()[:16]) == recs[u], "member source %d" % u
                 members_checked += 1
-    members = [comp[umap[i % S]] for i in range(lo, hi)]
-    expect = [("u", umap[i % S]) for i in range(lo, hi)]
-    if dec_fmt == "deflate64-raw":
-        # interleave the reference's deflate64 fixtures (distances > 32 KiB, codes 30/31)
-        fx = d64_fixtures()
-        step_k = max(1, len(members) // max(1, len(fx)))
-        for j, (blob, olen, osha) in enumerate(fx):
-            at = min(len(members), j * step_k + step_k // 2)
-            members.insert(at, blob)
-            expect.insert(at, ("f", olen, osha))
+    # (the fixtures: distances > 32 KiB, codes 30/31)
+    members = [comp[umap[e[1] % S]] if e[0] == "u" else fx[e[1]][0] for e in mine]
+    expect = [("u", umap[e[1] % S]) if e[0] == "u" else ("f", fx[e[1]][1], fx[e[1]][2]) for e in mine]
     N = len(members)
     caps = [L if e[0] == "u" else ((e[1] + 3) & ~3) for e in expect]
     blob = b"".join(members)
@@ -560,7 +563,7 @@ def main_inflate(args):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": "%d members (%d unique %s-corpus %d B buffers x %d%s), %s decode" % (
-                N_glob, S, args.corpus, L, R, " + the 9 reference deflate64 fixtures per rank" if dec_fmt ==
+                N_glob, S, args.corpus, L, R, " + the 9 reference deflate64 fixtures, sharded with them" if dec_fmt ==
                 "deflate64-raw" else "", dec_fmt), "members_per_gpu": N, "compressed_bytes": in_total,
                 "parallelism": "dp%d" % D.world},
             "verify": {"members_checked": checked, "mismatches": bad, "sources_vs_golden": members_checked,
