@@ -45,6 +45,7 @@
 
 #define ZS_SWEEP_MAX 65537u  // position + 1 <= 65535 for every inserted position: u16 members and offsets
 #define ZS_SW_WIN_WORDS ((ZS_SWEEP_MAX + 20u + 3u) / 4u + 2u)
+#define ZS_SW_SIG 11u  // signature bytes compared per chain step (see sw_lcp)
 #define ZS_SW_RING 128u  // records per wave (two blocks of 64 members), stored twice (mirror)
 
 typedef __attribute__((address_space(3))) uint32_t zs_sw_lds_u32;
@@ -241,9 +242,9 @@ static __device__ __forceinline__ uint32_t sw_word(const uint32_t* win, uint32_t
   return __builtin_amdgcn_alignbyte(win[i + 1], win[i], off & 3u);
 }
 
-// exact length of a candidate whose first 12 bytes match, clamped to maxc
+// exact length of a candidate whose first ZS_SW_SIG bytes match, clamped to maxc
 static __device__ __forceinline__ uint32_t sw_extend(const uint32_t* win, uint32_t p, uint32_t q, uint32_t maxc) {
-  uint32_t k = 12;
+  uint32_t k = ZS_SW_SIG;
   while (k < maxc) {
     const uint32_t y = sw_word(win, q + k) ^ sw_word(win, p + k);
     if (y) { k += (uint32_t)(__builtin_ctz(y) >> 3); break; }
@@ -252,15 +253,23 @@ static __device__ __forceinline__ uint32_t sw_extend(const uint32_t* win, uint32
   return k < maxc ? k : maxc;
 }
 
-// matched bytes (0..12) of two 12-byte signatures, capped at kcap / 8
+// Signatures are 11 bytes: a record's third word keeps bytes 8..10 (byte 11
+// zeroed, sw_rec2) and the lane's own third word carries a sentinel bit 24
+// (sw_own2), so the xor of the third words always has bit 24 set.  The
+// matched-byte count then saturates at 11 by itself -- no per-step cap -- and
+// lanes whose lookahead is at most 12 bytes (maxc <= 12, the last positions
+// of a stream) take an exact re-walk after the sweep instead.
+static __device__ __forceinline__ uint32_t sw_rec2(uint32_t w2) { return w2 & 0x00ffffffu; }
+static __device__ __forceinline__ uint32_t sw_own2(uint32_t w2) { return (w2 & 0x00ffffffu) | 0x01000000u; }
+// matched bytes (0..11) of a candidate's record words (a) against the lane's own (b)
 static __device__ __forceinline__ uint32_t sw_lcp(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t b0, uint32_t b1,
-                                                  uint32_t b2, uint32_t kcap) {
+                                                  uint32_t b2) {
   uint32_t f0, f1, f2;
   asm("v_ffbl_b32 %0, %1" : "=v"(f0) : "v"(a0 ^ b0));
   asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e64 %0, %0, 32 clamp" : "=&v"(f1) : "v"(a1 ^ b1));
-  asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e64 %0, %0, 64 clamp" : "=&v"(f2) : "v"(a2 ^ b2));
-  // ffbl(0) = ~0 and the clamped adds keep "no difference" at ~0: the cap wins
-  return min(min(f0, f1), min(f2, kcap)) >> 3;
+  asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e32 %0, 64, %0" : "=&v"(f2) : "v"(a2 ^ b2));
+  // ffbl(0) = ~0 and the clamped add keep "no difference" at ~0; f2 <= 88 (the sentinel)
+  return min(min(f0, f1), f2) >> 3;
 }
 
 struct SwRec {
@@ -325,7 +334,7 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
       const uint32_t q = mem[j];
       r.w0 = sw_word(win, q);
       r.w1 = sw_word(win, q + 4);
-      r.w2 = sw_word(win, q + 8);
+      r.w2 = sw_rec2(sw_word(win, q + 8));
       r.key = (sw_hash(r.w0) << 16) | q;
     }
     put_rec(j, r);
@@ -339,32 +348,35 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
     const int k = k0 + (int)lane;
     const bool own = (uint32_t)k < m;
     const uint32_t p = own ? mem[k] : 0u;
-    const uint32_t s0 = sw_word(win, p), s1 = sw_word(win, p + 4), s2 = sw_word(win, p + 8);
+    const uint32_t s0 = sw_word(win, p), s1 = sw_word(win, p + 4), s2r = sw_word(win, p + 8);
+    const uint32_t s2 = sw_own2(s2r);
     const uint32_t h = sw_hash(s0);
     const uint32_t look = n - p;
     const uint32_t maxc = look < ZS_MAX_MATCH ? look : ZS_MAX_MATCH;                 // deflate.ts:1068
     const uint32_t nice = look < (uint32_t)nice_cfg ? look : (uint32_t)nice_cfg;      // deflate.ts:1078-1080
-    const uint32_t kcap = 8u * (maxc < 12u ? maxc : 12u);
-    const uint32_t long_thr = maxc > 12u ? 12u : 13u;
+    const bool tail = maxc <= 12u;  // exact re-walk after the sweep
+    const uint32_t long_thr = tail ? 12u : ZS_SW_SIG;  // a tail lane records no long candidates
     const uint32_t limit = p > ZS_MAX_DIST ? p - ZS_MAX_DIST : 0u;                   // deflate.ts:1060
     const uint32_t khead = (h << 16) | (limit > 1u ? limit : 1u);
     const uint32_t klim = (h << 16) | limit;
     // ring: this chunk's block and the one before it
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    put_rec(k, own ? SwRec{s0, s1, s2, (h << 16) | p} : SwRec{0, 0, 0, 0});
+    put_rec(k, own ? SwRec{s0, s1, sw_rec2(s2r), (h << 16) | p} : SwRec{0, 0, 0, 0});
     load_rec(k - 64);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
 
     uint32_t best = 2u << 16, best_s = 2u << 16;
     uint32_t nl = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;  // long candidates: t << 16 | pos, in chain order
-    bool ovf = false, alive = false;
+    bool ovf = false;
+    // The live lanes as a wave-uniform lane mask (SGPRs): a chain step is a
+    // compare into a mask, scalar ands and one masked select per lane.
+    uint64_t alive_m = 0;
     uint32_t head = 0;  // bit 0: head candidate valid; 0x8000: at exactly MAX_DIST
     auto note_long = [&](uint32_t t, uint32_t key) {
-      if (nl == 4) {  // a fifth: the lane stops and re-walks its chain afterwards
+      if (nl == 4) {  // a fifth: the lane stops (cleared from alive_m by the caller) and re-walks its chain afterwards
         ovf = true;
-        alive = false;
       } else {
         const uint32_t e = (t << 16) | (key & 0xffffu);
         l0 = nl == 0 ? e : l0;
@@ -377,42 +389,46 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
     // t = 1: the head candidate (deflate.ts:1376)
     {
       const SwRec r = R[(uint32_t)(k - 1) & (ZS_SW_RING - 1)];
+      bool a1 = false;
       if (own && r.key >= khead) {
-        alive = true;
+        a1 = true;
         head = 1u | ((p - (r.key & 0xffffu)) == ZS_MAX_DIST ? 0x8000u : 0u);
-        const uint32_t kk = sw_lcp(r.w0, r.w1, r.w2, s0, s1, s2, kcap);
+        const uint32_t kk = sw_lcp(r.w0, r.w1, r.w2, s0, s1, s2);
         if (kk >= long_thr) note_long(1, r.key);
         best = max(best, (kk << 16) | (0xffffu - 1u));
       }
+      alive_m = __builtin_amdgcn_ballot_w64(a1);
     }
     // One chain step for every lane: a dead lane's result simply stops
     // changing (no per-step exit, no exec-mask bookkeeping).
-    auto step = [&](const uint4 r, uint32_t t, bool& lng) {
-      alive = alive & (r.w > klim);  // the chain ends at the first dead step (deflate.ts:1109)
-      const uint32_t kk = sw_lcp(r.x, r.y, r.z, s0, s1, s2, kcap);
+    auto step = [&](const uint4 r, uint32_t t, uint64_t& lng) {
+      alive_m &= __builtin_amdgcn_ballot_w64(r.w > klim);  // the chain ends at the first dead step (deflate.ts:1109)
+      const uint32_t kk = sw_lcp(r.x, r.y, r.z, s0, s1, s2);
       const uint32_t sc = max(best, (kk << 16) | (0xffffu - t));
-      best = alive ? sc : best;
-      lng = lng | (alive & (kk >= long_thr));
+      asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(sc), "s"(alive_m));
+      lng |= alive_m & __builtin_amdgcn_ballot_w64(kk >= long_thr);
     };
     // Long candidates are rare (~1 % of groups): a group with one is re-run
     // step by step to record them in chain order.
-    auto relong = [&](const SwRec* Rg, uint32_t t0, uint32_t cnt, bool al) {
+    auto relong = [&](const SwRec* Rg, uint32_t t0, uint32_t cnt, uint64_t al_m) {
+      bool al = ((al_m >> lane) & 1u) != 0;
       for (uint32_t u = 0; u < cnt; u++) {
         const SwRec r = Rg[-(int)u];
         al = al && r.key > klim;
-        if (al && sw_lcp(r.w0, r.w1, r.w2, s0, s1, s2, kcap) >= long_thr) {
+        if (al && sw_lcp(r.w0, r.w1, r.w2, s0, s1, s2) >= long_thr) {
           note_long(t0 + u, r.key);
           if (ovf) al = false;
         }
       }
+      alive_m &= ~__builtin_amdgcn_ballot_w64(ovf);
     };
     // Steps 2..4 (block 0, before the first full group).
     {
       const SwRec* const Rg = R + (((uint32_t)(k - 64) & (ZS_SW_RING - 1)) + 64u - 2u);
-      const bool alive0 = alive;
-      bool lng = false;
+      const uint64_t alive0 = alive_m;
+      uint64_t lng = 0;
       for (uint32_t u = 0; u < 3; u++) step(*(const uint4*)(Rg - (int)u), 2u + u, lng);
-      if (__builtin_expect(__builtin_amdgcn_ballot_w64(lng) != 0, 0)) relong(Rg, 2u, 3u, alive0);
+      if (__builtin_expect(lng != 0, 0)) relong(Rg, 2u, 3u, alive0);
     }
     // Steps [ta, tb] of block b in groups of four (ta = 1 mod 4, tb = 0 mod 4,
     // wave-uniform).  Step t reads slot base_b + 64b + 64 - t: one address per
@@ -424,14 +440,14 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
         const SwRec* const Rg = Rb - t0;  // step t0 + u reads Rg[-u]
         const uint4 r0 = *(const uint4*)(Rg), r1 = *(const uint4*)(Rg - 1), r2 = *(const uint4*)(Rg - 2),
                     r3 = *(const uint4*)(Rg - 3);
-        const bool alive0 = alive;
-        bool lng = false;
+        const uint64_t alive0 = alive_m;
+        uint64_t lng = 0;
         step(r0, t0, lng);
         step(r1, t0 + 1, lng);
         step(r2, t0 + 2, lng);
         step(r3, t0 + 3, lng);
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(lng) != 0, 0)) relong(Rg, t0, 4u, alive0);
-        if (!__builtin_amdgcn_ballot_w64(alive)) break;
+        if (__builtin_expect(lng != 0, 0)) relong(Rg, t0, 4u, alive0);
+        if (!alive_m) break;
       }
     };
     bool snapped = false;
@@ -454,7 +470,7 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
       } else {
         run(b, ta, tb);
       }
-      if (tb >= budget || !__builtin_amdgcn_ballot_w64(alive)) break;
+      if (tb >= budget || !alive_m) break;
     }
     if (!snapped) best_s = best;
     __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -462,6 +478,24 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
     if (own) {
       uint32_t rx = 0, ry = 0;
       if (head) {
+        if (tail) {  // maxc <= 12: min(lcp, maxc) exactly, first maximum in chain order (deflate.ts:1082-1105)
+          uint32_t b = 2u << 16, bs = 2u << 16;
+          for (uint32_t t = 1; t <= budget && (int)t <= k; t++) {
+            const uint32_t q = mem[k - (int)t];
+            const uint32_t key = (sw_hash(sw_word(win, q)) << 16) | q;
+            if (t == 1u ? key < khead : key <= klim) break;
+            uint32_t len = 12;
+            for (uint32_t o = 0; o < 12u; o += 4) {
+              const uint32_t y = sw_word(win, q + o) ^ sw_word(win, p + o);
+              if (y) { len = o + (uint32_t)(__builtin_ctz(y) >> 3); break; }
+            }
+            const uint32_t sc = ((len < maxc ? len : maxc) << 16) | (0xffffu - t);
+            b = max(b, sc);
+            if (t <= budget_s) bs = max(bs, sc);
+          }
+          best = b;
+          best_s = bs;
+        }
         const uint32_t bl = best >> 16, bsl = best_s >> 16;
         uint32_t bd = bl > 2u ? p - mem[k - (int)(0xffffu - (best & 0xffffu))] : 0u;
         uint32_t bsd = bsl > 2u ? p - mem[k - (int)(0xffffu - (best_s & 0xffffu))] : 0u;
@@ -477,10 +511,10 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
           if (ovf) {  // re-walk the chain from the first long candidate
             for (uint32_t t = l0 >> 16; t <= budget && (int)t <= k; t++) {
               const uint32_t q = mem[k - (int)t];
-              const uint32_t w0 = sw_word(win, q), w1 = sw_word(win, q + 4), w2 = sw_word(win, q + 8);
+              const uint32_t w0 = sw_word(win, q), w1 = sw_word(win, q + 4), w2 = sw_rec2(sw_word(win, q + 8));
               const uint32_t key = (sw_hash(w0) << 16) | q;
               if (t == 1u ? key < khead : key <= klim) break;
-              if (sw_lcp(w0, w1, w2, s0, s1, s2, kcap) < long_thr) continue;
+              if (sw_lcp(w0, w1, w2, s0, s1, s2) < long_thr) continue;
               if (take(t, q)) break;
             }
           } else {
