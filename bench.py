@@ -142,7 +142,7 @@ def profiled_traffic(kernel, kernel_ms):
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")))  # round directories sort in order
     stale, hit = None, None
-    for f in reversed(files):  # newest round first; among matching durations, the profile with the most launches
+    for f in reversed(files):  # newest round first; among matching durations, the closest
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
@@ -154,8 +154,8 @@ def profiled_traffic(kernel, kernel_ms):
         if abs(prof_ms - kernel_ms) > 0.1 * kernel_ms:
             stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
             continue
-        if hit is None or e.get("calls", 0) > hit[0]:
-            hit = (e.get("calls", 0), int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms))
+        if hit is None or abs(prof_ms - kernel_ms) < hit[0]:  # the closest duration: the profile of this build
+            hit = (abs(prof_ms - kernel_ms), int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms))
     if hit:
         return hit[1], hit[2]
     return None, stale or "no committed profile for %s" % kernel
@@ -173,7 +173,7 @@ def profiled_ceilings(kernel, kernel_ms):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_summary*.json")) +
                    glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")))
     stale, hit = None, None
-    for f in reversed(files):  # newest round first; among matching durations, the summary with the most launches
+    for f in reversed(files):  # newest round first; among matching durations, the closest
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
@@ -185,11 +185,11 @@ def profiled_ceilings(kernel, kernel_ms):
         if abs(prof_ms - kernel_ms) > 0.15 * kernel_ms:
             stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
             continue
-        if hit is None or e.get("dispatches", 0) > hit[0]:
+        if hit is None or abs(prof_ms - kernel_ms) < hit[0]:
             out = {k: e[k] for k in ("lds_bank_conflict_frac", "valu_busy", "active_frac_of_wave_cycles",
                                      "wait_frac_of_wave_cycles", "wait_inst_frac_of_wave_cycles") if k in e}
             out["source"] = "%s (%s avg %.3f ms under --pmc)" % (src, kernel, prof_ms)
-            hit = (e.get("dispatches", 0), out)
+            hit = (abs(prof_ms - kernel_ms), out)
     if hit:
         return hit[1]
     return {"source": stale or "no committed SQ summary for %s" % kernel}

@@ -11,17 +11,20 @@
 //     then members k-1, k-2, ... of its own bucket: the t-th predecessor is
 //     the t-th chain step, no links are followed.
 //   * the sweep: for t = 1, 2, ... every lane compares its position with the
-//     t-th predecessor's 12-byte signature; a candidate is alive while
+//     t-th predecessor's 11-byte signature (SIG; the kernel's sentinel bit
+//     saturates the matched-byte count at 11); a candidate is alive while
 //     key = hash << 16 | pos passes the head test (t = 1: non-NIL, distance
 //     <= MAX_DIST, deflate.ts:1376) or the chain test (t >= 2: pos > limit,
 //     deflate.ts:1109) and t <= budget; liveness is monotone in t.
-//   * a candidate whose 12 signature bytes all match (and maxc > 12) is "long":
+//   * a candidate whose 11 signature bytes all match (and maxc > 12) is "long":
 //     up to 4 are recorded (t, pos) and extended afterwards in chain order
 //     with the nice cut-off (deflate.ts:1100-1105); a fifth ends the lane's
 //     sweep and the lane re-walks its chain from the first long candidate.
 //   * short candidates keep the first max of (len, -t) (first strictly longer
 //     wins), clamped to maxc (deflate.ts:1068); when any long candidate is
 //     within the budget the result comes from the long ones only.
+//   * lanes with maxc <= 12 (the last positions of a stream) record no long
+//     candidates; their result is an exact re-walk, min(lcp, maxc), first max.
 // Test infrastructure (tests/test_emu_sweep.py); it checks the algorithm off
 // the GPU, not the kernel binary (tests/test_gpu_deflate.py does that).
 //
@@ -32,6 +35,7 @@
 #include <string.h>
 #define MAXD 32506u
 #define NLONG 4
+#define SIG 11u
 
 static uint8_t buf[65536 + 300];
 static int32_t head[32768], prev[65536];
@@ -61,15 +65,15 @@ static uint32_t ref_lm(uint32_t n, uint32_t p, uint32_t budget, uint32_t nice_cf
   return (bl << 16) | (bl > 2 ? bd : 0);
 }
 
-static uint32_t lcp12(uint32_t a, uint32_t b) {
+static uint32_t lcp_sig(uint32_t a, uint32_t b) {
   uint32_t k = 0;
-  while (k < 12 && buf[a + k] == buf[b + k]) k++;
+  while (k < SIG && buf[a + k] == buf[b + k]) k++;
   return k;
 }
 
-// exact length of a long candidate (>= 12 equal bytes), clamped to maxc
+// exact length of a long candidate (>= SIG equal bytes), clamped to maxc
 static uint32_t extend(uint32_t p, uint32_t q, uint32_t maxc) {
-  uint32_t k = 12;
+  uint32_t k = SIG;
   while (k < maxc && buf[q + k] == buf[p + k]) k++;
   return k < maxc ? k : maxc;
 }
@@ -107,7 +111,8 @@ int main(int argc, char** argv) {
     for (uint32_t k = 0; k < m; k++) {
       const uint32_t p = mem[k], h = hash3(p);
       const uint32_t look = n - p, maxc = look < 258 ? look : 258, nice = look < nice_cfg ? look : nice_cfg;
-      const uint32_t kcap = maxc < 12 ? maxc : 12, long_thr = maxc > 12 ? 12 : 13;
+      const int tail = maxc <= 12;
+      const uint32_t long_thr = tail ? 12 : SIG;
       const uint32_t limit = p > MAXD ? p - MAXD : 0;
       const uint32_t khead = (h << 16) | (limit > 1 ? limit : 1), klim = (h << 16) | limit;
       uint32_t best = 2u << 16, best_s = best, nl = 0, lt[NLONG], lq[NLONG], flag = 0, t_end = 0;
@@ -118,8 +123,7 @@ int main(int argc, char** argv) {
         if (t == 1) { headok = 1; flag = (p - q == MAXD) ? 0x8000u : 0u; }
         steps++;
         t_end = t;
-        uint32_t kk = lcp12(p, q);
-        kk = kk < kcap ? kk : kcap;
+        const uint32_t kk = lcp_sig(p, q);
         if (kk >= long_thr) {
           if (nl == NLONG) { ovf = 1; break; }
           lt[nl] = t; lq[nl] = q; nl++;
@@ -130,6 +134,18 @@ int main(int argc, char** argv) {
       }
       if (t_end < chain_s) best_s = best;
       uint32_t rx = 0, ry = 0;
+      if (headok && tail) {  // exact re-walk (deflate_sweep.hip: the tail lanes)
+        best = best_s = 2u << 16;
+        for (uint32_t t = 1; t <= chain && t <= k; t++) {
+          const uint32_t q = mem[k - t], key = (hash3(q) << 16) | q;
+          if (t == 1 ? key < khead : key <= klim) break;
+          uint32_t L = 0;
+          while (L < 12 && buf[q + L] == buf[p + L]) L++;
+          const uint32_t score = ((L < maxc ? L : maxc) << 16) | (0xffffu - t);
+          if (score > best) best = score;
+          if (t <= chain_s && score > best_s) best_s = score;
+        }
+      }
       if (headok) {
         uint32_t bl = best >> 16, bd = bl > 2 ? p - mem[k - (0xffffu - (best & 0xffffu))] : 0;
         uint32_t bsl = best_s >> 16, bsd = bsl > 2 ? p - mem[k - (0xffffu - (best_s & 0xffffu))] : 0;
@@ -141,7 +157,7 @@ int main(int argc, char** argv) {
             for (uint32_t t = lt[0]; t <= chain && t <= k; t++) {
               const uint32_t q = mem[k - t], key = (hash3(q) << 16) | q;
               if (t == 1 ? key < khead : key <= klim) break;
-              if (lcp12(p, q) < long_thr) continue;
+              if (lcp_sig(p, q) < long_thr) continue;
               const uint32_t L = extend(p, q, maxc);
               if (L > lb) { lb = L; ld = p - q; }
               if (t <= chain_s && L > lbs) { lbs = L; lds = p - q; }

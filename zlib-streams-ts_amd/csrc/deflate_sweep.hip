@@ -18,7 +18,7 @@
 // 2, ... for all 64 lanes at once: lane i reads the record of member
 // k0 + i - t from a per-wave LDS ring (consecutive lanes, consecutive 16-byte
 // records: conflict-free, and no load depends on the previous step), compares
-// the 8-byte signatures with xor + ffbl, and keeps the first maximum.
+// the 11-byte signatures with xor + ffbl, and keeps the first maximum.
 //
 // Exactness (checked off the GPU by tools/emu/emu_bucket_sweep.c against a
 // direct longest_match, and on the GPU by tests/test_gpu_deflate.py):
@@ -29,13 +29,14 @@
 //     monotone in t, so a lane leaves at its first dead step.
 //   * first strictly longer match wins (deflate.ts:1100-1105): the best is the
 //     maximum of (len << 16) | (0xffff - t).  Lengths are clamped to maxc =
-//     min(258, lookahead) (deflate.ts:1068) through the min3 below.
-//   * a candidate whose 12 signature bytes all match (maxc > 12) is "long":
+//     min(258, lookahead) (deflate.ts:1068): short candidates match at most
+//     10 bytes, and a lane with maxc <= 12 re-walks its chain exactly.
+//   * a candidate whose 11 signature bytes all match (maxc > 12) is "long":
 //     its exact length needs the window.  Up to four are recorded in chain
 //     order and extended after the sweep, with the nice cut-off (nice >= 16 at
 //     levels 4..9, so no short candidate reaches it unless the stream ends
 //     first, where maxc clamps it); when one exists within the budget the
-//     result is among them (every short one is <= 12).
+//     result is among them (every short one is <= 10).
 //     A fifth long candidate ends the lane's sweep, and the lane re-walks its
 //     chain from the first long one (repetitive data: the first is usually a
 //     nice match).
