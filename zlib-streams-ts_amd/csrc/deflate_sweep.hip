@@ -402,12 +402,15 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
     }
     // One chain step for every lane: a dead lane's result simply stops
     // changing (no per-step exit, no exec-mask bookkeeping).
-    auto step = [&](const uint4 r, uint32_t t, uint64_t& lng) {
+    // A step returns its score, 0 for a dead lane (below every best); the
+    // caller folds two steps at a time into best with one v_max3.
+    auto step = [&](const uint4 r, uint32_t t, uint64_t& lng) -> uint32_t {
       alive_m &= __builtin_amdgcn_ballot_w64(r.w > klim);  // the chain ends at the first dead step (deflate.ts:1109)
       const uint32_t kk = sw_lcp(r.x, r.y, r.z, s0, s1, s2);
-      const uint32_t sc = max(best, (kk << 16) | (0xffffu - t));
-      asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(best) : "v"(best), "v"(sc), "s"(alive_m));
+      uint32_t sc;
+      asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(sc) : "v"((kk << 16) | (0xffffu - t)), "s"(alive_m));
       lng |= alive_m & __builtin_amdgcn_ballot_w64(kk >= long_thr);
+      return sc;
     };
     // Long candidates are rare (~1 % of groups): a group with one is re-run
     // step by step to record them in chain order.
@@ -428,7 +431,7 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
       const SwRec* const Rg = R + (((uint32_t)(k - 64) & (ZS_SW_RING - 1)) + 64u - 2u);
       const uint64_t alive0 = alive_m;
       uint64_t lng = 0;
-      for (uint32_t u = 0; u < 3; u++) step(*(const uint4*)(Rg - (int)u), 2u + u, lng);
+      for (uint32_t u = 0; u < 3; u++) best = max(best, step(*(const uint4*)(Rg - (int)u), 2u + u, lng));
       if (__builtin_expect(lng != 0, 0)) relong(Rg, 2u, 3u, alive0);
     }
     // Steps [ta, tb] of block b in groups of four (ta = 1 mod 4, tb = 0 mod 4,
@@ -443,10 +446,10 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
                     r3 = *(const uint4*)(Rg - 3);
         const uint64_t alive0 = alive_m;
         uint64_t lng = 0;
-        step(r0, t0, lng);
-        step(r1, t0 + 1, lng);
-        step(r2, t0 + 2, lng);
-        step(r3, t0 + 3, lng);
+        const uint32_t c0 = step(r0, t0, lng), c1 = step(r1, t0 + 1, lng);
+        const uint32_t c2 = step(r2, t0 + 2, lng), c3 = step(r3, t0 + 3, lng);
+        best = max(max(best, c0), c1);
+        best = max(max(best, c2), c3);
         if (__builtin_expect(lng != 0, 0)) relong(Rg, t0, 4u, alive0);
         if (!alive_m) break;
       }
