@@ -133,7 +133,24 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def profiled_traffic(kernel, kernel_ms):
+def profile_tag(args):
+    """The config name the committed profiles carry (profiles/<round>/summary_<tag>.json)."""
+    if args.mode == "inflate":
+        return {"gzip": "c5_gunzip", "deflate64-raw": "c5_d64"}.get(args.format, "c3")
+    if args.format == "gzip":
+        return "c5_gzip_l%d" % args.level
+    return "c2" if args.stream_bytes == 65536 else "c4_l%d" % args.level
+
+
+def _tagged_first(files, tag):
+    """The files of this config (name contains _<tag>.) after the others, so the newest-first scan sees them first."""
+    if not tag:
+        return files
+    mine = [f for f in files if ("_%s." % tag) in os.path.basename(f)]
+    return [f for f in files if f not in mine] + mine
+
+
+def profiled_traffic(kernel, kernel_ms, tag=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3
     summary (profiles/*/summary*.json: FETCH_SIZE / WRITE_SIZE passes, gfx950
     read correction by tools/summarize_profile.py) -- used only when that
@@ -141,8 +158,9 @@ def profiled_traffic(kernel, kernel_ms):
     within 10 % (i.e. it profiled this build); otherwise (None, reason)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")))  # round directories sort in order
+    files = _tagged_first(files, tag)
     stale, hit = None, None
-    for f in reversed(files):  # newest round first; among matching durations, the closest
+    for f in reversed(files):  # this config's files first, newest round first; the first matching duration
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
@@ -154,14 +172,14 @@ def profiled_traffic(kernel, kernel_ms):
         if abs(prof_ms - kernel_ms) > 0.1 * kernel_ms:
             stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
             continue
-        if hit is None or abs(prof_ms - kernel_ms) < hit[0]:  # the closest duration: the profile of this build
-            hit = (abs(prof_ms - kernel_ms), int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms))
+        if hit is None:  # this config's newest matching profile, else the newest matching one
+            hit = (0, int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms))
     if hit:
         return hit[1], hit[2]
     return None, stale or "no committed profile for %s" % kernel
 
 
-def profiled_ceilings(kernel, kernel_ms):
+def profiled_ceilings(kernel, kernel_ms, tag=None):
     """The SQ-counter ratios that bound `kernel` below the HBM roofline, from the
     newest committed tools/pmc_sq.sh summary (profiles/*/sq_summary*.json,
     written by tools/sq_summary.py --json): LDS bank-conflict cycles over LDS
@@ -172,8 +190,9 @@ def profiled_ceilings(kernel, kernel_ms):
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_summary*.json")) +
                    glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")))
+    files = _tagged_first(files, tag)
     stale, hit = None, None
-    for f in reversed(files):  # newest round first; among matching durations, the closest
+    for f in reversed(files):  # this config's files first, newest round first; the first matching duration
         try:
             e = json.load(open(f)).get(kernel)
         except (OSError, ValueError):
@@ -185,11 +204,11 @@ def profiled_ceilings(kernel, kernel_ms):
         if abs(prof_ms - kernel_ms) > 0.15 * kernel_ms:
             stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
             continue
-        if hit is None or abs(prof_ms - kernel_ms) < hit[0]:
+        if hit is None:
             out = {k: e[k] for k in ("lds_bank_conflict_frac", "valu_busy", "active_frac_of_wave_cycles",
                                      "wait_frac_of_wave_cycles", "wait_inst_frac_of_wave_cycles") if k in e}
             out["source"] = "%s (%s avg %.3f ms under --pmc)" % (src, kernel, prof_ms)
-            hit = (abs(prof_ms - kernel_ms), out)
+            hit = (0, out)
     if hit:
         return hit[1]
     return {"source": stale or "no committed SQ summary for %s" % kernel}
@@ -384,12 +403,12 @@ def main():
             # bytes_in + bytes_out per stream x streams per launch (this rank's shard)
             alg = S * L + out_local
             achieved = alg / (phase_avg[dom] / 1e3) / 1e9
-            traffic, tsrc = profiled_traffic("zs_k_" + dom, phase_avg[dom])
+            traffic, tsrc = profiled_traffic("zs_k_" + dom, phase_avg[dom], profile_tag(args))
             roof = {"bound": "hbm", "kernel": "zs_k_" + dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "traffic_source": tsrc, "algorithmic_bytes": alg, "kernel_ms": phase_avg[dom],
                     "phase_ms": phase_avg, "pipeline_ms": round(sum(phase_avg.values()), 4),
-                    "ceilings": profiled_ceilings("zs_k_" + dom, phase_avg[dom])}
+                    "ceilings": profiled_ceilings("zs_k_" + dom, phase_avg[dom], profile_tag(args))}
         cpu = None
         if not (args.no_cpu_baseline or D.world > 1):
             import oracle
@@ -548,7 +567,7 @@ def main_inflate(args):
             olen = d_len.cpu().tolist()
             alg = sum(len(m) + olen[i] for i, m in enumerate(members) if len(m) > wmin)
         achieved = alg / (k_ms / 1e3) / 1e9
-        traffic, tsrc = profiled_traffic("zs_k_" + dom, k_ms)
+        traffic, tsrc = profiled_traffic("zs_k_" + dom, k_ms, profile_tag(args))
         cpu = None
         if not (args.no_cpu_baseline or D.world > 1):
             import oracle
@@ -572,7 +591,7 @@ def main_inflate(args):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg,
                          "kernel_ms": round(k_ms, 4), "phase_ms": phase_avg,
-                         "ceilings": profiled_ceilings("zs_k_" + dom, k_ms)},
+                         "ceilings": profiled_ceilings("zs_k_" + dom, k_ms, profile_tag(args))},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
