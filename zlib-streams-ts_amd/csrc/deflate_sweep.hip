@@ -402,14 +402,18 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
     }
     // One chain step for every lane: a dead lane's result simply stops
     // changing (no per-step exit, no exec-mask bookkeeping).
-    // A step returns its score, 0 for a dead lane (below every best); the
-    // caller folds two steps at a time into best with one v_max3.
-    auto step = [&](const uint4 r, uint32_t t, uint64_t& lng) -> uint32_t {
+    // A step returns its score, 0 for a dead lane (below every best).  The
+    // caller takes the maximum of a group's scores (v_max3), folds it into
+    // best with one v_max, and finds the group's long candidates from it: a
+    // live long candidate scores at least long_thr << 16, a dead one 0.
+    const uint32_t long16 = long_thr << 16;
+    auto step = [&](const uint4 r, uint32_t t) -> uint32_t {
       alive_m &= __builtin_amdgcn_ballot_w64(r.w > klim);  // the chain ends at the first dead step (deflate.ts:1109)
       const uint32_t kk = sw_lcp(r.x, r.y, r.z, s0, s1, s2);
-      uint32_t sc;
-      asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(sc) : "v"((kk << 16) | (0xffffu - t)), "s"(alive_m));
-      lng |= alive_m & __builtin_amdgcn_ballot_w64(kk >= long_thr);
+      uint32_t sc, sl;
+      // one v_lshl_or (the compiler would otherwise fold the >> 3 into a shift, an and and an or)
+      asm("v_lshl_or_b32 %0, %1, 16, %2" : "=v"(sl) : "v"(kk), "s"(0xffffu - t));
+      asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(sc) : "v"(sl), "s"(alive_m));
       return sc;
     };
     // Long candidates are rare (~1 % of groups): a group with one is re-run
@@ -430,9 +434,10 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
     {
       const SwRec* const Rg = R + (((uint32_t)(k - 64) & (ZS_SW_RING - 1)) + 64u - 2u);
       const uint64_t alive0 = alive_m;
-      uint64_t lng = 0;
-      for (uint32_t u = 0; u < 3; u++) best = max(best, step(*(const uint4*)(Rg - (int)u), 2u + u, lng));
-      if (__builtin_expect(lng != 0, 0)) relong(Rg, 2u, 3u, alive0);
+      uint32_t gm = 0;
+      for (uint32_t u = 0; u < 3; u++) gm = max(gm, step(*(const uint4*)(Rg - (int)u), 2u + u));
+      best = max(best, gm);
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(gm >= long16) != 0, 0)) relong(Rg, 2u, 3u, alive0);
     }
     // Steps [ta, tb] of block b in groups of four (ta = 1 mod 4, tb = 0 mod 4,
     // wave-uniform).  Step t reads slot base_b + 64b + 64 - t: one address per
@@ -445,12 +450,11 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
         const uint4 r0 = *(const uint4*)(Rg), r1 = *(const uint4*)(Rg - 1), r2 = *(const uint4*)(Rg - 2),
                     r3 = *(const uint4*)(Rg - 3);
         const uint64_t alive0 = alive_m;
-        uint64_t lng = 0;
-        const uint32_t c0 = step(r0, t0, lng), c1 = step(r1, t0 + 1, lng);
-        const uint32_t c2 = step(r2, t0 + 2, lng), c3 = step(r3, t0 + 3, lng);
-        best = max(max(best, c0), c1);
-        best = max(max(best, c2), c3);
-        if (__builtin_expect(lng != 0, 0)) relong(Rg, t0, 4u, alive0);
+        const uint32_t c0 = step(r0, t0), c1 = step(r1, t0 + 1);
+        const uint32_t c2 = step(r2, t0 + 2), c3 = step(r3, t0 + 3);
+        const uint32_t gm = max(max(c0, c1), max(c2, c3));
+        best = max(best, gm);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(gm >= long16) != 0, 0)) relong(Rg, t0, 4u, alive0);
         if (!alive_m) break;
       }
     };
