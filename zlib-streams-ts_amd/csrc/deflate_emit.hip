@@ -92,60 +92,6 @@ static __device__ void zs_pqdownheap(zs_tstate& t, int k) {
   hk[k] = v;
 }
 
-static __device__ void zs_gen_bitlen(zs_tstate& t, zs_tdesc& d) {  // trees.ts:187-259
-  int16_t* heap = t.w->heap;
-  uint16_t* bl_count = t.w->bl_count;
-  int h, n, m, bits, xbits, overflow = 0;
-  for (bits = 0; bits <= 15; bits++) bl_count[bits] = 0;
-  d.len[heap[t.heap_max]] = 0;
-  // heap[] and dad[] do not change here: read 8 entries and their parents
-  // ahead, so the loop's only dependent LDS read is len[parent]
-  for (int h0 = t.heap_max + 1; h0 < ZS_HEAP_SIZE; h0 += 8) {
-    int nb[8];
-    uint32_t db[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) nb[u] = h0 + u < ZS_HEAP_SIZE ? heap[h0 + u] : 0;
-#pragma unroll
-    for (int u = 0; u < 8; u++) db[u] = d.dad[nb[u]];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      if (h0 + u >= ZS_HEAP_SIZE) break;
-      n = nb[u];
-      bits = d.len[db[u]] + 1;
-      if (bits > d.max_length) { bits = d.max_length; overflow++; }
-      d.len[n] = (uint16_t)bits;
-      if (n > d.max_code) continue;
-      bl_count[bits]++;
-      xbits = n >= d.extra_base ? d.extra[n - d.extra_base] : 0;
-      const uint32_t f = d.freq[n];
-      t.opt_len += f * (uint32_t)(bits + xbits);
-      if (d.stat) t.static_len += f * ((d.stat[n] >> 16) + (uint32_t)xbits);
-    }
-  }
-  h = ZS_HEAP_SIZE;
-  if (overflow == 0) return;
-  do {
-    bits = d.max_length - 1;
-    while (bl_count[bits] == 0) bits--;
-    bl_count[bits]--;
-    bl_count[bits + 1] += 2;
-    bl_count[d.max_length]--;
-    overflow -= 2;
-  } while (overflow > 0);
-  for (bits = d.max_length; bits != 0; bits--) {
-    n = bl_count[bits];
-    while (n != 0) {
-      m = heap[--h];
-      if (m > d.max_code) continue;
-      if (d.len[m] != bits) {
-        t.opt_len += (uint32_t)((bits - (int)d.len[m]) * (int)d.freq[m]);
-        d.len[m] = (uint16_t)bits;
-      }
-      n--;
-    }
-  }
-}
-
 // gen_codes (trees.ts:54-76) by the wave: symbol n's code is the first code of
 // its length plus the number of symbols m < n of the same length, counted
 // with one ballot per length over 64 symbols at a time.  All lanes call it.
@@ -210,7 +156,102 @@ static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:2
     zs_pqdownheap(t, 1);
   } while (t.heap_len >= 2);
   heap[--t.heap_max] = (int16_t)(hk[1] & 1023u);
-  zs_gen_bitlen(t, d);  // the codes follow by the wave (zs_gen_codes_wave)
+  // the bit lengths follow by the wave (zs_gen_bitlen_wave), then the codes (zs_gen_codes_wave)
+}
+
+// gen_bitlen (trees.ts:187-259) by the wave.  Without overflow a node's
+// length is its depth, so the depths come from pointer jumping over dad[]
+// (anc/dep in the free hk[] words, a few synchronous rounds instead of one
+// dependent LDS round trip per node); lengths clamp at max_length, and
+// overflow counts every non-root node deeper than max_length -- the nodes the
+// serial loop clamps.  bl_count, opt_len and static_len are the same sums.
+// The overflow repair (rare) stays serial on lane 0.  All lanes call it after
+// zs_build_tree on lane 0 (t.heap_max, d.max_code: lane 0's).
+#define ZS_GB_PER_LANE ((ZS_HEAP_SIZE + 63) / 64)
+static __device__ void zs_gen_bitlen_wave(zs_tstate& t, zs_tdesc& d, uint32_t lane) {
+  int16_t* heap = t.w->heap;
+  uint16_t* bl_count = t.w->bl_count;
+  uint32_t* anc = t.w->hk;  // free after the build: anc[node] = ancestor << 16 | depth to it
+  const int hm = __builtin_amdgcn_readlane(t.heap_max, 0);
+  const int max_code = __builtin_amdgcn_readlane(d.max_code, 0);
+  const int root = heap[hm];
+  if (lane < 16) bl_count[lane] = 0;
+  int nd[ZS_GB_PER_LANE];
+#pragma unroll
+  for (int r = 0; r < ZS_GB_PER_LANE; r++) {
+    const int h = hm + (int)lane + 64 * r;
+    nd[r] = h < ZS_HEAP_SIZE ? heap[h] : -1;
+    if (nd[r] >= 0) anc[nd[r]] = nd[r] == root ? (uint32_t)root << 16 : ((uint32_t)d.dad[nd[r]] << 16) | 1u;
+  }
+  __syncthreads();
+  for (int round = 0; round < 10; round++) {  // depth <= ZS_HEAP_SIZE < 2^10
+    uint32_t nv[ZS_GB_PER_LANE];
+    bool moved = false;
+#pragma unroll
+    for (int r = 0; r < ZS_GB_PER_LANE; r++) {
+      nv[r] = 0;
+      if (nd[r] < 0) continue;
+      const uint32_t e = anc[nd[r]], a = e >> 16;
+      if ((int)a == root) { nv[r] = e; continue; }
+      const uint32_t f = anc[a];
+      nv[r] = (f & 0xffff0000u) | ((e & 0xffffu) + (f & 0xffffu));
+      moved = true;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < ZS_GB_PER_LANE; r++)
+      if (nd[r] >= 0) anc[nd[r]] = nv[r];
+    __syncthreads();
+    if (!__builtin_amdgcn_ballot_w64(moved)) break;
+  }
+  uint32_t opt = 0, stat = 0;
+  int overflow = 0;
+#pragma unroll
+  for (int r = 0; r < ZS_GB_PER_LANE; r++) {
+    const int n = nd[r];
+    if (n < 0) continue;
+    if (n == root) { d.len[n] = 0; continue; }
+    int bits = (int)(anc[n] & 0xffffu);
+    if (bits > d.max_length) { bits = d.max_length; overflow++; }
+    d.len[n] = (uint16_t)bits;
+    if (n > max_code) continue;
+    atomicAdd(reinterpret_cast<uint32_t*>(&bl_count[bits & ~1]), 1u << (16 * (bits & 1)));
+    const int xbits = n >= d.extra_base ? d.extra[n - d.extra_base] : 0;
+    const uint32_t f = d.freq[n];
+    opt += f * (uint32_t)(bits + xbits);
+    if (d.stat) stat += f * ((d.stat[n] >> 16) + (uint32_t)xbits);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    opt += __shfl_xor(opt, o, 64);
+    stat += __shfl_xor(stat, o, 64);
+    overflow += __shfl_xor(overflow, o, 64);
+  }
+  t.opt_len += opt;
+  t.static_len += stat;
+  __syncthreads();
+  if (overflow == 0 || lane != 0) return;
+  int bits, n, m, h = ZS_HEAP_SIZE;  // trees.ts:222-258, serial
+  do {
+    bits = d.max_length - 1;
+    while (bl_count[bits] == 0) bits--;
+    bl_count[bits]--;
+    bl_count[bits + 1] += 2;
+    bl_count[d.max_length]--;
+    overflow -= 2;
+  } while (overflow > 0);
+  for (bits = d.max_length; bits != 0; bits--) {
+    n = bl_count[bits];
+    while (n != 0) {
+      m = heap[--h];
+      if (m > d.max_code) continue;
+      if (d.len[m] != bits) {
+        t.opt_len += (uint32_t)((bits - (int)d.len[m]) * (int)d.freq[m]);
+        d.len[m] = (uint16_t)bits;
+      }
+      n--;
+    }
+  }
 }
 
 static __device__ __forceinline__ void zs_hput(zs_tstate& t, uint32_t v, int n) {
@@ -362,9 +403,13 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   B.extra = ZS_EXTRA_BLBITS;
   if (lane == 0) zs_build_tree(t, L);
   __syncthreads();
+  zs_gen_bitlen_wave(t, L, lane);
+  __syncthreads();
   zs_gen_codes_wave(w.bl_count, w.llen, w.lcode, __builtin_amdgcn_readlane(L.max_code, 0), lane);
   __syncthreads();
   if (lane == 0) zs_build_tree(t, D);
+  __syncthreads();
+  zs_gen_bitlen_wave(t, D, lane);
   __syncthreads();
   zs_gen_codes_wave(w.bl_count, w.dlen, w.dcode, __builtin_amdgcn_readlane(D.max_code, 0), lane);
   __syncthreads();
@@ -382,6 +427,8 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   if (lane < ZS_BL_CODES) w.bfreq[lane] = (uint16_t)(w.bfreq[lane] + w.b32[lane]);
   __syncthreads();
   if (lane == 0) zs_build_tree(t, B);
+  __syncthreads();
+  zs_gen_bitlen_wave(t, B, lane);
   __syncthreads();
   zs_gen_codes_wave(w.bl_count, w.blen, w.bcode, __builtin_amdgcn_readlane(B.max_code, 0), lane);
   __syncthreads();
