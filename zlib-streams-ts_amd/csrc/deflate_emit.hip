@@ -2,9 +2,9 @@
 //
 //   zs_k_trees  : one wave per block.  The wave histograms the block's symbols
 //                 with LDS atomics; lane 0 then runs the serial heart of the
-//                 reference's exact tree construction (heap ordered by freq
-//                 then depth, bit lengths with overflow repair --
-//                 trees.ts:167-316), the tree run-length coding
+//                 reference's exact tree construction (the heap ordered by freq
+//                 then depth, trees.ts:167-316; the bit lengths follow by the
+//                 wave, with lane 0's overflow repair), the tree run-length coding
 //                 (trees.ts:318-447) and the stored/static/dynamic choice
 //                 (trees.ts:554-583); the wave does the rest in parallel
 //                 (frequency set-up, canonical codes by per-length ballots,
