@@ -119,16 +119,33 @@ static __device__ void zs_gen_codes_wave(const uint16_t* bl_count, const uint16_
   }
 }
 
-static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:261-316, lane 0
+// the leaves in symbol order (trees.ts:276-284) by the wave: heap entry i is
+// the i-th symbol with a nonzero frequency, placed by a ballot prefix; all
+// lanes call it, before zs_build_tree on lane 0
+static __device__ void zs_tree_leaves_wave(zs_tstate& t, zs_tdesc& d, uint32_t lane) {
+  uint32_t* hk = t.w->hk;
+  const uint64_t below = (1ull << lane) - 1ull;
+  int hl = 0, max_code = -1;
+  for (int n0 = 0; n0 < d.elems; n0 += 64) {
+    const int n = n0 + (int)lane;
+    const uint32_t f = n < d.elems ? d.freq[n] : 0u;
+    const uint64_t m = __ballot(f != 0u);
+    if (n < d.elems) {
+      if (f) hk[hl + 1 + __popcll(m & below)] = (f << 17) | (uint32_t)n;
+      else d.len[n] = 0;
+    }
+    if (m) max_code = n0 + 63 - (int)__clzll(m);
+    hl += __popcll(m);
+  }
+  t.heap_len = hl;
+  d.max_code = max_code;
+}
+
+static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:285-316, lane 0 (leaves placed)
   int16_t* heap = t.w->heap;
   uint32_t* hk = t.w->hk;
-  int n, max_code = -1, node;
-  t.heap_len = 0;
+  int n, max_code = d.max_code, node;
   t.heap_max = ZS_HEAP_SIZE;
-  for (n = 0; n < d.elems; n++) {
-    if (d.freq[n] != 0) hk[++t.heap_len] = ((uint32_t)d.freq[n] << 17) | (uint32_t)(max_code = n);
-    else d.len[n] = 0;
-  }
   while (t.heap_len < 2) {
     node = max_code < 2 ? ++max_code : 0;
     hk[++t.heap_len] = (1u << 17) | (uint32_t)node;
@@ -401,11 +418,15 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   zs_tdesc D = {w.dfreq, w.dlen, w.ddad, w.dcode, ZS_STATIC_DTREE, ZS_EXTRA_DBITS, 0, ZS_D_CODES, 15, 0};
   zs_tdesc B = {w.bfreq, w.blen, w.bdad, w.bcode, nullptr, nullptr, 0, ZS_BL_CODES, 7, 0};
   B.extra = ZS_EXTRA_BLBITS;
+  zs_tree_leaves_wave(t, L, lane);
+  __syncthreads();
   if (lane == 0) zs_build_tree(t, L);
   __syncthreads();
   zs_gen_bitlen_wave(t, L, lane);
   __syncthreads();
   zs_gen_codes_wave(w.bl_count, w.llen, w.lcode, __builtin_amdgcn_readlane(L.max_code, 0), lane);
+  __syncthreads();
+  zs_tree_leaves_wave(t, D, lane);
   __syncthreads();
   if (lane == 0) zs_build_tree(t, D);
   __syncthreads();
@@ -425,6 +446,8 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   zs_scan_tree_wave(w.dlen, dmax, w.b32, lane);
   __syncthreads();
   if (lane < ZS_BL_CODES) w.bfreq[lane] = (uint16_t)(w.bfreq[lane] + w.b32[lane]);
+  __syncthreads();
+  zs_tree_leaves_wave(t, B, lane);
   __syncthreads();
   if (lane == 0) zs_build_tree(t, B);
   __syncthreads();
