@@ -141,20 +141,39 @@ static __device__ void zs_tree_leaves_wave(zs_tstate& t, zs_tdesc& d, uint32_t l
   d.max_code = max_code;
 }
 
-static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:285-316, lane 0 (leaves placed)
-  int16_t* heap = t.w->heap;
+// trees.ts:290-304 by the wave (after zs_tree_leaves_wave): the padding to two
+// nodes (wave-uniform; lane 0 stores), then the heapify level by level from the
+// deepest: the sequential n = heap_len / 2 .. 1 order sifts every deeper node
+// before a shallower one, and the nodes of one level own disjoint subtrees,
+// so sifting a level's nodes at once (one lane each) gives the same heap
+static __device__ void zs_tree_heapify_wave(zs_tstate& t, zs_tdesc& d, uint32_t lane) {
   uint32_t* hk = t.w->hk;
-  int n, max_code = d.max_code, node;
-  t.heap_max = ZS_HEAP_SIZE;
+  int max_code = d.max_code;
   while (t.heap_len < 2) {
-    node = max_code < 2 ? ++max_code : 0;
-    hk[++t.heap_len] = (1u << 17) | (uint32_t)node;
-    d.freq[node] = 1;
+    const int node = max_code < 2 ? ++max_code : 0;
+    ++t.heap_len;
+    if (lane == 0) {
+      hk[t.heap_len] = (1u << 17) | (uint32_t)node;
+      d.freq[node] = 1;
+    }
     t.opt_len--;
     if (d.stat) t.static_len -= d.stat[node] >> 16;
   }
   d.max_code = max_code;
-  for (n = t.heap_len / 2; n >= 1; n--) zs_pqdownheap(t, n);
+  __syncthreads();
+  const int last = t.heap_len / 2;
+  for (int lv = 31 - __clz(last); lv >= 0; lv--) {
+    const int hi = min((2 << lv) - 1, last);
+    for (int n = (1 << lv) + (int)lane; n <= hi; n += 64) zs_pqdownheap(t, n);
+    __syncthreads();
+  }
+}
+
+static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:305-316, lane 0 (heap built)
+  int16_t* heap = t.w->heap;
+  uint32_t* hk = t.w->hk;
+  int node;
+  t.heap_max = ZS_HEAP_SIZE;
   node = d.elems;
   do {
     const uint32_t en = hk[1];
@@ -420,6 +439,7 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   B.extra = ZS_EXTRA_BLBITS;
   zs_tree_leaves_wave(t, L, lane);
   __syncthreads();
+  zs_tree_heapify_wave(t, L, lane);
   if (lane == 0) zs_build_tree(t, L);
   __syncthreads();
   zs_gen_bitlen_wave(t, L, lane);
@@ -428,6 +448,7 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   __syncthreads();
   zs_tree_leaves_wave(t, D, lane);
   __syncthreads();
+  zs_tree_heapify_wave(t, D, lane);
   if (lane == 0) zs_build_tree(t, D);
   __syncthreads();
   zs_gen_bitlen_wave(t, D, lane);
@@ -449,6 +470,7 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   __syncthreads();
   zs_tree_leaves_wave(t, B, lane);
   __syncthreads();
+  zs_tree_heapify_wave(t, B, lane);
   if (lane == 0) zs_build_tree(t, B);
   __syncthreads();
   zs_gen_bitlen_wave(t, B, lane);
