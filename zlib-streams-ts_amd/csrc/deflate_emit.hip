@@ -92,6 +92,39 @@ static __device__ void zs_pqdownheap(zs_tstate& t, int k) {
   hk[k] = v;
 }
 
+// pqdownheap of a value v the caller holds in a register (placed at k, i.e.
+// hk[k] = v then the sift): no LDS read of hk[k] first, and it returns the
+// entry that ends at k -- the new root for k = 1 -- so the merge loop reads
+// neither hk[1] back
+static __device__ uint32_t zs_pqdownheap_v(zs_tstate& t, int k, uint32_t v) {
+  uint32_t* hk = t.w->hk;
+  const uint32_t kv = zs_hkey(v);
+  const int len = t.heap_len, k0 = k;
+  uint32_t top = v;
+  int j = k << 1;
+  while (j <= len) {
+    const uint2 ch = *reinterpret_cast<const uint2*>(&hk[j]);
+    const uint4 gc = *reinterpret_cast<const uint4*>(&hk[2 * j]);
+    const bool right = j < len && zs_hkey(ch.y) <= zs_hkey(ch.x);
+    const uint32_t c = right ? ch.y : ch.x;
+    if (kv <= zs_hkey(c)) break;
+    hk[k] = c;
+    if (k == k0) top = c;
+    k = j + (right ? 1 : 0);
+    const int j2 = k << 1;
+    if (j2 > len) break;
+    const uint32_t a2 = right ? gc.z : gc.x, b2 = right ? gc.w : gc.y;
+    const bool right2 = j2 < len && zs_hkey(b2) <= zs_hkey(a2);
+    const uint32_t c2 = right2 ? b2 : a2;
+    if (kv <= zs_hkey(c2)) break;
+    hk[k] = c2;
+    k = j2 + (right2 ? 1 : 0);
+    j = k << 1;
+  }
+  hk[k] = v;
+  return top;
+}
+
 // gen_codes (trees.ts:54-76) by the wave: symbol n's code is the first code of
 // its length plus the number of symbols m < n of the same length, counted
 // with one ballot per length over 64 symbols at a time.  All lanes call it.
@@ -175,11 +208,11 @@ static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:3
   int node;
   t.heap_max = ZS_HEAP_SIZE;
   node = d.elems;
+  uint32_t root = hk[1];
   do {
-    const uint32_t en = hk[1];
-    hk[1] = hk[t.heap_len--];
-    zs_pqdownheap(t, 1);
-    const uint32_t em = hk[1];
+    const uint32_t en = root;
+    const uint32_t last = hk[t.heap_len--];
+    const uint32_t em = zs_pqdownheap_v(t, 1, last);
     const uint32_t nn = en & 1023u, mm = em & 1023u;
     heap[--t.heap_max] = (int16_t)nn;
     heap[--t.heap_max] = (int16_t)mm;
@@ -187,11 +220,10 @@ static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:3
     const uint32_t dn = (en >> 10) & 127u, dm = (em >> 10) & 127u;
     d.freq[node] = (uint16_t)f;
     d.dad[nn] = d.dad[mm] = (uint16_t)node;
-    hk[1] = (f << 17) | (((dn >= dm ? dn : dm) + 1) << 10) | (uint32_t)node;
+    root = zs_pqdownheap_v(t, 1, (f << 17) | (((dn >= dm ? dn : dm) + 1) << 10) | (uint32_t)node);
     node++;
-    zs_pqdownheap(t, 1);
   } while (t.heap_len >= 2);
-  heap[--t.heap_max] = (int16_t)(hk[1] & 1023u);
+  heap[--t.heap_max] = (int16_t)(root & 1023u);
   // the bit lengths follow by the wave (zs_gen_bitlen_wave), then the codes (zs_gen_codes_wave)
 }
 
