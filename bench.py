@@ -2,7 +2,9 @@
 """Headline benchmark: uncompressed MB/s, deflate-raw L6, one 4096 x 64 KiB
 synthetic T-corpus batch (BASELINE.json configs[1]) at 1/2/4/8 GPUs.
 
-One process per GPU (torch.distributed.run for N > 1).  A "step" is one batch
+One process per GPU: for N > 1 either a launcher's ranks (torch.distributed.run
+sets WORLD_SIZE; it must equal --gpus) or, run directly with --gpus N, N child
+ranks this script starts itself before any GPU call.  A "step" is one batch
 compression, inputs already resident in HBM, outputs written to HBM.
 
 * Strong scaling (default, the north star's "batch partitioned across the
@@ -150,22 +152,34 @@ def _tagged_first(files, tag):
     return [f for f in files if f not in mine] + mine
 
 
+def build_id():
+    import zsamd
+    return zsamd.build_id()
+
+
 def profiled_traffic(kernel, kernel_ms, tag=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3
     summary (profiles/*/summary*.json: FETCH_SIZE / WRITE_SIZE passes, gfx950
     read correction by tools/summarize_profile.py) -- used only when that
-    profile's average kernel duration agrees with this run's HIP-event time
-    within 10 % (i.e. it profiled this build); otherwise (None, reason)."""
+    profile was made from this build (its "_build_id", zsamd.build_id()) and its
+    average kernel duration agrees with this run's HIP-event time within 10 %;
+    otherwise (None, reason)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")))  # round directories sort in order
     files = _tagged_first(files, tag)
     stale, hit = None, None
+    bid = build_id()
     for f in reversed(files):  # this config's files first, newest round first; the first matching duration
         try:
-            e = json.load(open(f)).get(kernel)
+            j = json.load(open(f))
         except (OSError, ValueError):
             continue
+        e = j.get(kernel)
         if not e or "hbm_bytes_corrected" not in e:
+            continue
+        if j.get("_build_id") != bid:
+            stale = stale or "stale: %s is of build %s, this is build %s" % (os.path.relpath(f, ROOT),
+                                                                              j.get("_build_id"), bid)
             continue
         prof_ms = e["avg_ns"] / 1e6
         src = os.path.relpath(f, ROOT)
@@ -192,14 +206,19 @@ def profiled_ceilings(kernel, kernel_ms, tag=None):
                    glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")))
     files = _tagged_first(files, tag)
     stale, hit = None, None
+    bid = build_id()
     for f in reversed(files):  # this config's files first, newest round first; the first matching duration
         try:
-            e = json.load(open(f)).get(kernel)
+            j = json.load(open(f))
         except (OSError, ValueError):
             continue
+        e = j.get(kernel)
         if not e:
             continue
         src = os.path.relpath(f, ROOT)
+        if j.get("_build_id") != bid:
+            stale = stale or "stale: %s is of build %s, this is build %s" % (src, j.get("_build_id"), bid)
+            continue
         prof_ms = e["avg_ns"] / 1e6
         if abs(prof_ms - kernel_ms) > 0.15 * kernel_ms:
             stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
@@ -271,8 +290,44 @@ def layout(S, L, cap):
     return in_off, in_len, out_off, out_cap
 
 
+def launch_ranks(args):
+    """`--gpus N` (N > 1) run directly, without a launcher's WORLD_SIZE: start the N
+    ranks here -- fresh child processes, one per GPU, nothing of the GPU touched in
+    this parent -- with torch.distributed's env rendezvous on 127.0.0.1, and exit
+    with the first failing rank's code (the others are stopped then)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    sys.exit(rc)
+
+
 def main():
     args = parse()
+    world = os.environ.get("WORLD_SIZE")
+    if world is None and args.gpus > 1:
+        return launch_ranks(args)
+    if world is not None:
+        assert int(world) == args.gpus, "WORLD_SIZE=%s but --gpus %d" % (world, args.gpus)
     if args.corpus is None:
         args.corpus = "mixed" if (args.mode == "inflate" and args.format == "deflate-raw") else "text"
     if args.mode == "inflate":

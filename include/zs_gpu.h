@@ -107,6 +107,66 @@ int zs_inflate_batch(zs_ctx *ctx, int wbits, uint32_t n_streams, const uint8_t *
                      const uint32_t *in_len, uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                      int32_t *status, int32_t *phase, int32_t *msg, uint32_t *out_len, uint32_t *consumed);
 
+/* The same batch entries with the per-stream check value: check[i] is the
+ * reference's strm.adler after stream i (deflate.ts:155-159,462,778,788;
+ * inflate.ts:105,1014,1080): the adler32 (zlib) / crc32 (gzip) of the stream's
+ * uncompressed bytes; for deflate-raw compression 1 (adler32(0), never updated
+ * without a wrapper), for raw / deflate64-raw decompression 0 (createStream's
+ * initial value, common/utils.ts:49); 0 for a stream that failed.  d_check /
+ * check may be NULL (then these are the calls above). */
+int zs_deflate_batch_device_ex(zs_ctx *ctx, int level, int wbits, uint32_t n_streams, const uint8_t *d_in,
+                               const uint64_t *in_off, const uint32_t *in_len, uint8_t *d_out,
+                               const uint64_t *out_off, const uint32_t *out_cap, int32_t *d_status,
+                               uint32_t *d_out_len, uint32_t *d_check, void *hip_stream);
+int zs_deflate_batch_ex(zs_ctx *ctx, int level, int wbits, uint32_t n_streams, const uint8_t *in,
+                        const uint64_t *in_off, const uint32_t *in_len, uint8_t *out, const uint64_t *out_off,
+                        const uint32_t *out_cap, int32_t *status, uint32_t *out_len, uint32_t *check);
+int zs_inflate_batch_device_ex(zs_ctx *ctx, int wbits, uint32_t n_streams, const uint8_t *d_in,
+                               const uint64_t *in_off, const uint32_t *in_len, uint8_t *d_out,
+                               const uint64_t *out_off, const uint32_t *out_cap, int32_t *d_status, int32_t *d_phase,
+                               int32_t *d_msg, uint32_t *d_out_len, uint32_t *d_consumed, uint32_t *d_check,
+                               void *hip_stream);
+int zs_inflate_batch_ex(zs_ctx *ctx, int wbits, uint32_t n_streams, const uint8_t *in, const uint64_t *in_off,
+                        const uint32_t *in_len, uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                        int32_t *status, int32_t *phase, int32_t *msg, uint32_t *out_len, uint32_t *consumed,
+                        uint32_t *check);
+
+/* Unbounded decode, as DecompressionStream (streams.ts:46,132-182: pooled 64 KiB
+ * output buffers until Z_STREAM_END, no output cap).  Host buffers; the outputs
+ * land in ONE buffer the library allocates: on ZS_OK *out points to it, stream i
+ * at (*out)[out_off[i]], out_len[i] bytes; release it with zs_free().  Members
+ * are retried, alone, with eight times the room until they fit, so no member
+ * reports the capacity message unless its output exceeds 4 GiB - 4 bytes (the
+ * u32 length of this ABI). */
+int zs_inflate_batch_auto(zs_ctx *ctx, int wbits, uint32_t n_streams, const uint8_t *in, const uint64_t *in_off,
+                          const uint32_t *in_len, uint8_t **out, uint64_t *out_off, int32_t *status, int32_t *phase,
+                          int32_t *msg, uint32_t *out_len, uint32_t *consumed, uint32_t *check);
+void zs_free(void *p);
+
+/* Multi-GPU pool (SURVEY.md 8(b) "device mask", 8(e)): one context per device
+ * of device_mask (bit d = HIP device d; 0 = every visible device).  A batch is
+ * partitioned into contiguous stream ranges [k n / G, (k + 1) n / G) over the G
+ * devices, one host thread per device; each shard writes straight into the
+ * caller's arrays (offsets are absolute), so results are identical to one
+ * device's.  Same arguments and semantics as the single-context host calls.
+ * One batch at a time per pool. */
+typedef struct zs_pool zs_pool;
+int zs_pool_create(uint64_t device_mask, zs_pool **out);
+void zs_pool_destroy(zs_pool *pool);
+int zs_pool_size(const zs_pool *pool);
+int zs_pool_device(const zs_pool *pool, int k);
+int zs_pool_deflate_batch(zs_pool *pool, int level, int wbits, uint32_t n_streams, const uint8_t *in,
+                          const uint64_t *in_off, const uint32_t *in_len, uint8_t *out, const uint64_t *out_off,
+                          const uint32_t *out_cap, int32_t *status, uint32_t *out_len, uint32_t *check);
+int zs_pool_inflate_batch(zs_pool *pool, int wbits, uint32_t n_streams, const uint8_t *in, const uint64_t *in_off,
+                          const uint32_t *in_len, uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                          int32_t *status, int32_t *phase, int32_t *msg, uint32_t *out_len, uint32_t *consumed,
+                          uint32_t *check);
+int zs_pool_inflate_batch_auto(zs_pool *pool, int wbits, uint32_t n_streams, const uint8_t *in,
+                               const uint64_t *in_off, const uint32_t *in_len, uint8_t **out, uint64_t *out_off,
+                               int32_t *status, int32_t *phase, int32_t *msg, uint32_t *out_len, uint32_t *consumed,
+                               uint32_t *check);
+
 /* The z_stream message for a d_msg index (inflate.ts:397-1031, inffast.ts:108,197,210). */
 const char *zs_inflate_message(int32_t msg_index);
 
@@ -145,22 +205,18 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * "check_phases" (default 0): synchronise after every kernel phase and fail
  * with ZS_MEM_ERROR naming the phase whose launch or execution failed;
  * "match_sweep" (default 1): levels 4..9, streams <= 65,537 B find matches by
- * a counting sort by hash + lock-step sweep (0: chain links + per-tile walk);
- * "parse_split" (default 0): levels 4..9 parse as per-range + per-stream
- * kernels (0: one wave per stream); "parse_win" (default 32; 16, or 0 for
- * direct loads): match-table entries the one-wave parse stages per lane in
- * LDS; "lane_block" (default 0 = by batch size;
+ * a counting sort by hash + lock-step sweep (0: the chain-link + per-tile walk
+ * kernels that serve longer streams, for every stream -- a cross-check);
+ * "lane_block" (default 0 = by batch size;
  * else 1..64, a power of two): members per workgroup of the inflate lane path;
  * "inflate_wave_min" (default 32768; 0 = never): members with more input bytes
  * decode one per wave (inflate_wave.hip) beside the lane kernel;
- * "parse_waves" (default 0 = two below 2048 streams, else one; 1 or 2): waves
- * per stream of the levels 4..9 one-wave-family parse (two: 512-position
- * segments, two rounds' speculative passes at once);
+ * "parse_waves" (default 0 = two below 2048 streams, else one; 1, 2 or 4):
+ * waves per stream of the levels 4..9 lazy parse (two: 512-position segments,
+ * two rounds' speculative passes at once);
  * "fast_group" (default 1): levels 1..3 replay deflate_fast a group of 64
- * positions at a time from speculative per-lane chain walks (0: step by step);
- * "chunks" (default 0 = chosen from the batch, 1 today; else 1..64): deflate
- * batches run as that many contiguous chunks of streams pipelined over two
- * HIP streams.  These options never change output bytes.  "inflate_ref_wrap" (default 1)
+ * positions at a time from speculative per-lane chain walks (0: step by step).
+ * These options never change output bytes.  "inflate_ref_wrap" (default 1)
  * does: 1 reproduces the reference's inflate_fast window-wrap copy
  * (inffast.ts:133-147), which changes the output of members whose match
  * crosses the reference's window wrap between inflate() calls; 0 decodes with

@@ -1,0 +1,209 @@
+"""GPU parity of the drop-in boundary's semantics and of the
+two configs decoded at their full size:
+
+* DecompressionStream has no output cap (src/mod/streams.ts:46,132-182): the
+  default batch decode returns any member whole (zs_inflate_batch_auto);
+* formats and levels map as streams.ts:220-221,233 (unknown -> windowBits 15,
+  a non-number level -> the default);
+* the per-stream check value is the reference's strm.adler after the stream
+  (deflate.ts:155-159,462; inflate.ts:105,1014,1080);
+* the multi-GPU pool (device mask) returns what one device returns;
+* C3 -- all 65,536 members -- and C5-i -- the gunzip of all 8,192 gzip
+  members with their CRC-32 -- decode to their sources.
+"""
+import ctypes
+import hashlib
+import os
+import zlib
+
+import pytest
+
+import corpus
+import golden_io
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def test_default_decode_is_unbounded(engine):
+    """zeros_100k.deflate64 (369 B -> 100,000 B, the reference's test/data) and a
+    1 MiB zero stream in every format decode with default options."""
+    z64 = open(os.path.join(golden_io.GOLDEN, "d64", "zeros_100k.deflate64"), "rb").read()
+    assert engine.decompress_batch([z64], "deflate64-raw") == [bytes(100000)]
+    zeros = bytes(1 << 20)
+    for fmt in ("deflate-raw", "deflate", "gzip"):
+        comp = engine.compress_batch([zeros, b"", b"x" * 70000], fmt, 6)
+        assert len(comp[0]) < 2000  # ratio > 500: far beyond any first-pass capacity guess
+        assert engine.decompress_batch(comp, fmt) == [zeros, b"", b"x" * 70000]
+    # mixed batch: small and huge ratios, corrupt members keep their reference errors
+    srcs = [bytes(3 << 20), corpus.text(corpus.stream_seed(5), 65536), bytes(200000), b"abc"]
+    comps = [oracle.compress(s, 9, "deflate-raw")[1] for s in srcs]
+    bad = bytearray(comps[2])
+    bad[len(bad) // 2] ^= 0x40
+    comps.append(bytes(bad))
+    res = engine.decompress_batch_raw(comps, "deflate-raw")
+    for s, (st, ph, msg, out, cons) in zip(srcs, res):
+        assert st == 1 and out == s
+    ost, oout, ocons, oph, omsg = oracle.decompress(comps[4], "deflate-raw", cap=1 << 22)
+    st, ph, msg, out, cons = res[4]
+    assert (st, ph, msg) == (ost, oph, omsg)
+    assert msg != "output capacity exceeded"
+
+
+def test_explicit_cap_is_a_cap(engine):
+    c = oracle.compress(bytes(100000), 6, "deflate-raw")[1]
+    (st, ph, msg, out, cons), = engine.decompress_batch_raw([c], "deflate-raw", out_caps=[1000])
+    assert st == -5 and msg == "output capacity exceeded"
+
+
+def test_format_and_level_fall_through(engine):
+    xs = [corpus.text(corpus.stream_seed(i), 20000 + i) for i in range(3)]
+    assert engine.compress_batch(xs, "bogus", 6) == engine.compress_batch(xs, "deflate", 6)
+    assert engine.compress_batch(xs, "deflate-raw", "9") == engine.compress_batch(xs, "deflate-raw", 6)
+    assert engine.compress_batch(xs, "deflate-raw", None) == engine.compress_batch(xs, "deflate-raw", -1)
+    comp = engine.compress_batch(xs, "deflate", 6)
+    assert engine.decompress_batch(comp, "no-such-format") == xs
+
+
+@pytest.mark.parametrize("fmt", ["deflate-raw", "deflate", "gzip"])
+def test_check_values_are_strm_adler(engine, fmt):
+    xs = [b"", b"hello", corpus.text(corpus.stream_seed(3), 65536), corpus.rand(4, 100000)]
+    for level in (0, 1, 6, 9):
+        res = engine.compress_batch_detailed(xs, fmt, level)
+        for x, (st, out, chk) in zip(xs, res):
+            want = {"deflate-raw": 1, "deflate": zlib.adler32(x), "gzip": zlib.crc32(x)}[fmt]
+            assert st == 1 and chk == want, (fmt, level, len(x))
+        back = engine.decompress_batch_detailed([o for _, o, _ in res], fmt)
+        for x, (st, ph, msg, out, cons, chk) in zip(xs, back):
+            want = {"deflate-raw": 0, "deflate": zlib.adler32(x), "gzip": zlib.crc32(x)}[fmt]
+            assert st == 1 and out == x and chk == want
+
+
+@pytest.mark.parametrize("fmt", ["deflate-raw", "deflate", "gzip"])
+def test_level0_short_capacity_reports_buf_error_and_writes_nothing(engine, fmt):
+    """Level 0 (zs_k_stored) with a capacity below its output: Z_BUF_ERROR,
+    out_len 0, and no byte of the output region is touched -- the other levels'
+    rule (zs_k_finish)."""
+    import torch
+    import zsamd
+
+    data = [corpus.text(corpus.stream_seed(1), 50000), corpus.text(corpus.stream_seed(2), 40000)]
+    blob = b"".join(data)
+    d_in = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    caps = [1024, zsamd.deflate_capacity(40000, fmt)]
+    d_out = torch.full((caps[0] + caps[1] + 4096,), 0xA5, dtype=torch.uint8, device="cuda")
+    d_st = torch.zeros(2, dtype=torch.int32, device="cuda")
+    d_len = torch.zeros(2, dtype=torch.int32, device="cuda")
+    u64, u32 = ctypes.c_uint64 * 2, ctypes.c_uint32 * 2
+    engine.compress_device(0, fmt, 2, d_in.data_ptr(), u64(0, 50000), u32(50000, 40000), d_out.data_ptr(),
+                           u64(0, caps[0]), u32(*caps), d_st.data_ptr(), d_len.data_ptr())
+    torch.cuda.synchronize()
+    assert d_st.tolist() == [-5, 1] and d_len.tolist()[0] == 0
+    assert bool((d_out[:caps[0]] == 0xA5).all())  # the failed stream wrote nothing
+    o = d_out[caps[0]: caps[0] + d_len.tolist()[1]].cpu().numpy().tobytes()
+    assert o == oracle.compress(data[1], 0, fmt)[1]
+    # the host path reports the same and leaves the caller's bytes alone
+    st = engine.compress_batch_raw(data, fmt, 0)
+    assert [s for s, _ in st] == [1, 1]
+
+
+def test_pool_on_one_device_equals_engine(engine):
+    import zsamd
+
+    pool = zsamd.Pool([0])
+    assert pool.devices == [0]
+    xs = [corpus.text(corpus.stream_seed(i), 65536) for i in range(64)] + [b"", b"abc"]
+    for fmt in ("deflate-raw", "gzip"):
+        a = pool.compress_batch_detailed(xs, fmt, 6)
+        assert a == engine.compress_batch_detailed(xs, fmt, 6)
+        back = pool.decompress_batch([o for _, o, _ in a], fmt)
+        assert back == xs
+    with pytest.raises(ValueError):
+        zsamd.Pool([63])  # no such device
+    pool.close()
+
+
+@pytest.mark.slow
+def test_c3_all_65536_members_decode(engine):
+    """BASELINE.json configs[2] at its full size: the 4,096 unique M-corpus
+    members (pinned by the reference golden batch_m64_l6_raw) x 16 = 65,536
+    members in one batch, default lane_block, every output equal to its source."""
+    import torch
+    import zsamd
+
+    recs = golden_io.batch("m64_l6_raw")
+    S, R, L = 4096, 16, 65536
+    host = zsamd.corpus("mixed", 0, S, L)
+    src = [bytes(host[i * L:(i + 1) * L]) for i in range(S)]
+    comp = engine.compress_batch(src, "deflate-raw", 6)
+    bad = [i for i, c in enumerate(comp) if (len(c), hashlib.sha256(c).digest()[:16]) != recs[i]]
+    assert not bad, bad[:10]
+    assert sum(len(c) for c in comp) == 123877078
+    members = comp * R
+    blob = b"".join(members)
+    N = len(members)
+    offs, o = [], 0
+    for m in members:
+        offs.append(o)
+        o += len(m)
+    d_in = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    d_out = torch.zeros(N * L, dtype=torch.uint8, device="cuda")
+    i32 = lambda: torch.zeros(N, dtype=torch.int32, device="cuda")
+    d_st, d_ph, d_msg, d_len, d_cons = i32(), i32(), i32(), i32(), i32()
+    engine.decompress_device("deflate-raw", N, d_in.data_ptr(), (ctypes.c_uint64 * N)(*offs),
+                             (ctypes.c_uint32 * N)(*[len(m) for m in members]), d_out.data_ptr(),
+                             (ctypes.c_uint64 * N)(*[i * L for i in range(N)]), (ctypes.c_uint32 * N)(*([L] * N)),
+                             d_st.data_ptr(), d_ph.data_ptr(), d_msg.data_ptr(), d_len.data_ptr(), d_cons.data_ptr())
+    torch.cuda.synchronize()
+    assert int((d_st != 1).sum()) == 0
+    assert int((d_len != L).sum()) == 0
+    assert d_cons.tolist() == [len(m) for m in members]
+    want = torch.frombuffer(host, dtype=torch.uint8).cuda().view(1, S, L)
+    same = (d_out.view(R, S, L) == want).all(dim=2)
+    assert bool(same.all()), [(int(r), int(s)) for r, s in (~same).nonzero()[:10]]
+    assert engine.last_lane_count() == N  # every member on the lane fast path
+
+
+@pytest.mark.slow
+def test_c5_gunzip_all_8192_members_with_crc(engine):
+    """C5-i decode at its full size: the 8,192 gzip L6 members (pinned by the
+    reference golden batch_t64_l6_gzip) gunzipped in one batch, each output equal
+    to its source, each trailer's CRC-32 verified by the engine and returned as the
+    check value (= zlib.crc32 of the source)."""
+    import torch
+    import zsamd
+
+    recs = golden_io.batch("t64_l6_gzip")
+    N, L = 8192, 65536
+    host = zsamd.corpus("text", 0, N, L)
+    src = [bytes(host[i * L:(i + 1) * L]) for i in range(N)]
+    gz = []
+    for lo in (0, 4096):
+        gz += engine.compress_batch(src[lo:lo + 4096], "gzip", 6)
+    bad = [i for i, c in enumerate(gz) if (len(c), hashlib.sha256(c).digest()[:16]) != recs[i]]
+    assert not bad, bad[:10]
+    blob = b"".join(gz)
+    offs, o = [], 0
+    for m in gz:
+        offs.append(o)
+        o += len(m)
+    d_in = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    d_out = torch.zeros(N * L, dtype=torch.uint8, device="cuda")
+    i32 = lambda: torch.zeros(N, dtype=torch.int32, device="cuda")
+    d_st, d_ph, d_msg, d_len, d_cons, d_chk = i32(), i32(), i32(), i32(), i32(), i32()
+    lib = engine._L
+    r = lib.zs_inflate_batch_device_ex(engine.handle, 31, N, ctypes.c_void_p(d_in.data_ptr()),
+                                       (ctypes.c_uint64 * N)(*offs), (ctypes.c_uint32 * N)(*[len(m) for m in gz]),
+                                       ctypes.c_void_p(d_out.data_ptr()),
+                                       (ctypes.c_uint64 * N)(*[i * L for i in range(N)]),
+                                       (ctypes.c_uint32 * N)(*([L] * N)), ctypes.c_void_p(d_st.data_ptr()),
+                                       ctypes.c_void_p(d_ph.data_ptr()), ctypes.c_void_p(d_msg.data_ptr()),
+                                       ctypes.c_void_p(d_len.data_ptr()), ctypes.c_void_p(d_cons.data_ptr()),
+                                       ctypes.c_void_p(d_chk.data_ptr()), None)
+    assert r == 0
+    torch.cuda.synchronize()
+    assert int((d_st != 1).sum()) == 0 and int((d_len != L).sum()) == 0
+    assert bool((d_out.view(N, L) == torch.frombuffer(host, dtype=torch.uint8).cuda().view(N, L)).all())
+    chk = [c & 0xffffffff for c in d_chk.tolist()]
+    assert chk == [zlib.crc32(s) for s in src]
+    assert d_cons.tolist() == [len(m) for m in gz]

@@ -88,7 +88,9 @@ def test_inffast_window_wrap_defect_is_reproduced():
     """The reference's inflate_fast mis-copies when a window-sourced match wraps the
     ring and the remainder fits in w_next (inffast.ts:139-147 reads `output` from 0).
     The oracle reproduces the reference's corrupt bytes exactly (reference_bugs=True)
-    and decodes correctly otherwise; the GPU engine implements the correct decode."""
+    and decodes correctly otherwise.  The GPU engine reproduces the reference's bytes
+    by default and decodes with zlib semantics under inflate_ref_wrap = 0
+    (tests/test_gpu_inflate.py::test_inffast_window_wrap_defect_is_reproduced)."""
     j = json.load(open(os.path.join(golden_io.GOLDEN, "inffast_wrap_defect.json")))
     src = corpus.make(j["source"])
     st, comp, _ = oracle.compress(src, 6, "deflate-raw")

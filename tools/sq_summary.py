@@ -59,5 +59,9 @@ for k, cs in sorted(agg.items()):
         print("   %-24s %16.0f" % (c, v[c]))
     for c, x in derived(v).items():
         print("   %-32s %8.4f" % (c, x))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'zlib-streams-ts_amd'))
+import zsamd  # noqa: E402
+
+res['_build_id'] = zsamd.build_id()  # the build these counters belong to
 if out_json:
     json.dump(res, open(out_json, "w"), indent=1, sort_keys=True)

@@ -34,6 +34,10 @@ for k, v in stats.items():
         e["hbm_bytes_raw"] = (e["fetch_kib"] + e["write_kib"]) * 1024
         e["hbm_bytes_corrected"] = (2 * e["fetch_kib"] + e["write_kib"]) * 1024
     out[k] = e
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'zlib-streams-ts_amd'))
+import zsamd  # noqa: E402
+
+out['_build_id'] = zsamd.build_id()  # the build these counters belong to
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
 for k, e in sorted(out.items(), key=lambda kv: -kv[1]["total_ns"]):

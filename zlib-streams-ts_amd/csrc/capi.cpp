@@ -77,6 +77,8 @@ const zs_level_cfg kLevels[10] = {{0, 0, 0, 0},     {4, 4, 8, 4},     {4, 5, 16,
 
 }  // namespace
 
+void zs_set_last_error(const std::string& msg) { g_err = msg; }
+
 #define ZS_PARSE2W_AUTO 2048u  // batches below this many streams parse with two waves per stream (option parse_waves = 0)
 
 struct zs_ctx {
@@ -86,17 +88,13 @@ struct zs_ctx {
   bool check_phases = false;  // synchronise after every phase and name the one that failed
   // workspace
   Buf meta, prevd, mres, syms, blocks, streams, codes, hdr, check, istate, pscr, ltabs, lres, llen, lstat;
-  hipStream_t last_stream = nullptr;  // stream of the last inflate batch
   bool inflate_fast = true;
   bool inflate_ref_wrap = true;  // reproduce the reference's inflate_fast window-wrap copy (inffast.ts:133-147)
-  bool match_sweep = true;
-  bool parse_split = false;  // L4..9: zs_k_parse_a + zs_k_parse_b (default 0: the one-wave zs_k_parse, faster so far)
-  int parse_win = 32;        // L4..9 parse: match-table entries staged per lane in LDS (32, 16; 0: direct loads)
+  bool match_sweep = true;   // 0: the chain-walk kernels for every stream (a cross-check of the sweep)
   int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
   int cur_pw = 1;            // waves per stream of the current deflate batch's parse (zs_k_parse / _2w / _4w)
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
-  int chunks = 0;             // deflate: chunks of the batch pipelined over two streams (0: chosen from the batch)
   uint32_t inflate_wave_min = 32768;  // members with more input bytes decode one per wave (inflate_wave.hip); 0: never
   hipStream_t side = nullptr;         // second stream: the wave-per-member kernel runs beside the lane kernel
   hipEvent_t fork = nullptr, join = nullptr;
@@ -114,9 +112,19 @@ struct zs_ctx {
     hipStream_t st;
   };
   std::vector<Mark> marks;  // a phase = the time between consecutive marks on the same stream
-  std::vector<std::pair<std::string, double>> phase_ms;
+  // folded (pending) results since the last query: marks are folded in when
+  // more than kMaxMarks are pending, so an unqueried timing run stays bounded
+  std::vector<std::pair<std::string, double>> phase_acc;
+  double total_acc = 0;
+  bool acc_any = false;
+  std::vector<std::pair<std::string, double>> phase_ms;  // the last query's results
   double total_ms = -1;
+  // inflate lane count of the last batch: copied to pinned memory on the batch's stream, then an event
+  uint32_t* lane_count_host = nullptr;
+  hipEvent_t lane_ev = nullptr;
 };
+static constexpr size_t kMaxMarks = 1024;
+static void fold_marks(zs_ctx* c);
 
 // Phase boundary: records a timing event and, with check_phases, waits for the
 // phase and reports a launch or execution error under the phase's name.
@@ -130,6 +138,7 @@ static int mark(zs_ctx* c, hipStream_t st, const char* name) {
     }
   }
   if (!c->timing) return ZS_OK;
+  if (c->marks.size() >= kMaxMarks) fold_marks(c);
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return ZS_OK;
   (void)hipEventRecord(e, st);
@@ -142,18 +151,11 @@ static int mark(zs_ctx* c, hipStream_t st, const char* name) {
     if (r_ != ZS_OK) return r_;                 \
   } while (0)
 
-// Turns the pending marks (of every batch since the last query) into phase
-// times: waits for the last one.  Batch calls never wait for their marks, so a
-// timed sequence of batches runs back to back.
-static void collect_marks(zs_ctx* c) {
-  if (c->marks.empty()) return;  // nothing new: keep the last results
-  c->phase_ms.clear();
-  c->total_ms = -1;
-  if (c->marks.size() < 2) {
-    for (auto& m : c->marks) (void)hipEventDestroy(m.ev);
-    c->marks.clear();
-    return;
-  }
+// Folds the pending marks into the accumulated phase times: waits for the
+// last one, keeps it as the anchor of the next marks (so the time between two
+// folds is not lost) and destroys the others.
+static void fold_marks(zs_ctx* c) {
+  if (c->marks.size() < 2) return;
   (void)hipEventSynchronize(c->marks.back().ev);
   for (size_t i = 1; i < c->marks.size(); i++) {
     size_t j = i;  // the previous mark on the same stream
@@ -161,13 +163,29 @@ static void collect_marks(zs_ctx* c) {
     if (j == (size_t)-1) continue;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->marks[j].ev, c->marks[i].ev);
-    c->phase_ms.emplace_back(c->marks[i].name, ms);
+    c->phase_acc.emplace_back(c->marks[i].name, ms);
   }
   float tot = 0;
   (void)hipEventElapsedTime(&tot, c->marks.front().ev, c->marks.back().ev);
-  c->total_ms = tot;
+  c->total_acc += tot;
+  c->acc_any = true;
+  for (size_t i = 0; i + 1 < c->marks.size(); i++) (void)hipEventDestroy(c->marks[i].ev);
+  c->marks.erase(c->marks.begin(), c->marks.end() - 1);
+}
+
+// Turns the marks of every batch since the last query into phase times (waits
+// for the last one).  Batch calls never wait for their marks, so a timed
+// sequence of batches runs back to back.
+static void collect_marks(zs_ctx* c) {
+  fold_marks(c);
   for (auto& m : c->marks) (void)hipEventDestroy(m.ev);
   c->marks.clear();
+  if (!c->acc_any) return;  // nothing new: keep the last results
+  c->phase_ms.swap(c->phase_acc);
+  c->phase_acc.clear();
+  c->total_ms = c->total_acc;
+  c->total_acc = 0;
+  c->acc_any = false;
 }
 
 extern "C" {
@@ -236,6 +254,10 @@ void zs_ctx_destroy(zs_ctx* c) {
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&c->h_in, &c->h_out})
     if (b->p) (void)hipHostFree(b->p);
+  for (auto& m : c->marks) (void)hipEventDestroy(m.ev);
+  if (c->lane_ev) (void)hipEventSynchronize(c->lane_ev);
+  if (c->lane_count_host) (void)hipHostFree(c->lane_count_host);
+  if (c->lane_ev) (void)hipEventDestroy(c->lane_ev);
   if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->fork) (void)hipEventDestroy(c->fork);
   if (c->join) (void)hipEventDestroy(c->join);
@@ -253,22 +275,15 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "inflate_ref_wrap")) c->inflate_ref_wrap = value != 0;
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
-  else if (!strcmp(name, "parse_split")) c->parse_split = value != 0;
   else if (!strcmp(name, "fast_group")) c->fast_group = value != 0;
   else if (!strcmp(name, "parse_waves")) {
     if (value < 0 || value > 4 || value == 3) return fail(ZS_STREAM_ERROR, "parse_waves must be 0, 1, 2 or 4");
     c->parse_waves = value;
   }
-  else if (!strcmp(name, "parse_win")) {
-    if (value != 0 && value != 16 && value != 32) return fail(ZS_STREAM_ERROR, "parse_win must be 0, 16 or 32");
-    c->parse_win = value;
-  } else if (!strcmp(name, "lane_block")) {
+  else if (!strcmp(name, "lane_block")) {
     if (value != 0 && (value < 1 || value > 64 || (value & (value - 1))))
       return fail(ZS_STREAM_ERROR, "lane_block must be 0 or a power of two <= 64");
     c->lane_block = value;
-  } else if (!strcmp(name, "chunks")) {
-    if (value < 0 || value > 64) return fail(ZS_STREAM_ERROR, "chunks must be in 0..64");
-    c->chunks = value;
   } else if (!strcmp(name, "inflate_wave_min")) {
     if (value < 0) return fail(ZS_STREAM_ERROR, "inflate_wave_min must be >= 0");
     c->inflate_wave_min = (uint32_t)value;
@@ -280,11 +295,8 @@ double zs_last_batch_ms(zs_ctx* c) {
   return c->total_ms;
 }
 uint32_t zs_last_inflate_lane_count(zs_ctx* c) {
-  uint32_t v = 0;
-  if (!c || !c->lstat.p || hipStreamSynchronize(c->last_stream) != hipSuccess ||
-      hipMemcpy(&v, c->lstat.p, 4, hipMemcpyDeviceToHost) != hipSuccess)
-    return 0;
-  return v;
+  if (!c || !c->lane_count_host || hipEventSynchronize(c->lane_ev) != hipSuccess) return 0;
+  return *(volatile uint32_t*)c->lane_count_host;
 }
 double zs_last_phase_ms(zs_ctx* c, const char* phase) {
   collect_marks(c);
@@ -302,9 +314,9 @@ uint64_t zs_deflate_bound(uint64_t n, int wbits) {  // deflate.ts:615-674, memLe
 
 }  // extern "C"
 
-// Device metadata block: in_off | in_len | out_off | out_cap | pos_base | blk_base | range_base
+// Device metadata block: in_off | in_len | out_off | out_cap | pos_base | blk_base
 struct MetaLayout {
-  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, range_base, bytes;
+  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, bytes;
   explicit MetaLayout(uint32_t n) {
     size_t o = 0;
     auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~size_t(255); return r; };
@@ -314,7 +326,6 @@ struct MetaLayout {
     out_cap = take(4ull * n);
     pos_base = take(8ull * n);
     blk_base = take(4ull * n);
-    range_base = take(4ull * n);
     bytes = o;
   }
 };
@@ -373,7 +384,6 @@ static int deflate_stored_batch(zs_ctx* c, int wrap, uint32_t n, const uint8_t* 
 // segments, two rounds' speculative passes at once) for a batch of n streams?
 // The whole batch decides (chunks of one batch share the scratch layout).
 static int parse_waves_for(const zs_ctx* c, uint32_t n) {
-  if (c->parse_win != 32) return 1;
   if (c->parse_waves) return c->parse_waves;
   return n < ZS_PARSE2W_AUTO ? 2 : 1;
 }
@@ -382,20 +392,12 @@ static uint32_t parse_seg_words(int w) {
   return w == 4 ? ZS_PARSE4W_SEG_WORDS : w == 2 ? ZS_PARSE2W_SEG_WORDS : ZS_PARSE_SEG_WORDS;
 }
 
-// Chunks a deflate batch of n streams is pipelined in (option chunks = 0).
-static uint32_t auto_chunks(uint32_t n, int level) {
-  (void)n;
-  (void)level;
-  return 1;
-}
-
-// One chunk of a deflate batch (streams [a, a + n) of the caller's batch, every
-// per-stream array already offset to a): the whole kernel sequence on stream st.
-static int deflate_chunk(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
-                         uint32_t max_len, uint32_t max_blk, const uint8_t* d_in, const uint64_t* d_in_off,
-                         const uint32_t* d_in_len, uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
-                         const uint64_t* d_pos, const uint32_t* d_blk, const uint32_t* d_rng, zs_stream* d_st,
-                         uint32_t* syms, uint32_t* pscr, uint32_t* check, int32_t* d_status, uint32_t* d_out_len) {
+// The deflate launch sequence of a batch (levels 1..9) on stream st.
+static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
+                          uint32_t max_len, uint32_t max_blk, const uint8_t* d_in, const uint64_t* d_in_off,
+                          const uint32_t* d_in_len, uint8_t* d_out, const uint64_t* d_out_off,
+                          const uint32_t* d_out_cap, const uint64_t* d_pos, const uint32_t* d_blk, zs_stream* d_st,
+                          uint32_t* syms, uint32_t* pscr, uint32_t* check, int32_t* d_status, uint32_t* d_out_len) {
   zs_block* d_bk = c->blocks.as<zs_block>();
   const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
   MARK("start");
@@ -410,7 +412,8 @@ static int deflate_chunk(zs_ctx* c, hipStream_t st, int level, int wrap, const z
       // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
       // longer ones: chain links + per-tile chain walk (deflate_match.hip)
       zs_k_bucket<<<n, 256, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
-      if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+      if (max_len > 65537u)
+        zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), 65537u);
       MARK("bucket");
       zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
                                      cfg.chain, cfg.nice);
@@ -421,29 +424,17 @@ static int deflate_chunk(zs_ctx* c, hipStream_t st, int level, int wrap, const z
         MARK("match");
       }
     } else {
-      // streams of <= 65537 bytes take the u16-head kernel, the others the u32 one
-      zs_k_prev16<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
-      if (max_len > 65537u) zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>());
+      // cross-check (option match_sweep = 0): the chain-walk kernels for every stream
+      zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), 0u);
       MARK("prev");
       if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
                                                    c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
       MARK("match");
     }
-    if (c->parse_split) {
-      // the lazy parse: per-range speculative parse + merges, then per-stream joins and splice (deflate_parse.hip)
-      if (max_len)
-        zs_k_parse_a<<<dim3((max_len + ZS_PARSE_RANGE - 1) / ZS_PARSE_RANGE, n), 64, 0, st>>>(
-            d_in, d_in_off, d_in_len, d_pos, d_rng, c->mres.as<uint2>(), pscr, cfg.good, cfg.lazy);
-      zs_k_parse_b<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, d_rng, c->mres.as<uint2>(),
-                                     syms, d_bk, d_st, pscr, cfg.good, cfg.lazy);
-    } else {
-      auto parse = c->parse_win == 32 ? zs_k_parse : c->parse_win == 16 ? zs_k_parse16 : zs_k_parse_direct;
-      const int pw = c->cur_pw;  // decided for the whole batch (scratch layout)
-      if (pw == 2) parse = zs_k_parse_2w;
-      if (pw == 4) parse = zs_k_parse_4w;
-      parse<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(),
-                              syms, d_bk, d_st, pscr, cfg.good, cfg.lazy);
-    }
+    const int pw = c->cur_pw;  // waves per stream of the lazy parse (deflate_parse.hip)
+    auto parse = pw == 4 ? zs_k_parse_4w : pw == 2 ? zs_k_parse_2w : zs_k_parse;
+    parse<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), syms, d_bk, d_st, pscr,
+                                 cfg.good, cfg.lazy);
     MARK("parse");
   } else {
     const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
@@ -468,10 +459,28 @@ static int deflate_chunk(zs_ctx* c, hipStream_t st, int level, int wrap, const z
   return ZS_OK;
 }
 
+// Per-stream check value (the reference's strm.adler after the stream,
+// deflate.ts:155-159,462,778,788): adler32 (zlib) / crc32 (gzip) of the input,
+// 1 for deflate-raw (adler32(0), never updated without a wrapper); 0 for a
+// stream that failed.
+__global__ void zs_k_deflate_check(const int32_t* status, const uint32_t* check, int wrap, uint32_t* out, int n) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  out[s] = status[s] != ZS_Z_STREAM_END ? 0u : wrap ? check[s] : 1u;
+}
+
 extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* d_in,
                                        const uint64_t* in_off, const uint32_t* in_len, uint8_t* d_out,
                                        const uint64_t* out_off, const uint32_t* out_cap, int32_t* d_status,
                                        uint32_t* d_out_len, void* hip_stream) {
+  return zs_deflate_batch_device_ex(c, level, wbits, n, d_in, in_off, in_len, d_out, out_off, out_cap, d_status,
+                                    d_out_len, nullptr, hip_stream);
+}
+
+extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* d_in,
+                                          const uint64_t* in_off, const uint32_t* in_len, uint8_t* d_out,
+                                          const uint64_t* out_off, const uint32_t* out_cap, int32_t* d_status,
+                                          uint32_t* d_out_len, uint32_t* d_check, void* hip_stream) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   if (level == -1) level = 6;  // Z_DEFAULT_COMPRESSION, deflate.ts:268-270
   int wrap;
@@ -483,8 +492,15 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
-  if (level == 0) return deflate_stored_batch(c, wrap, n, d_in, in_off, in_len, d_out, out_off, out_cap, d_status,
-                                              d_out_len, st);
+  if (level == 0) {
+    const int r = deflate_stored_batch(c, wrap, n, d_in, in_off, in_len, d_out, out_off, out_cap, d_status,
+                                       d_out_len, st);
+    if (r == ZS_OK && d_check) {
+      zs_k_deflate_check<<<(n + 255) / 256, 256, 0, st>>>(d_status, c->check.as<uint32_t>(), wrap, d_check, (int)n);
+      HIPCHK(hipGetLastError());
+    }
+    return r;
+  }
   // host-side layout: workspace bases
   MetaLayout ml(n);
   c->hmeta.resize(ml.bytes);
@@ -496,15 +512,12 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   memcpy(hm + ml.out_cap, out_cap, 4ull * n);
   uint64_t* pos_base = (uint64_t*)(hm + ml.pos_base);
   uint32_t* blk_base = (uint32_t*)(hm + ml.blk_base);
-  uint32_t* range_base = (uint32_t*)(hm + ml.range_base);
   uint64_t P = 0;
-  uint32_t B = 0, max_len = 0, max_blk = 0, NR = 0;
+  uint32_t B = 0, max_len = 0, max_blk = 0;
   for (uint32_t i = 0; i < n; i++) {
     if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
     pos_base[i] = P;
     blk_base[i] = B;
-    range_base[i] = NR;
-    NR += (in_len[i] + ZS_PARSE_RANGE - 1) / ZS_PARSE_RANGE;
     P += ((uint64_t)in_len[i] + 7) & ~7ull;  // per-position tables start 8-aligned (16-B link loads in zs_k_match)
     const uint32_t nb = in_len[i] / ZS_SYM_END + 2;
     B += nb;
@@ -515,10 +528,9 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   HIPCHK(c->prevd.ensure(2 * P + 64));
   HIPCHK(c->mres.ensure(8 * P + 64));
   HIPCHK(c->syms.ensure(4 * (P + n) + 64));
-  c->cur_pw = level >= 4 && !c->parse_split ? parse_waves_for(c, n) : 1;
+  c->cur_pw = level >= 4 ? parse_waves_for(c, n) : 1;
   if (level >= 4)
-    HIPCHK(c->pscr.ensure(c->parse_split ? 4ull * ZS_PARSE_RANGE_WORDS * (NR + 1)
-                                         : 4ull * parse_seg_words(c->cur_pw) * (P / parse_seg(c->cur_pw) + n + 1)));
+    HIPCHK(c->pscr.ensure(4ull * parse_seg_words(c->cur_pw) * (P / parse_seg(c->cur_pw) + n + 1)));
   HIPCHK(c->blocks.ensure(sizeof(zs_block) * (size_t)B));
   HIPCHK(c->streams.ensure(sizeof(zs_stream) * (size_t)n));
   HIPCHK(c->codes.ensure(4ull * (ZS_L_CODES + ZS_D_CODES) * B));
@@ -526,47 +538,15 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
   HIPCHK(c->check.ensure(4ull * n));
   HIPCHK(hipMemcpyAsync(c->meta.p, hm, ml.bytes, hipMemcpyHostToDevice, st));
   uint8_t* dm = c->meta.as<uint8_t>();
-  const uint64_t* d_in_off = (const uint64_t*)(dm + ml.in_off);
-  const uint32_t* d_in_len = (const uint32_t*)(dm + ml.in_len);
-  const uint64_t* d_out_off = (const uint64_t*)(dm + ml.out_off);
-  const uint32_t* d_out_cap = (const uint32_t*)(dm + ml.out_cap);
-  const uint64_t* d_pos = (const uint64_t*)(dm + ml.pos_base);
-  const uint32_t* d_blk = (const uint32_t*)(dm + ml.blk_base);
-  const uint32_t* d_rng = (const uint32_t*)(dm + ml.range_base);
-  zs_stream* d_st = c->streams.as<zs_stream>();
-  const zs_level_cfg cfg = kLevels[level];
-  // The batch runs as K contiguous chunks of streams, alternating between the
-  // context's two HIP streams: chunk j+1's match finding (which fills the chip)
-  // runs while chunk j's parse, trees and emit (one wave per stream or block,
-  // latency-bound) finish.  Every kernel indexes its workspace through the
-  // per-stream bases, so a chunk is the same launch sequence over offset
-  // per-stream arrays.
-  uint32_t K = c->chunks ? (uint32_t)c->chunks : auto_chunks(n, level);
-  K = std::max(1u, std::min(K, n));
-  if (K > 1) {  // the side stream starts after the caller's prior work and the metadata upload
-    HIPCHK(hipEventRecord(c->fork, st));
-    HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
-  }
-  for (uint32_t j = 0; j < K; j++) {
-    const uint32_t a = (uint32_t)((uint64_t)n * j / K), e = (uint32_t)((uint64_t)n * (j + 1) / K);
-    uint32_t cmax_len = 0, cmax_blk = 0;
-    for (uint32_t i = a; i < e; i++) {
-      cmax_len = std::max(cmax_len, in_len[i]);
-      cmax_blk = std::max(cmax_blk, in_len[i] / ZS_SYM_END + 2);
-    }
-    hipStream_t X = (j & 1) ? c->side : st;
-    const int r = deflate_chunk(c, X, level, wrap, cfg, e - a, cmax_len, cmax_blk, d_in, d_in_off + a, d_in_len + a,
-                                d_out, d_out_off + a, d_out_cap + a, d_pos + a, d_blk + a, d_rng + a, d_st + a,
-                                c->syms.as<uint32_t>() + a,
-                                c->pscr.as<uint32_t>() + (c->parse_split ? 0
-                                                          : (size_t)parse_seg_words(c->cur_pw) * a),
-                                c->check.as<uint32_t>() + a, d_status + a, d_out_len + a);
-    if (r != ZS_OK) return r;
-  }
-  if (K > 1) {
-    HIPCHK(hipEventRecord(c->join, c->side));
-    HIPCHK(hipStreamWaitEvent(st, c->join, 0));
-  }
+  const int r = deflate_launch(c, st, level, wrap, kLevels[level], n, max_len, max_blk, d_in,
+                               (const uint64_t*)(dm + ml.in_off), (const uint32_t*)(dm + ml.in_len), d_out,
+                               (const uint64_t*)(dm + ml.out_off), (const uint32_t*)(dm + ml.out_cap),
+                               (const uint64_t*)(dm + ml.pos_base), (const uint32_t*)(dm + ml.blk_base),
+                               c->streams.as<zs_stream>(), c->syms.as<uint32_t>(), c->pscr.as<uint32_t>(),
+                               c->check.as<uint32_t>(), d_status, d_out_len);
+  if (r != ZS_OK) return r;
+  if (d_check)
+    zs_k_deflate_check<<<(n + 255) / 256, 256, 0, st>>>(d_status, c->check.as<uint32_t>(), wrap, d_check, (int)n);
   MARK("end");
   HIPCHK(hipGetLastError());
   return ZS_OK;  // timing marks are collected when queried (no wait here)
@@ -617,10 +597,11 @@ __global__ void zs_k_compact(const uint8_t* __restrict__ src, const uint64_t* __
 // Compacts the produced outputs (len[] already on the host) and copies them
 // into the caller's buffer at out_off[].
 static int fetch_out(zs_ctx* c, uint32_t n, const uint64_t* soff, const uint32_t* d_len, const uint32_t* len,
-                     uint8_t* out, const uint64_t* out_off) {
+                     const uint32_t* cap, uint8_t* out, const uint64_t* out_off) {
   std::vector<uint64_t> offs(2ull * n), poff(n);
   uint64_t P = 0;
   for (uint32_t i = 0; i < n; i++) {
+    if (len[i] > cap[i]) return fail(ZS_MEM_ERROR, "stream %s reported more output than its capacity", std::to_string(i).c_str());
     offs[i] = soff[i];
     offs[n + i] = poff[i] = P;
     P += ((uint64_t)len[i] + 3) & ~3ull;
@@ -641,6 +622,13 @@ static int fetch_out(zs_ctx* c, uint32_t n, const uint64_t* soff, const uint32_t
 extern "C" int zs_deflate_batch(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* in, const uint64_t* in_off,
                                 const uint32_t* in_len, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                 int32_t* status, uint32_t* out_len) {
+  return zs_deflate_batch_ex(c, level, wbits, n, in, in_off, in_len, out, out_off, out_cap, status, out_len, nullptr);
+}
+
+extern "C" int zs_deflate_batch_ex(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* in,
+                                   const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
+                                   const uint64_t* out_off, const uint32_t* out_cap, int32_t* status,
+                                   uint32_t* out_len, uint32_t* check) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   HIPCHK(hipSetDevice(c->device));
   std::vector<uint64_t> doff, ooff(n);
@@ -654,16 +642,19 @@ extern "C" int zs_deflate_batch(zs_ctx* c, int level, int wbits, uint32_t n, con
     ototal += ocap[i];
   }
   HIPCHK(c->d_out.ensure(ototal + 16));
-  HIPCHK(c->d_res.ensure(8ull * n + 16));
+  HIPCHK(c->d_res.ensure(12ull * n + 16));
   int32_t* d_status = c->d_res.as<int32_t>();
   uint32_t* d_len = (uint32_t*)(d_status + n);
-  r = zs_deflate_batch_device(c, level, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len, c->d_out.as<uint8_t>(),
-                              ooff.data(), ocap.data(), d_status, d_len, c->stream);
+  uint32_t* d_chk = d_len + n;
+  r = zs_deflate_batch_device_ex(c, level, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len,
+                                 c->d_out.as<uint8_t>(), ooff.data(), ocap.data(), d_status, d_len,
+                                 check ? d_chk : nullptr, c->stream);
   if (r != ZS_OK) return r;
   HIPCHK(hipMemcpyAsync(status, d_status, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(out_len, d_len, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  if (check) HIPCHK(hipMemcpyAsync(check, d_chk, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  return fetch_out(c, n, ooff.data(), d_len, out_len, out, out_off);  // out_len is 0 for failed streams
+  return fetch_out(c, n, ooff.data(), d_len, out_len, ocap.data(), out, out_off);  // out_len is 0 for failed streams
 }
 
 static int checksum_batch(zs_ctx* c, int kind, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
@@ -880,10 +871,37 @@ __global__ void zs_k_inflate_finish(const zs_inflate_result* r, const zs_lane_re
   consumed[s] = r[s].consumed;
 }
 
+// Per-stream check value (the reference's strm.adler after a successful
+// stream, inflate.ts:105,1014,1080): the adler32 (zlib) / crc32 (gzip) of the
+// output -- equal to the verified trailer, so read from it; 0 for raw and
+// deflate64-raw (createStream's initial _adler, common/utils.ts:49, never
+// updated without a wrapper) and for a failed stream.
+__global__ void zs_k_inflate_check(const uint8_t* in, const uint64_t* in_off, const int32_t* status,
+                                   const uint32_t* consumed, int wbits, uint32_t* out, int n) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  uint32_t v = 0;
+  if (status[s] == ZS_Z_STREAM_END && wbits > 0) {
+    const uint8_t* t = in + in_off[s] + consumed[s] - (wbits == 31 ? 8 : 4);
+    v = wbits == 31 ? (uint32_t)t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24
+                    : (uint32_t)t[0] << 24 | (uint32_t)t[1] << 16 | (uint32_t)t[2] << 8 | (uint32_t)t[3];
+  }
+  out[s] = v;
+}
+
 extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
                                        const uint32_t* in_len, uint8_t* d_out, const uint64_t* out_off,
                                        const uint32_t* out_cap, int32_t* d_status, int32_t* d_phase, int32_t* d_msg,
                                        uint32_t* d_out_len, uint32_t* d_consumed, void* hip_stream) {
+  return zs_inflate_batch_device_ex(c, wbits, n, d_in, in_off, in_len, d_out, out_off, out_cap, d_status, d_phase,
+                                    d_msg, d_out_len, d_consumed, nullptr, hip_stream);
+}
+
+extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, const uint8_t* d_in,
+                                          const uint64_t* in_off, const uint32_t* in_len, uint8_t* d_out,
+                                          const uint64_t* out_off, const uint32_t* out_cap, int32_t* d_status,
+                                          int32_t* d_phase, int32_t* d_msg, uint32_t* d_out_len,
+                                          uint32_t* d_consumed, uint32_t* d_check, void* hip_stream) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   // inflateInit2_ / inflateReset2 validation (inflate.ts:138-192) for the stream-layer formats
   if (!(wbits == -15 || wbits == 15 || wbits == 31 || wbits == -16))
@@ -976,7 +994,14 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
   HIPCHK(hipMemsetAsync(c->lstat.p, 0, 4, st));
   zs_k_inflate_finish<<<(n + 255) / 256, 256, 0, st>>>(c->istate.as<zs_inflate_result>(), lres, d_status, d_phase,
                                                        d_msg, d_out_len, d_consumed, (int)n, c->lstat.as<uint32_t>());
-  c->last_stream = st;
+  if (!c->lane_count_host) {
+    HIPCHK(hipHostMalloc((void**)&c->lane_count_host, 64, hipHostMallocDefault));
+    HIPCHK(hipEventCreateWithFlags(&c->lane_ev, hipEventDisableTiming));
+  }
+  HIPCHK(hipMemcpyAsync(c->lane_count_host, c->lstat.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipEventRecord(c->lane_ev, st));
+  if (d_check)
+    zs_k_inflate_check<<<(n + 255) / 256, 256, 0, st>>>(d_in, d_ioff, d_status, d_consumed, wbits, d_check, (int)n);
   MARK("finish");
   HIPCHK(hipGetLastError());
   return ZS_OK;  // timing marks are collected when queried (no wait here)
@@ -985,6 +1010,14 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
 extern "C" int zs_inflate_batch(zs_ctx* c, int wbits, uint32_t n, const uint8_t* in, const uint64_t* in_off,
                                 const uint32_t* in_len, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                                 int32_t* status, int32_t* phase, int32_t* msg, uint32_t* out_len, uint32_t* consumed) {
+  return zs_inflate_batch_ex(c, wbits, n, in, in_off, in_len, out, out_off, out_cap, status, phase, msg, out_len,
+                             consumed, nullptr);
+}
+
+extern "C" int zs_inflate_batch_ex(zs_ctx* c, int wbits, uint32_t n, const uint8_t* in, const uint64_t* in_off,
+                                   const uint32_t* in_len, uint8_t* out, const uint64_t* out_off,
+                                   const uint32_t* out_cap, int32_t* status, int32_t* phase, int32_t* msg,
+                                   uint32_t* out_len, uint32_t* consumed, uint32_t* check) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   HIPCHK(hipSetDevice(c->device));
   std::vector<uint64_t> doff, ooff(n);
@@ -994,20 +1027,23 @@ extern "C" int zs_inflate_batch(zs_ctx* c, int wbits, uint32_t n, const uint8_t*
   std::vector<uint32_t> ocap(n);
   for (uint32_t i = 0; i < n; i++) { ooff[i] = ototal; ocap[i] = out_cap[i]; ototal += ((uint64_t)out_cap[i] + 3) & ~3ull; }
   HIPCHK(c->d_out.ensure(ototal + 16));
-  HIPCHK(c->d_res.ensure(20ull * n + 16));
+  HIPCHK(c->d_res.ensure(24ull * n + 16));
   int32_t* d_status = c->d_res.as<int32_t>();
   int32_t* d_phase = d_status + n;
   int32_t* d_msg = d_phase + n;
   uint32_t* d_len = (uint32_t*)(d_msg + n);
   uint32_t* d_cons = d_len + n;
-  r = zs_inflate_batch_device(c, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len, c->d_out.as<uint8_t>(),
-                              ooff.data(), ocap.data(), d_status, d_phase, d_msg, d_len, d_cons, c->stream);
+  uint32_t* d_chk = d_cons + n;
+  r = zs_inflate_batch_device_ex(c, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len, c->d_out.as<uint8_t>(),
+                                 ooff.data(), ocap.data(), d_status, d_phase, d_msg, d_len, d_cons,
+                                 check ? d_chk : nullptr, c->stream);
   if (r != ZS_OK) return r;
+  if (check) HIPCHK(hipMemcpyAsync(check, d_chk, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(status, d_status, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(phase, d_phase, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(msg, d_msg, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(out_len, d_len, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(consumed, d_cons, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  return fetch_out(c, n, ooff.data(), d_len, out_len, out, out_off);
+  return fetch_out(c, n, ooff.data(), d_len, out_len, ocap.data(), out, out_off);
 }

@@ -842,7 +842,7 @@ __global__ __launch_bounds__(256) void zs_k_stored(const uint8_t* __restrict__ i
   const bool fits = total <= out_cap[s];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     status[s] = fits ? ZS_Z_STREAM_END : ZS_Z_BUF_ERROR;
-    out_len_res[s] = (uint32_t)total;
+    out_len_res[s] = fits ? (uint32_t)total : 0u;  // as zs_k_finish: failed streams produce nothing
   }
   if (!fits) return;
   const uint8_t* src = in + in_off[s];

@@ -33,15 +33,15 @@
 // position with the same hash -- the reference's prev[] link.  head[] holds
 // q + 1 (absolute, 32-bit), so no slide (deflate.ts:125-141) is needed.
 #define ZS_PREV_STAGE 4096u
-#define ZS_PREV16_MAX 65537u  // positions <= n-3, so position + 1 <= 65535
 __global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                 const uint32_t* __restrict__ in_len,
-                                                const uint64_t* __restrict__ pos_base, uint16_t* __restrict__ prevd) {
+                                                const uint64_t* __restrict__ pos_base, uint16_t* __restrict__ prevd,
+                                                uint32_t min_len) {
   __shared__ uint32_t head[32768];
   __shared__ uint32_t stg[ZS_PREV_STAGE / 4 + 2];  // input bytes [c0, c0 + 4096 + 8)
   const int s = blockIdx.x;
   const uint32_t n = in_len[s];
-  if (n <= ZS_PREV16_MAX) return;  // zs_k_prev16's stream
+  if (n <= min_len) return;  // a stream zs_k_bucket + zs_k_sweep handle (min_len 65537; 0 = every stream)
   const uint8_t* src = in + in_off[s];
   uint16_t* out = prevd + pos_base[s];
   const uint32_t lane = threadIdx.x;
@@ -93,83 +93,6 @@ __global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, 
   }
 }
 
-// -------------------------------------------------------------- zs_k_prev16
-// zs_k_prev for streams of at most ZS_PREV16_MAX bytes (every inserted
-// position + 1 fits in 16 bits): head[] packs two u16 buckets per LDS word
-// (64 KiB instead of 128 KiB, so two streams share a CU), and the lane-ordered
-// exchange of one bucket is a ds_mskor_rtn_b32 -- (word & ~mask) | value, the
-// old word returned -- which replaces one half of the word atomically.  The
-// same lane-order property is required of it (checked by zs_selftest).
-typedef __attribute__((address_space(3))) uint32_t zs_lds_u32;
-static __device__ __forceinline__ uint32_t zs_lds_addr(uint32_t* p) { return (uint32_t)(uintptr_t)(zs_lds_u32*)p; }
-
-__global__ __launch_bounds__(64) void zs_k_prev16(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                  const uint32_t* __restrict__ in_len,
-                                                  const uint64_t* __restrict__ pos_base, uint16_t* __restrict__ prevd) {
-  __shared__ uint32_t head[16384];
-  __shared__ uint32_t stg[ZS_PREV_STAGE / 4 + 2];  // input bytes [c0, c0 + 4096 + 8)
-  const int s = blockIdx.x;
-  const uint32_t n = in_len[s];
-  if (n > ZS_PREV16_MAX) return;  // zs_k_prev's stream
-  const uint8_t* src = in + in_off[s];
-  uint16_t* out = prevd + pos_base[s];
-  const uint32_t lane = threadIdx.x;
-  for (uint32_t i = lane; i < 16384; i += 64) head[i] = 0;
-  const bool aligned = ((uintptr_t)src & 3u) == 0;
-  for (uint32_t c0 = 0; c0 < n; c0 += ZS_PREV_STAGE) {
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < ZS_PREV_STAGE / 4 + 2; i += 64) {
-      const uint32_t at = c0 + 4 * i;
-      uint32_t v = 0;
-      if (aligned && at + 4 <= n) {
-        v = *(const uint32_t*)(src + at);
-      } else {
-        for (uint32_t k = 0; k < 4; k++)
-          if (at + k < n) v |= (uint32_t)src[at + k] << (8 * k);
-      }
-      stg[i] = v;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t c1 = min(n, c0 + ZS_PREV_STAGE);
-    for (uint32_t g0 = c0; g0 < c1; g0 += 256) {
-      uint32_t a[4], m[4], v[4], sh[4], e[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t p = g0 + 64 * j + lane;
-        const uint32_t o = p - c0;
-        const uint32_t w = __builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u);
-        const bool valid = p + 2 < n && p < c1;  // positions <= n-3 are inserted (deflate.ts:1367-1370)
-        const uint32_t h = (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
-        sh[j] = 16u * (h & 1u);
-        a[j] = zs_lds_addr(&head[h >> 1]);
-        m[j] = valid ? 0xffffu << sh[j] : 0u;  // an invalid lane ORs nothing into the word
-        v[j] = valid ? (p + 1) << sh[j] : 0u;
-      }
-      // in order: group j's exchanges land after group j-1's (LDS executes a wave's ops in order)
-      asm volatile(
-          "ds_mskor_rtn_b32 %0, %4, %8, %12\n\t"
-          "ds_mskor_rtn_b32 %1, %5, %9, %13\n\t"
-          "ds_mskor_rtn_b32 %2, %6, %10, %14\n\t"
-          "ds_mskor_rtn_b32 %3, %7, %11, %15\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(e[0]), "=&v"(e[1]), "=&v"(e[2]), "=&v"(e[3])
-          : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]),
-            "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3])
-          : "memory");
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t p = g0 + 64 * j + lane;
-        if (p < c1) {
-          const uint32_t q1 = (e[j] >> sh[j]) & 0xffffu;  // previous position + 1, 0 = none
-          const uint32_t d = q1 ? p + 1 - q1 : 0u;
-          out[p] = (uint16_t)(m[j] && d != 0u && d <= 32767u ? d : 0xffffu);
-        }
-      }
-    }
-  }
-}
 
 // --------------------------------------------------------------- zs_k_match
 #define ZS_TILE 8192u

@@ -70,10 +70,10 @@ struct zs_round_state {
 // on the previous step's entry, so direct loads put the full memory latency on
 // every step.  Entry k of lane l is at m[k / 2][l] (a lane's reads are 16 B
 // apart from its neighbours': conflict-free), bytes in[w + 4 j, +4) at s[j][l].
-// WIN = 32 (the default, 19 KiB of LDS: 8 workgroups per CU) halves the
-// stages of WIN = 16 (10 KiB: all 16 workgroups a CU gets at 4096 streams
-// fit) and measures faster: 1.54 vs 1.77 ms at 4096 streams, 2.99 ms with
-// direct loads (WIN = 0); 0.40 / 0.42 / 0.54 ms at 512 (tools/ab_parse.sh).
+// WIN = 32 (19 KiB of LDS: 8 workgroups per CU) halves the stages of WIN = 16
+// (10 KiB) and measured faster in round 2: 1.54 vs 1.77 ms at 4096 streams,
+// 2.99 ms with direct loads (WIN = 0); 0.40 / 0.42 / 0.54 ms at 512.  Only
+// WIN = 32 is built.
 template <uint32_t WIN>
 struct zs_parse_win {
   uint4 m[WIN / 2][64];
@@ -440,9 +440,7 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
     zs_parse_body<WIN, SEG, NWV>(W[w_], T[w_], RS, in, in_off, in_len, pos_base, blk_base, mres, syms, blocks,      \
                                  streams, scratch, good, lazy);                                                     \
   }
-ZS_PARSE_KERNEL(zs_k_parse16, 16, ZS_PARSE_SEG, 1)
 ZS_PARSE_KERNEL(zs_k_parse, 32, ZS_PARSE_SEG, 1)
-ZS_PARSE_KERNEL(zs_k_parse_direct, 0, ZS_PARSE_SEG, 1)
 // two waves per stream, 512-position segments: half the speculative pass per lane (small batches)
 ZS_PARSE_KERNEL(zs_k_parse_2w, 32, ZS_PARSE2W_SEG, 2)
 // four waves per stream, 256-position segments

@@ -1,5 +1,5 @@
 // selftest.hip -- run-time check of the one hardware property the chain
-// builder (zs_k_prev, deflate_match.hip) relies on beyond the ISA manual:
+// builders (zs_k_prev, zs_k_bucket, zs_k_fast) rely on beyond the ISA manual:
 // same-address LDS atomics (ds_wrxchg_rtn_b32, ds_mskor_rtn_b32 on 16-bit
 // halves, and ds_add_rtn_u32 on whole words and on 16-bit halves) issued by
 // ONE wave instruction are applied in increasing lane order on gfx950.  Probed
@@ -20,7 +20,7 @@ __global__ __launch_bounds__(64) void zs_k_selftest(uint32_t* __restrict__ bad, 
   __shared__ uint32_t tab[256];
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t keys[64];
-  __shared__ uint32_t half[128];  // 256 u16 buckets, two per word (zs_k_prev16)
+  __shared__ uint32_t half[128];  // 256 u16 buckets, two per word (zs_k_fast's head[])
   __shared__ uint32_t hcnt[128];  // 256 u16 counters, two per word (zs_k_bucket)
   const uint32_t lane = threadIdx.x;
   const uint32_t mask = (blockIdx.x & 3u) == 0 ? 0u : (blockIdx.x & 3u) == 1 ? 3u : (blockIdx.x & 3u) == 2 ? 15u : 255u;

@@ -31,9 +31,7 @@ struct zs_stream {
 };
 
 __global__ void zs_k_prev(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                          uint16_t* prevd);
-__global__ void zs_k_prev16(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                            uint16_t* prevd);
+                          uint16_t* prevd, uint32_t min_len);
 __global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint16_t* prevd, uint2* mres, int chain, int nice, uint32_t min_len);
 // levels 4..9, streams of at most 65,537 bytes (deflate_sweep.hip)
@@ -41,15 +39,12 @@ __global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uin
                             uint16_t* members, uint2* mres);
 __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint16_t* members, uint2* mres, int chain, int nice);
-// the one-wave lazy parse (deflate_parse.hip): pass A stages 32 / 16 match-table
-// entries per lane in LDS (zs_k_parse / zs_k_parse16) or loads them directly (zs_k_parse_direct)
+// the lazy parse (deflate_parse.hip): pass A stages 32 match-table entries per lane in LDS
 #define ZS_PARSE_DECL(name)                                                                                        \
   __global__ void name(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base, \
                        const uint32_t* blk_base, const uint2* mres, uint32_t* syms, zs_block* blocks,              \
                        zs_stream* streams, uint32_t* scratch, int good, int lazy);
 ZS_PARSE_DECL(zs_k_parse)
-ZS_PARSE_DECL(zs_k_parse16)
-ZS_PARSE_DECL(zs_k_parse_direct)
 ZS_PARSE_DECL(zs_k_parse_2w)  // two waves per stream, ZS_PARSE2W_SEG-position segments
 ZS_PARSE_DECL(zs_k_parse_4w)  // four waves per stream, ZS_PARSE4W_SEG-position segments
 // parse scratch words per 1024-position segment (deflate_parse.hip)
@@ -59,14 +54,6 @@ ZS_PARSE_DECL(zs_k_parse_4w)  // four waves per stream, ZS_PARSE4W_SEG-position 
 #define ZS_PARSE2W_SEG_WORDS 2060u
 #define ZS_PARSE4W_SEG 256u
 #define ZS_PARSE4W_SEG_WORDS 1292u
-// the two-kernel parse (deflate_parse2.hip): positions per range, scratch words per range
-#define ZS_PARSE_RANGE 2048u
-#define ZS_PARSE_RANGE_WORDS 5376u
-__global__ void zs_k_parse_a(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                             const uint32_t* range_base, const uint2* mres, uint32_t* scratch, int good, int lazy);
-__global__ void zs_k_parse_b(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                             const uint32_t* blk_base, const uint32_t* range_base, const uint2* mres, uint32_t* syms,
-                             zs_block* blocks, zs_stream* streams, uint32_t* scratch, int good, int lazy);
 template <int NW>
 __global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,

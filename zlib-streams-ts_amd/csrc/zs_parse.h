@@ -1,6 +1,6 @@
 // zs_parse.h -- one step of deflate_slow's lazy parse over the match table
-// (deflate.ts:1356-1426) and the slide schedule, shared by zs_k_parse
-// (deflate_parse.hip) and zs_k_parse_a / zs_k_parse_b (deflate_parse2.hip).
+// (deflate.ts:1356-1426) and the slide schedule, used by the zs_k_parse family
+// (deflate_parse.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

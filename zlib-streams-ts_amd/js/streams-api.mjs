@@ -15,9 +15,12 @@ import { createRequire } from "module";
 const require = createRequire(import.meta.url);
 const addon = require("./zsnapi.node");
 
-// format -> windowBits, streams.ts:220 (compression) and 233 (decompression)
-const COMPRESS_WBITS = { "deflate": 15, "deflate-raw": -15, "gzip": 31 };
-const DECOMPRESS_WBITS = { "deflate": 15, "deflate-raw": -15, "gzip": 31, "deflate64-raw": -16 };
+// format -> windowBits exactly as streams.ts:220 (compression) and 233
+// (decompression): loose comparisons, and every other value -- unknown strings,
+// undefined -- falls through to 15 ("deflate", the zlib wrapper).
+const compressWbits = (format) => (format == "gzip" ? 15 + 16 : format == "deflate-raw" ? -15 : 15);
+const decompressWbits = (format) =>
+  format == "gzip" ? 15 + 16 : format == "deflate-raw" ? -15 : format == "deflate64-raw" ? -16 : 15;
 const Z_STREAM_END = 1;
 const Z_STREAM_ERROR = -2;
 const PHASE_INIT = 1, PHASE_FINISH = 3;
@@ -38,26 +41,24 @@ function checkInputs(inputs) {
   });
 }
 
-function compressWbits(format) {
-  const w = COMPRESS_WBITS[format];
-  if (w === undefined) throw new TypeError(`Unsupported compression format: ${format}`);
-  return w;
-}
-
-function decompressWbits(format) {
-  const w = DECOMPRESS_WBITS[format];
-  if (w === undefined) throw new TypeError(`Unsupported decompression format: ${format}`);
-  return w;
+// The device set of a batch (SURVEY.md 8(b) "device mask"): options.devices
+// (an array of GPU indices: the batch is split into contiguous stream ranges,
+// one per GPU, zs_pool) or options.device (one index); default GPU 0.
+function devicesOf(options) {
+  if (Array.isArray(options.devices)) return options.devices;
+  return options.device === undefined ? 0 : options.device;
 }
 
 // The addon runs each batch on a worker thread (napi_async_work) and settles a
 // Promise: the event loop is not blocked while the GPU works.
 async function runCompress(inputs, format, options) {
+  options = options || {};
   const wbits = compressWbits(format);
-  const level = options.level === undefined ? -1 : options.level;  // -1 -> 6, deflate.ts:268-270
+  // streams.ts:221: a level that is not a number means Z_DEFAULT_COMPRESSION (-1 -> 6, deflate.ts:268-270)
+  const level = typeof options.level == "number" ? options.level : -1;
   let res;
   try {
-    res = await addon.compressBatch(checkInputs(inputs), wbits, level, options.device || 0);
+    res = await addon.compressBatch(checkInputs(inputs), wbits, level, devicesOf(options));
   } catch (e) {
     // argument validation of deflateInit2_ (deflate.ts:281-294) surfaces as the stream layer's init error
     if (e.code === String(Z_STREAM_ERROR)) throw streamError(Z_STREAM_ERROR, PHASE_INIT);
@@ -67,10 +68,11 @@ async function runCompress(inputs, format, options) {
 }
 
 async function runDecompress(inputs, format, options) {
+  options = options || {};
   const wbits = decompressWbits(format);
   const ins = checkInputs(inputs);
-  const cap = options.outCapacity === undefined ? ins.map((x) => Math.max(65536, 16 * x.length)) : options.outCapacity;
-  const res = await addon.decompressBatch(ins, wbits, cap, options.device || 0);
+  // no outCapacity: unbounded output, as DecompressionStream (streams.ts:46,132-182); a caller cap is a cap
+  const res = await addon.decompressBatch(ins, wbits, options.outCapacity, devicesOf(options));
   return res.outputs.map((out, i) => {
     if (res.status[i] === Z_STREAM_END) return out;
     const err = streamError(res.status[i], res.phase[i]);
@@ -107,5 +109,18 @@ export async function decompressBatchSettled(inputs, format = "deflate", options
 }
 
 export const deflateBound = (length, format = "deflate") => addon.deflateBound(length, compressWbits(format));
+
+/** Per-stream results with the check value (the reference's strm.adler after the
+ * stream: adler32 / crc32 of the uncompressed bytes for "deflate" / "gzip"). */
+export async function compressBatchDetailed(inputs, format = "deflate", options = {}) {
+  options = options || {};
+  const level = typeof options.level == "number" ? options.level : -1;
+  return addon.compressBatch(checkInputs(inputs), compressWbits(format), level, devicesOf(options));
+}
+
+export async function decompressBatchDetailed(inputs, format = "deflate", options = {}) {
+  options = options || {};
+  return addon.decompressBatch(checkInputs(inputs), decompressWbits(format), options.outCapacity, devicesOf(options));
+}
 export const engineVersion = () => addon.version();
 export const selfTest = (device = 0) => addon.selfTest(device);

@@ -85,6 +85,43 @@ async function main() {
   let msg = "";
   try { await api.compressBatch([inputs[0]], "deflate", { level: 10 }); } catch (e) { msg = e.message; }
   expect(msg === "init failed: -2", "level 10 -> init failed: -2");
+  // DecompressionStream has no output cap (streams.ts:46,132-182): default options decode any ratio
+  const z64 = new Uint8Array(readFileSync(join(golden, "d64", "zeros_100k.deflate64")));
+  const [zout] = await api.decompressBatch([z64], "deflate64-raw");
+  expect(zout.length === 100000 && zout.every((b) => b === 0), "zeros_100k.deflate64 with default options");
+  const zeros = new Uint8Array(1 << 20);
+  for (const format of ["deflate-raw", "deflate", "gzip"]) {
+    const [zc] = await api.compressBatch([zeros], format);
+    const [zd] = await api.decompressBatch([zc], format);
+    expect(zd.length === zeros.length && zd.every((b) => b === 0), `1 MiB of zeros (${zc.length} B) back, ${format}`);
+  }
+  // an explicit cap is a cap
+  const capped = await api.decompressBatchSettled([z64], "deflate64-raw", { outCapacity: 4096 });
+  expect(capped[0].status === "rejected", "a caller cap below the output rejects");
+  // unknown formats fall through to windowBits 15 and non-number levels to the default (streams.ts:220-221,233)
+  const viaBogus = await api.compressBatch(inputs, "bogus");
+  const viaDeflate = await api.compressBatch(inputs, "deflate");
+  viaBogus.forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(viaDeflate[i])) === 0, `"bogus" == "deflate" ${i}`));
+  const backBogus = await api.decompressBatch(viaDeflate, "bogus");
+  backBogus.forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(inputs[i])) === 0, `decompress "bogus" ${i}`));
+  const viaString = await api.compressBatch(inputs, "deflate-raw", { level: "9" });
+  const viaDefault = await api.compressBatch(inputs, "deflate-raw", { level: 6 });
+  viaString.forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(viaDefault[i])) === 0, `level "9" -> default ${i}`));
+  // the device set: an explicit [0] is the default device's batch
+  const viaDevices = await api.compressBatch(inputs, "gzip", { devices: [0] });
+  const viaDevice = await api.compressBatch(inputs, "gzip");
+  viaDevices.forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(viaDevice[i])) === 0, `devices [0] ${i}`));
+  // check values: strm.adler after the stream
+  for (const format of ["deflate-raw", "deflate", "gzip"]) {
+    const d = await api.compressBatchDetailed(inputs, format);
+    const back = await api.decompressBatchDetailed(d.outputs, format);
+    d.outputs.forEach((o, i) => {
+      const want = format === "deflate-raw" ? 1 : format === "gzip" ? Buffer.from(o).readUInt32LE(o.length - 8)
+                                                                     : Buffer.from(o).readUInt32BE(o.length - 4);
+      expect(d.check[i] === want, `compress check ${format} ${i}`);
+      expect(back.check[i] === (format === "deflate-raw" ? 0 : want), `decompress check ${format} ${i}`);
+    });
+  }
   expect(api.selfTest() === 0, "LDS lane-order self-test");
   console.log("ok " + checks);
 }

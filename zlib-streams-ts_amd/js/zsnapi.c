@@ -6,12 +6,13 @@
  * host batch, runs zs_deflate_batch / zs_inflate_batch on the GPU and returns
  * fresh Uint8Arrays -- nothing is retained after the call (SURVEY.md 8(b)
  * "Ownership").  The batch calls return Promises: the GPU work runs on a libuv
- * worker thread (napi_async_work), so the event loop keeps running; batches
- * on one device are serialized (one context per GPU, created lazily on the JS
- * thread).
+ * worker thread (napi_async_work), so the event loop keeps running.  A batch
+ * runs on a device set (SURVEY.md 8(b) "device mask"): a zs_pool per distinct
+ * set, created lazily on the JS thread, splits it into contiguous stream
+ * ranges with one host thread per GPU (so an 8-GPU batch is not capped by
+ * libuv's 4-thread pool); batches on one set are serialized by the pool.
  */
 #include <node_api.h>
-#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,7 +21,14 @@
 #include "../../include/zs_gpu.h"
 
 #define MAX_DEV 64
-static zs_ctx *g_ctx[MAX_DEV];
+static zs_ctx *g_ctx[MAX_DEV]; /* selfTest only */
+
+#define MAX_POOLS 64
+static struct {
+  uint64_t mask;
+  zs_pool *pool;
+} g_pools[MAX_POOLS];
+static int g_npools;
 
 #define NAPI_OK(call)                                      \
   do {                                                     \
@@ -37,6 +45,13 @@ static napi_value throw_code(napi_env env, int code, const char *msg) {
   return NULL;
 }
 
+static void throw_unavailable(napi_env env) {
+  /* no device / self-test failure: the engine is unavailable, never a CPU fallback */
+  char m[600];
+  snprintf(m, sizeof m, "MI355X engine unavailable: %s", zs_last_error());
+  napi_throw_error(env, "ZS_UNAVAILABLE", m);
+}
+
 static zs_ctx *ctx_for(napi_env env, int dev) {
   if (dev < 0 || dev >= MAX_DEV) {
     throw_code(env, ZS_STREAM_ERROR, "device index out of range");
@@ -44,16 +59,60 @@ static zs_ctx *ctx_for(napi_env env, int dev) {
   }
   if (!g_ctx[dev]) {
     zs_ctx *c = NULL;
-    int r = zs_ctx_create(dev, &c);
-    if (r != ZS_OK) {  /* no device / self-test failure: the engine is unavailable, never a CPU fallback */
-      char m[600];
-      snprintf(m, sizeof m, "MI355X engine unavailable: %s", zs_last_error());
-      napi_throw_error(env, "ZS_UNAVAILABLE", m);
+    if (zs_ctx_create(dev, &c) != ZS_OK) {
+      throw_unavailable(env);
       return NULL;
     }
     g_ctx[dev] = c;
   }
   return g_ctx[dev];
+}
+
+/* device spec: a device index, an array of them, or undefined (device 0) -> bit mask;
+ * 0 on an invalid spec (a JS exception is pending) */
+static uint64_t device_mask(napi_env env, napi_value v) {
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok) return 0;
+  if (t == napi_undefined || t == napi_null) return 1;
+  bool arr = false;
+  napi_is_array(env, v, &arr);
+  uint32_t n = 1;
+  if (arr) napi_get_array_length(env, v, &n);
+  uint64_t m = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    napi_value e = v;
+    if (arr) napi_get_element(env, v, i, &e);
+    napi_valuetype et;
+    int32_t d = -1;
+    if (napi_typeof(env, e, &et) == napi_ok && et == napi_number) napi_get_value_int32(env, e, &d);
+    if (d < 0 || d >= MAX_DEV) {
+      napi_throw_error(env, "ZS_BAD_DEVICE", "devices must be GPU indices in 0..63");
+      return 0;
+    }
+    m |= 1ull << d;
+  }
+  if (!m) napi_throw_error(env, "ZS_BAD_DEVICE", "devices must name at least one GPU");
+  return m;
+}
+
+static zs_pool *pool_for(napi_env env, uint64_t mask) {
+  for (int i = 0; i < g_npools; i++)
+    if (g_pools[i].mask == mask) return g_pools[i].pool;
+  if (g_npools == MAX_POOLS) {
+    napi_throw_error(env, "ZS_BAD_DEVICE", "too many distinct device sets");
+    return NULL;
+  }
+  zs_pool *p = NULL;
+  const int r = zs_pool_create(mask, &p);
+  if (r != ZS_OK) {
+    if (r == ZS_STREAM_ERROR && strstr(zs_last_error(), "device mask")) napi_throw_error(env, "ZS_BAD_DEVICE", zs_last_error());
+    else throw_unavailable(env);
+    return NULL;
+  }
+  g_pools[g_npools].mask = mask;
+  g_pools[g_npools].pool = p;
+  g_npools++;
+  return p;
 }
 
 /* Borrowed view of one input. */
@@ -98,13 +157,25 @@ static napi_value make_u8(napi_env env, const uint8_t *src, size_t n) {
   return ta;
 }
 
-static napi_value make_i32(napi_env env, const int32_t *src, size_t n) {
+static napi_value make_32(napi_env env, const void *src, size_t n, napi_typedarray_type type) {
   void *data = NULL;
   napi_value ab, ta;
   if (napi_create_arraybuffer(env, 4 * n, &data, &ab) != napi_ok) return NULL;
   if (n) memcpy(data, src, 4 * n);
-  if (napi_create_typedarray(env, napi_int32_array, n, ab, 0, &ta) != napi_ok) return NULL;
+  if (napi_create_typedarray(env, type, n, ab, 0, &ta) != napi_ok) return NULL;
   return ta;
+}
+#define make_i32(env, src, n) make_32(env, src, n, napi_int32_array)
+#define make_u32(env, src, n) make_32(env, src, n, napi_uint32_array)
+
+/* an output capacity: a number clamped to 0 .. 4 GiB - 4 (the ABI's u32 lengths) */
+static uint32_t arg_cap(napi_env env, napi_value v, uint32_t dflt) {
+  napi_valuetype t;
+  double x = dflt;
+  if (napi_typeof(env, v, &t) == napi_ok && t == napi_number) napi_get_value_double(env, v, &x);
+  if (!(x > 0)) return 0;
+  if (x > 4294967292.0) x = 4294967292.0;
+  return (uint32_t)x;
 }
 
 static int32_t arg_i32(napi_env env, napi_value v, int32_t dflt) {
@@ -120,29 +191,25 @@ static int32_t arg_i32(napi_env env, napi_value v, int32_t dflt) {
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
-  int inflate;  /* 0 compress, 1 decompress */
-  int dev, wbits, level;
+  int inflate;   /* 0 compress, 1 decompress */
+  int unbounded; /* decompress without a caller capacity: zs_pool_inflate_batch_auto */
+  int wbits, level;
   uint32_t n;
-  zs_ctx *ctx;
+  zs_pool *pool;
   uint64_t *in_off, *out_off;
-  uint32_t *in_len, *cap, *olen, *cons;
+  uint32_t *in_len, *cap, *olen, *cons, *check;
   int32_t *status, *phase, *msg;
   uint8_t *blob, *out;
   int rc;
   char err[512];
 } job;
 
-/* one batch at a time per device context (the context's workspaces are reused) */
-static pthread_mutex_t g_dev_mtx[MAX_DEV];
-static pthread_once_t g_once = PTHREAD_ONCE_INIT;
-static void init_mutexes(void) {
-  for (int i = 0; i < MAX_DEV; i++) pthread_mutex_init(&g_dev_mtx[i], NULL);
-}
-
 static void job_free(job *j) {
   if (!j) return;
-  free(j->in_off); free(j->out_off); free(j->in_len); free(j->cap); free(j->olen); free(j->cons);
-  free(j->status); free(j->phase); free(j->msg); free(j->blob); free(j->out);
+  free(j->in_off); free(j->out_off); free(j->in_len); free(j->cap); free(j->olen); free(j->cons); free(j->check);
+  free(j->status); free(j->phase); free(j->msg); free(j->blob);
+  if (j->unbounded) zs_free(j->out);
+  else free(j->out);
   free(j);
 }
 
@@ -156,10 +223,12 @@ static job *job_new(uint32_t n) {
   j->cap = (uint32_t *)calloc(n + 1, 4);
   j->olen = (uint32_t *)calloc(n + 1, 4);
   j->cons = (uint32_t *)calloc(n + 1, 4);
+  j->check = (uint32_t *)calloc(n + 1, 4);
   j->status = (int32_t *)calloc(n + 1, 4);
   j->phase = (int32_t *)calloc(n + 1, 4);
   j->msg = (int32_t *)calloc(n + 1, 4);
-  if (!j->in_off || !j->out_off || !j->in_len || !j->cap || !j->olen || !j->cons || !j->status || !j->phase || !j->msg) {
+  if (!j->in_off || !j->out_off || !j->in_len || !j->cap || !j->olen || !j->cons || !j->check || !j->status ||
+      !j->phase || !j->msg) {
     job_free(j);
     return NULL;
   }
@@ -170,16 +239,17 @@ static job *job_new(uint32_t n) {
 static void job_execute(napi_env env, void *data) {
   job *j = (job *)data;
   (void)env;
-  pthread_mutex_lock(&g_dev_mtx[j->dev]);
   if (j->n == 0) j->rc = ZS_OK;
+  else if (j->inflate && j->unbounded)
+    j->rc = zs_pool_inflate_batch_auto(j->pool, j->wbits, j->n, j->blob, j->in_off, j->in_len, &j->out, j->out_off,
+                                       j->status, j->phase, j->msg, j->olen, j->cons, j->check);
   else if (j->inflate)
-    j->rc = zs_inflate_batch(j->ctx, j->wbits, j->n, j->blob, j->in_off, j->in_len, j->out, j->out_off, j->cap,
-                             j->status, j->phase, j->msg, j->olen, j->cons);
+    j->rc = zs_pool_inflate_batch(j->pool, j->wbits, j->n, j->blob, j->in_off, j->in_len, j->out, j->out_off, j->cap,
+                                  j->status, j->phase, j->msg, j->olen, j->cons, j->check);
   else
-    j->rc = zs_deflate_batch(j->ctx, j->level, j->wbits, j->n, j->blob, j->in_off, j->in_len, j->out, j->out_off,
-                             j->cap, j->status, j->olen);
+    j->rc = zs_pool_deflate_batch(j->pool, j->level, j->wbits, j->n, j->blob, j->in_off, j->in_len, j->out,
+                                  j->out_off, j->cap, j->status, j->olen, j->check);
   if (j->rc != ZS_OK) snprintf(j->err, sizeof j->err, "%s", zs_last_error());  /* the error is per thread */
-  pthread_mutex_unlock(&g_dev_mtx[j->dev]);
 }
 
 static napi_value build_result(napi_env env, job *j) {
@@ -188,7 +258,7 @@ static napi_value build_result(napi_env env, job *j) {
   napi_value msgs = NULL;
   if (j->inflate && napi_create_array_with_length(env, j->n, &msgs) != napi_ok) return NULL;
   for (uint32_t i = 0; i < j->n; i++) {
-    napi_value u = make_u8(env, j->out + j->out_off[i], j->status[i] == ZS_STREAM_END ? j->olen[i] : 0);
+    napi_value u = make_u8(env, j->out ? j->out + j->out_off[i] : NULL, j->status[i] == ZS_STREAM_END ? j->olen[i] : 0);
     if (!u || napi_set_element(env, outs, i, u) != napi_ok) return NULL;
     if (j->inflate) {
       napi_value s;
@@ -199,6 +269,7 @@ static napi_value build_result(napi_env env, job *j) {
     }
   }
   napi_set_named_property(env, obj, "status", make_i32(env, j->status, j->n));
+  napi_set_named_property(env, obj, "check", make_u32(env, j->check, j->n));
   if (j->inflate) {
     napi_set_named_property(env, obj, "phase", make_i32(env, j->phase, j->n));
     napi_set_named_property(env, obj, "consumed", make_i32(env, (const int32_t *)j->cons, j->n));
@@ -241,25 +312,26 @@ static napi_value queue_job(napi_env env, job *j, const char *name) {
   return promise;
 }
 
-/* compressBatch(inputs: Uint8Array[], wbits, level, device) ->
- *   Promise<{status: Int32Array, outputs: Uint8Array[]}> */
+/* compressBatch(inputs: Uint8Array[], wbits, level, devices: number | number[]) ->
+ *   Promise<{status: Int32Array, check: Uint32Array, outputs: Uint8Array[]}> */
 static napi_value CompressBatch(napi_env env, napi_callback_info info) {
   size_t argc = 4;
   napi_value argv[4];
   NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  if (argc < 3) return throw_code(env, ZS_STREAM_ERROR, "compressBatch(inputs, wbits, level[, device])");
+  if (argc < 3) return throw_code(env, ZS_STREAM_ERROR, "compressBatch(inputs, wbits, level[, devices])");
   view *v = NULL;
   uint32_t n = 0;
   if (get_views(env, argv[0], &v, &n) != 0) return throw_code(env, ZS_STREAM_ERROR, "inputs must be Uint8Array[]");
-  const int dev = argc > 3 ? arg_i32(env, argv[3], 0) : 0;
-  zs_ctx *ctx = ctx_for(env, dev);
-  job *j = ctx ? job_new(n) : NULL;
+  napi_value undef;
+  napi_get_undefined(env, &undef);
+  const uint64_t mask = device_mask(env, argc > 3 ? argv[3] : undef);
+  zs_pool *pool = mask ? pool_for(env, mask) : NULL;
+  job *j = pool ? job_new(n) : NULL;
   if (!j) {
     free(v);
-    return ctx ? throw_code(env, ZS_MEM_ERROR, "out of host memory") : NULL;
+    return pool ? throw_code(env, ZS_MEM_ERROR, "out of host memory") : NULL;
   }
-  j->ctx = ctx;
-  j->dev = dev;
+  j->pool = pool;
   j->wbits = arg_i32(env, argv[1], -15);
   j->level = arg_i32(env, argv[2], -1);
   uint64_t tin = 0, tout = 0;
@@ -284,49 +356,54 @@ static napi_value CompressBatch(napi_env env, napi_callback_info info) {
   return queue_job(env, j, "zs.compressBatch");
 }
 
-/* decompressBatch(inputs: Uint8Array[], wbits, outCapacity: number | number[], device) ->
- *   Promise<{status, phase: Int32Array, message: string[], outputs: Uint8Array[], consumed: Int32Array}> */
+/* decompressBatch(inputs: Uint8Array[], wbits, outCapacity: number | number[] | undefined, devices) ->
+ *   Promise<{status, phase: Int32Array, message: string[], outputs: Uint8Array[], consumed: Int32Array,
+ *            check: Uint32Array}>
+ * outCapacity undefined: unbounded output, as DecompressionStream (zs_pool_inflate_batch_auto). */
 static napi_value DecompressBatch(napi_env env, napi_callback_info info) {
   size_t argc = 4;
   napi_value argv[4];
   NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  if (argc < 3) return throw_code(env, ZS_STREAM_ERROR, "decompressBatch(inputs, wbits, outCapacity[, device])");
+  if (argc < 2) return throw_code(env, ZS_STREAM_ERROR, "decompressBatch(inputs, wbits[, outCapacity[, devices]])");
   view *v = NULL;
   uint32_t n = 0;
   if (get_views(env, argv[0], &v, &n) != 0) return throw_code(env, ZS_STREAM_ERROR, "inputs must be Uint8Array[]");
-  const int dev = argc > 3 ? arg_i32(env, argv[3], 0) : 0;
-  zs_ctx *ctx = ctx_for(env, dev);
-  job *j = ctx ? job_new(n) : NULL;
+  napi_value undef;
+  napi_get_undefined(env, &undef);
+  const uint64_t mask = device_mask(env, argc > 3 ? argv[3] : undef);
+  zs_pool *pool = mask ? pool_for(env, mask) : NULL;
+  job *j = pool ? job_new(n) : NULL;
   if (!j) {
     free(v);
-    return ctx ? throw_code(env, ZS_MEM_ERROR, "out of host memory") : NULL;
+    return pool ? throw_code(env, ZS_MEM_ERROR, "out of host memory") : NULL;
   }
   j->inflate = 1;
-  j->ctx = ctx;
-  j->dev = dev;
+  j->pool = pool;
   j->wbits = arg_i32(env, argv[1], -15);
+  napi_valuetype ct = napi_undefined;
+  if (argc > 2) napi_typeof(env, argv[2], &ct);
+  j->unbounded = ct == napi_undefined || ct == napi_null;
   bool caps_arr = false;
-  napi_is_array(env, argv[2], &caps_arr);
-  const int32_t cap_all = caps_arr ? 0 : arg_i32(env, argv[2], 1 << 16);
+  if (!j->unbounded) napi_is_array(env, argv[2], &caps_arr);
+  const uint32_t cap_all = caps_arr || j->unbounded ? 0 : arg_cap(env, argv[2], 1 << 16);
   uint64_t tin = 0, tout = 0;
   for (uint32_t i = 0; i < n; i++) {
-    int32_t c = cap_all;
+    uint32_t c = cap_all;
     if (caps_arr) {
       napi_value e;
       napi_get_element(env, argv[2], i, &e);
-      c = arg_i32(env, e, 1 << 16);
+      c = arg_cap(env, e, 1 << 16);
     }
-    if (c < 0) c = 0;
     j->in_off[i] = tin;
     j->in_len[i] = (uint32_t)v[i].n;
     tin += v[i].n;
     j->out_off[i] = tout;
-    j->cap[i] = ((uint32_t)c + 3u) & ~3u;
+    j->cap[i] = (uint32_t)(((uint64_t)c + 3u) & 0xfffffffcull);
     tout += j->cap[i];
   }
   j->blob = (uint8_t *)malloc(tin ? tin : 1);
-  j->out = (uint8_t *)malloc(tout ? tout : 1);
-  if (!j->blob || !j->out) {
+  j->out = j->unbounded ? NULL : (uint8_t *)malloc(tout ? tout : 1);  /* unbounded: the library allocates it */
+  if (!j->blob || (!j->unbounded && !j->out)) {
     free(v);
     job_free(j);
     return throw_code(env, ZS_MEM_ERROR, "out of host memory");
@@ -368,7 +445,6 @@ static napi_value SelfTest(napi_env env, napi_callback_info info) {
 }
 
 static napi_value Init(napi_env env, napi_value exports) {
-  pthread_once(&g_once, init_mutexes);
   napi_property_descriptor d[] = {
       {"compressBatch", NULL, CompressBatch, NULL, NULL, NULL, napi_default, NULL},
       {"decompressBatch", NULL, DecompressBatch, NULL, NULL, NULL, napi_default, NULL},

@@ -55,6 +55,13 @@ class ZsError(Exception):
         self.status, self.phase, self.msg = status, phase, msg
 
 
+def compress_level(level) -> int:
+    """streams.ts:221: a level that is not a number means Z_DEFAULT_COMPRESSION (-1, deflate.ts:268-270)."""
+    if isinstance(level, bool) or not isinstance(level, int):
+        return -1
+    return level
+
+
 def stream_error_text(status: int, phase: int) -> str:
     if phase == PHASE_INIT:
         return "init failed: %d" % status
@@ -88,6 +95,21 @@ def lib():
                                           _U32P, _P, _P, _P]
     L.zs_deflate_batch.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p, _U64P, _U32P,
                                    _P, _U64P, _U32P, _I32P, _U32P]
+    L.zs_deflate_batch_ex.argtypes = L.zs_deflate_batch.argtypes + [_U32P]
+    L.zs_deflate_batch_device_ex.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, _P, _U64P, _U32P, _P,
+                                             _U64P, _U32P, _P, _P, _P, _P]
+    _inf_host = [ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p, _U64P, _U32P]
+    _inf_res = [_I32P, _I32P, _I32P, _U32P, _U32P, _U32P]
+    L.zs_inflate_batch_ex.argtypes = [_P] + _inf_host + [_P, _U64P, _U32P] + _inf_res
+    L.zs_inflate_batch_auto.argtypes = [_P] + _inf_host + [ctypes.POINTER(_P), _U64P] + _inf_res
+    L.zs_free.argtypes = [_P]
+    L.zs_pool_create.argtypes = [ctypes.c_uint64, ctypes.POINTER(_P)]
+    L.zs_pool_destroy.argtypes = [_P]
+    L.zs_pool_size.argtypes = [_P]
+    L.zs_pool_device.argtypes = [_P, ctypes.c_int]
+    L.zs_pool_deflate_batch.argtypes = L.zs_deflate_batch_ex.argtypes
+    L.zs_pool_inflate_batch.argtypes = L.zs_inflate_batch_ex.argtypes
+    L.zs_pool_inflate_batch_auto.argtypes = L.zs_inflate_batch_auto.argtypes
     if hasattr(L, "zs_inflate_batch"):
         L.zs_inflate_batch.argtypes = [_P, ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p, _U64P, _U32P, _P, _U64P,
                                        _U32P, _I32P, _I32P, _I32P, _U32P, _U32P]
@@ -113,6 +135,23 @@ def lib():
     L.zs_debug_fetch.argtypes = [_P, ctypes.c_int, ctypes.c_uint32, _P, ctypes.c_uint64]
     _lib = L
     return L
+
+
+def build_id() -> str:
+    """Identity of the engine build: sha256 (16 hex) over the sources libzsgpu.so
+    is compiled from (csrc/*, include/zs_gpu.h).  Committed rocprofv3 summaries
+    carry it ("_build_id"); bench.py uses a summary's traffic / counters only
+    for the build that produced them."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(os.path.dirname(_HERE), "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".cpp", ".h")) or f == "Makefile")
+    for f in files + ["../../include/zs_gpu.h"]:
+        h.update(f.encode() + b"\0")
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def _arr(ctype, values):
@@ -199,89 +238,43 @@ class Engine:
     def compress_batch_raw(self, inputs: Sequence[bytes], fmt: str = "deflate-raw", level: int = -1
                            ) -> List[Tuple[int, bytes]]:
         """Returns [(status, bytes)] -- status Z_STREAM_END on success."""
-        n = len(inputs)
-        if n == 0:
-            return []
-        wbits = compress_wbits(fmt)
-        blob = b"".join(inputs)
-        offs, lens, o = [], [], 0
-        for b in inputs:
-            offs.append(o)
-            lens.append(len(b))
-            o += len(b)
-        caps = [(int(self._L.zs_deflate_bound(len(b), wbits)) + 3) & ~3 for b in inputs]
-        ooffs, oo = [], 0
-        for c in caps:
-            ooffs.append(oo)
-            oo += c
-        out = ctypes.create_string_buffer(max(1, oo))
-        status = (ctypes.c_int32 * n)()
-        olen = (ctypes.c_uint32 * n)()
-        r = self._L.zs_deflate_batch(self._ctx, level, wbits, n, blob, _arr(ctypes.c_uint64, offs),
-                                     _arr(ctypes.c_uint32, lens), out, _arr(ctypes.c_uint64, ooffs),
-                                     _arr(ctypes.c_uint32, caps), status, olen)
-        self._check(r, "zs_deflate_batch")
-        raw = out.raw
-        return [(status[i], raw[ooffs[i]: ooffs[i] + olen[i]]) for i in range(n)]
+        return [(st, b) for st, b, _ in self.compress_batch_detailed(inputs, fmt, level)]
+
+    def compress_batch_detailed(self, inputs: Sequence[bytes], fmt: str = "deflate-raw", level: int = -1
+                                ) -> List[Tuple[int, bytes, int]]:
+        """Returns [(status, bytes, check)]: check = the reference's strm.adler after the
+        stream (adler32 / crc32 of the input for deflate / gzip, 1 for deflate-raw)."""
+        return _deflate_host(self._L, self._L.zs_deflate_batch_ex, self._ctx, inputs, fmt, level, self._check)
 
     def compress_batch(self, inputs: Sequence[bytes], fmt: str = "deflate-raw", level: int = -1) -> List[bytes]:
-        res = []
-        for st, b in self.compress_batch_raw(inputs, fmt, level):
-            if st != Z_STREAM_END:
-                raise ZsError(stream_error_text(st, PHASE_FINISH), st, PHASE_FINISH)
-            res.append(b)
-        return res
+        return _ok_or_raise_c(self.compress_batch_raw(inputs, fmt, level))
 
     def decompress_batch_raw(self, inputs: Sequence[bytes], fmt: str = "deflate-raw",
                              out_caps: Optional[Sequence[int]] = None):
-        """Returns [(status, phase, msg, bytes, consumed)]."""
+        """Returns [(status, phase, msg, bytes, consumed)].  out_caps None: unbounded
+        output, as DecompressionStream (zs_inflate_batch_auto); else per-stream caps."""
+        return [r[:5] for r in self.decompress_batch_detailed(inputs, fmt, out_caps)]
+
+    def decompress_batch_detailed(self, inputs: Sequence[bytes], fmt: str = "deflate-raw",
+                                  out_caps: Optional[Sequence[int]] = None):
+        """Returns [(status, phase, msg, bytes, consumed, check)]."""
         L = self._L
-        if not hasattr(L, "zs_inflate_batch"):
-            raise ZsUnavailable("this libzsgpu.so has no inflate engine")
-        n = len(inputs)
-        if n == 0:
-            return []
-        wbits = decompress_wbits(fmt)
-        blob = b"".join(inputs)
-        offs, lens, o = [], [], 0
-        for b in inputs:
-            offs.append(o)
-            lens.append(len(b))
-            o += len(b)
         if out_caps is None:
-            out_caps = [max(1 << 16, 16 * len(b)) for b in inputs]
-        caps = [(int(c) + 3) & ~3 for c in out_caps]
-        ooffs, oo = [], 0
-        for c in caps:
-            ooffs.append(oo)
-            oo += c
-        out = ctypes.create_string_buffer(max(1, oo))
-        status, phase, msg = (ctypes.c_int32 * n)(), (ctypes.c_int32 * n)(), (ctypes.c_int32 * n)()
-        olen, cons = (ctypes.c_uint32 * n)(), (ctypes.c_uint32 * n)()
-        r = L.zs_inflate_batch(self._ctx, wbits, n, blob, _arr(ctypes.c_uint64, offs), _arr(ctypes.c_uint32, lens),
-                               out, _arr(ctypes.c_uint64, ooffs), _arr(ctypes.c_uint32, caps), status, phase, msg,
-                               olen, cons)
-        self._check(r, "zs_inflate_batch")
-        raw = out.raw
-        return [(status[i], phase[i], L.zs_inflate_message(msg[i]).decode(), raw[ooffs[i]: ooffs[i] + olen[i]],
-                 cons[i]) for i in range(n)]
+            return _inflate_host_auto(L, L.zs_inflate_batch_auto, self._ctx, inputs, fmt, self._check)
+        return _inflate_host(L, L.zs_inflate_batch_ex, self._ctx, inputs, fmt, out_caps, self._check)
 
     def decompress_batch(self, inputs: Sequence[bytes], fmt: str = "deflate-raw",
                          out_caps: Optional[Sequence[int]] = None) -> List[bytes]:
-        res = []
-        for st, ph, msg, b, _ in self.decompress_batch_raw(inputs, fmt, out_caps):
-            if st != Z_STREAM_END:
-                raise ZsError(stream_error_text(st, ph), st, ph, msg)
-            res.append(b)
-        return res
+        return _ok_or_raise_d(self.decompress_batch_raw(inputs, fmt, out_caps))
 
     # ---------------------------------------------------- device-resident
     def compress_device(self, level: int, fmt: str, n: int, d_in: int, in_off, in_len, d_out: int, out_off, out_cap,
-                        d_status: int, d_out_len: int, hip_stream: int = 0):
+                        d_status: int, d_out_len: int, hip_stream: int = 0, d_check: int = 0):
         """Device pointers (ints) + host layout arrays (ctypes arrays)."""
-        r = self._L.zs_deflate_batch_device(self._ctx, level, compress_wbits(fmt), n, _P(d_in), in_off, in_len,
-                                            _P(d_out), out_off, out_cap, _P(d_status), _P(d_out_len),
-                                            _P(hip_stream) if hip_stream else None)
+        r = self._L.zs_deflate_batch_device_ex(self._ctx, compress_level(level), compress_wbits(fmt), n, _P(d_in),
+                                               in_off, in_len, _P(d_out), out_off, out_cap, _P(d_status),
+                                               _P(d_out_len), _P(d_check) if d_check else None,
+                                               _P(hip_stream) if hip_stream else None)
         self._check(r, "zs_deflate_batch_device")
 
     def decompress_device(self, fmt: str, n: int, d_in: int, in_off, in_len, d_out: int, out_off, out_cap,
@@ -332,6 +325,152 @@ class Engine:
         return self.checksum("adler32", bufs, seeds)
 
 
+def _layout(inputs):
+    offs, lens, o = [], [], 0
+    for b in inputs:
+        offs.append(o)
+        lens.append(len(b))
+        o += len(b)
+    return b"".join(inputs), offs, lens
+
+
+def _deflate_host(L, fn, handle, inputs, fmt, level, check):
+    n = len(inputs)
+    if n == 0:
+        return []
+    wbits = compress_wbits(fmt)
+    blob, offs, lens = _layout(inputs)
+    caps = [(int(L.zs_deflate_bound(len(b), wbits)) + 3) & ~3 for b in inputs]
+    ooffs, oo = [], 0
+    for c in caps:
+        ooffs.append(oo)
+        oo += c
+    out = ctypes.create_string_buffer(max(1, oo))
+    status, olen, chk = (ctypes.c_int32 * n)(), (ctypes.c_uint32 * n)(), (ctypes.c_uint32 * n)()
+    r = fn(handle, compress_level(level), wbits, n, blob, _arr(ctypes.c_uint64, offs), _arr(ctypes.c_uint32, lens),
+           out, _arr(ctypes.c_uint64, ooffs), _arr(ctypes.c_uint32, caps), status, olen, chk)
+    check(r, "deflate batch")
+    raw = out.raw
+    return [(status[i], raw[ooffs[i]: ooffs[i] + olen[i]], chk[i]) for i in range(n)]
+
+
+def _inflate_results(L, n, raw, ooffs, status, phase, msg, olen, cons, chk):
+    return [(status[i], phase[i], L.zs_inflate_message(msg[i]).decode(), raw[ooffs[i]: ooffs[i] + olen[i]], cons[i],
+             chk[i]) for i in range(n)]
+
+
+def _inflate_host(L, fn, handle, inputs, fmt, out_caps, check):
+    n = len(inputs)
+    if n == 0:
+        return []
+    blob, offs, lens = _layout(inputs)
+    caps = [min(0xfffffffc, (int(c) + 3) & ~3) for c in out_caps]
+    ooffs, oo = [], 0
+    for c in caps:
+        ooffs.append(oo)
+        oo += c
+    out = ctypes.create_string_buffer(max(1, oo))
+    res = [(ctypes.c_int32 * n)() for _ in range(3)] + [(ctypes.c_uint32 * n)() for _ in range(3)]
+    r = fn(handle, decompress_wbits(fmt), n, blob, _arr(ctypes.c_uint64, offs), _arr(ctypes.c_uint32, lens), out,
+           _arr(ctypes.c_uint64, ooffs), _arr(ctypes.c_uint32, caps), *res)
+    check(r, "inflate batch")
+    return _inflate_results(L, n, out.raw, ooffs, *res)
+
+
+def _inflate_host_auto(L, fn, handle, inputs, fmt, check):
+    n = len(inputs)
+    if n == 0:
+        return []
+    blob, offs, lens = _layout(inputs)
+    res = [(ctypes.c_int32 * n)() for _ in range(3)] + [(ctypes.c_uint32 * n)() for _ in range(3)]
+    ooffs = (ctypes.c_uint64 * n)()
+    outp = _P()
+    r = fn(handle, decompress_wbits(fmt), n, blob, _arr(ctypes.c_uint64, offs), _arr(ctypes.c_uint32, lens),
+           ctypes.byref(outp), ooffs, *res)
+    check(r, "inflate batch")
+    try:
+        olen = res[4]
+        total = max((ooffs[i] + olen[i] for i in range(n)), default=0)
+        raw = ctypes.string_at(outp, total) if total else b""
+    finally:
+        L.zs_free(outp)
+    return _inflate_results(L, n, raw, list(ooffs), *res)
+
+
+def _ok_or_raise_c(results):
+    out = []
+    for st, b in results:
+        if st != Z_STREAM_END:
+            raise ZsError(stream_error_text(st, PHASE_FINISH), st, PHASE_FINISH)
+        out.append(b)
+    return out
+
+
+def _ok_or_raise_d(results):
+    out = []
+    for st, ph, msg, b, _ in results:
+        if st != Z_STREAM_END:
+            raise ZsError(stream_error_text(st, ph), st, ph, msg)
+        out.append(b)
+    return out
+
+
+class Pool:
+    """A multi-GPU batch engine (zs_pool, SURVEY.md 8(b) device mask / 8(e)): one
+    context per device; each batch is split into contiguous stream ranges, one
+    per device, run in parallel -- results identical to one device's."""
+
+    def __init__(self, devices: Optional[Sequence[int]] = None):
+        L = lib()
+        mask = 0
+        for d in devices or []:
+            mask |= 1 << int(d)
+        p = _P()
+        r = L.zs_pool_create(mask, ctypes.byref(p))
+        if r != 0:
+            err = L.zs_last_error().decode()
+            if r == Z_STREAM_ERROR and "device mask" in err:
+                raise ValueError(err)
+            raise ZsUnavailable("zs_pool_create failed: %s" % err)
+        self._L, self._pool = L, p
+        self.devices = [L.zs_pool_device(p, k) for k in range(L.zs_pool_size(p))]
+
+    def close(self):
+        if getattr(self, "_pool", None):
+            self._L.zs_pool_destroy(self._pool)
+            self._pool = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, r: int, what: str):
+        Engine._check(self, r, what)
+
+    def compress_batch_detailed(self, inputs, fmt="deflate-raw", level=-1):
+        return _deflate_host(self._L, self._L.zs_pool_deflate_batch, self._pool, inputs, fmt, level, self._check)
+
+    def compress_batch_raw(self, inputs, fmt="deflate-raw", level=-1):
+        return [(st, b) for st, b, _ in self.compress_batch_detailed(inputs, fmt, level)]
+
+    def compress_batch(self, inputs, fmt="deflate-raw", level=-1):
+        return _ok_or_raise_c(self.compress_batch_raw(inputs, fmt, level))
+
+    def decompress_batch_detailed(self, inputs, fmt="deflate-raw", out_caps=None):
+        L = self._L
+        if out_caps is None:
+            return _inflate_host_auto(L, L.zs_pool_inflate_batch_auto, self._pool, inputs, fmt, self._check)
+        return _inflate_host(L, L.zs_pool_inflate_batch, self._pool, inputs, fmt, out_caps, self._check)
+
+    def decompress_batch_raw(self, inputs, fmt="deflate-raw", out_caps=None):
+        return [r[:5] for r in self.decompress_batch_detailed(inputs, fmt, out_caps)]
+
+    def decompress_batch(self, inputs, fmt="deflate-raw", out_caps=None):
+        return _ok_or_raise_d(self.decompress_batch_raw(inputs, fmt, out_caps))
+
+
 _default: Optional[Engine] = None
 
 
@@ -374,7 +513,7 @@ class CompressionStream(_OneShotStream):
 
     def __init__(self, fmt: str = "deflate", level: Optional[int] = None):
         super().__init__()
-        self.format, self.level = fmt, (-1 if level is None else level)
+        self.format, self.level = fmt, compress_level(level)
 
     def close(self) -> bytes:
         self._out = default_engine().compress_batch([b"".join(self._chunks)], self.format, self.level)[0]
