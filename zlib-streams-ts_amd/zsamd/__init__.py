@@ -389,7 +389,7 @@ def _inflate_host_auto(L, fn, handle, inputs, fmt, check):
            ctypes.byref(outp), ooffs, *res)
     check(r, "inflate batch")
     try:
-        olen = res[4]
+        olen = res[3]
         total = max((ooffs[i] + olen[i] for i in range(n)), default=0)
         raw = ctypes.string_at(outp, total) if total else b""
     finally:
