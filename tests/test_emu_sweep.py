@@ -38,6 +38,11 @@ def _streams():
              ("text", 3), ("text", 4), ("text", 13), ("text", 259), ("mixed", 1000), ("text", 32769),
              ("text", 65535), ("text", 65537), ("zeros", 65537)]
     out = [corpus.make({"kind": k, "n": n, "seed": 7000 + i}) for i, (k, n) in enumerate(specs)]
+    # 7-bit streams take the 8-byte signature [X, b3..b9]: random 7-bit bytes collide in the 15-bit hash with
+    # different first three bytes everywhere; a small alphabet gives long matches and deep chains
+    out.append(bytes(x & 0x7F for x in corpus.rand(91, 65536)))
+    out.append(bytes(0x41 + (x & 3) for x in corpus.rand(92, 65536)))
+    out.append(bytes(x & 0x7F for x in corpus.rand(93, 20000)) + corpus.text(94, 45536))
     b = bytearray(corpus.rand(77, 65536))  # a head candidate at exactly MAX_DIST
     b[40000:40020] = b[40000 - 32506:40000 - 32506 + 20]
     out.append(bytes(b))
@@ -54,3 +59,4 @@ def test_sweep_model_matches_longest_match(emu, tmp_path, level):
     r = subprocess.run([emu, str(f), str(chain), str(nice)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout, r.stdout
+    assert " 0 in 7-bit" not in r.stdout  # both signature forms were exercised

@@ -78,6 +78,11 @@ def test_sweep_match_table_equals_chain_walk(engine, level):
     b = bytearray(corpus.rand(77, 65536))  # a candidate at exactly MAX_DIST
     b[40000:40020] = b[40000 - 32506:40000 - 32506 + 20]
     inputs.append(bytes(b))
+    # 7-bit streams (the sweep's 8-byte signature form): hash collisions with different first bytes,
+    # deep chains over a small alphabet, text after 7-bit noise
+    inputs.append(bytes(x & 0x7F for x in corpus.rand(91 + level, 65536)))
+    inputs.append(bytes(0x41 + (x & 3) for x in corpus.rand(92 + level, 65536)))
+    inputs.append(bytes(x & 0x7F for x in corpus.rand(93, 20000)) + corpus.text(94, 45537))
     tables, outs = [], []
     try:
         for sweep in (1, 0):

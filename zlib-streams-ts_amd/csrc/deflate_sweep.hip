@@ -43,11 +43,15 @@
 #include <hip/hip_runtime.h>
 #include "zs_common.h"
 #include "zs_kernels.h"
+#include <type_traits>
 
 #define ZS_SWEEP_MAX 65537u  // position + 1 <= 65535 for every inserted position: u16 members and offsets
 #define ZS_SW_WIN_WORDS ((ZS_SWEEP_MAX + 20u + 3u) / 4u + 2u)
-#define ZS_SW_SIG 11u  // signature bytes compared per chain step (see sw_lcp)
 #define ZS_SW_RING 128u  // records per wave (two blocks of 64 members), stored twice (mirror)
+#ifndef ZS_SW_EXP
+#define ZS_SW_EXP 0  // experiments (timing A/B only; 0 in the product)
+#endif
+#define ZS_SW_MW 320u    // per-wave LDS window of member positions (chain + 64 <= ZS_SW_MW: levels 4..7)
 
 typedef __attribute__((address_space(3))) uint32_t zs_sw_lds_u32;
 static __device__ __forceinline__ uint32_t sw_lds_addr(const void* p) {
@@ -243,9 +247,10 @@ static __device__ __forceinline__ uint32_t sw_word(const uint32_t* win, uint32_t
   return __builtin_amdgcn_alignbyte(win[i + 1], win[i], off & 3u);
 }
 
-// exact length of a candidate whose first ZS_SW_SIG bytes match, clamped to maxc
-static __device__ __forceinline__ uint32_t sw_extend(const uint32_t* win, uint32_t p, uint32_t q, uint32_t maxc) {
-  uint32_t k = ZS_SW_SIG;
+// exact length of a candidate whose first `from` bytes match, clamped to maxc
+static __device__ __forceinline__ uint32_t sw_extend(const uint32_t* win, uint32_t p, uint32_t q, uint32_t maxc,
+                                                     uint32_t from) {
+  uint32_t k = from;
   while (k < maxc) {
     const uint32_t y = sw_word(win, q + k) ^ sw_word(win, p + k);
     if (y) { k += (uint32_t)(__builtin_ctz(y) >> 3); break; }
@@ -254,212 +259,339 @@ static __device__ __forceinline__ uint32_t sw_extend(const uint32_t* win, uint32
   return k < maxc ? k : maxc;
 }
 
-// Signatures are 11 bytes: a record's third word keeps bytes 8..10 (byte 11
-// zeroed, sw_rec2) and the lane's own third word carries a sentinel bit 24
-// (sw_own2), so the xor of the third words always has bit 24 set.  The
-// matched-byte count then saturates at 11 by itself -- no per-step cap -- and
-// lanes whose lookahead is at most 12 bytes (maxc <= 12, the last positions
-// of a stream) take an exact re-walk after the sweep instead.
-static __device__ __forceinline__ uint32_t sw_rec2(uint32_t w2) { return w2 & 0x00ffffffu; }
-static __device__ __forceinline__ uint32_t sw_own2(uint32_t w2) { return (w2 & 0x00ffffffu) | 0x01000000u; }
-// matched bytes (0..11) of a candidate's record words (a) against the lane's own (b)
-static __device__ __forceinline__ uint32_t sw_lcp(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t b0, uint32_t b1,
-                                                  uint32_t b2) {
-  uint32_t f0, f1, f2;
-  asm("v_ffbl_b32 %0, %1" : "=v"(f0) : "v"(a0 ^ b0));
-  asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e64 %0, %0, 32 clamp" : "=&v"(f1) : "v"(a1 ^ b1));
-  asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e32 %0, 64, %0" : "=&v"(f2) : "v"(a2 ^ b2));
-  // ffbl(0) = ~0 and the clamped add keep "no difference" at ~0; f2 <= 88 (the sentinel)
-  return min(min(f0, f1), f2) >> 3;
+// a wave-uniform 64-bit value kept in SGPRs (lane masks updated in loops with divergent bodies)
+static __device__ __forceinline__ uint64_t sw_uniform(uint64_t x) {
+  // (readfirstlane returns int: widen through uint32_t, not by sign extension)
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
-struct SwRec {
-  uint32_t w0, w1, w2, key;  // bytes [q, q + 12) and hash << 16 | q
+static __device__ __forceinline__ uint32_t max3(uint32_t a, uint32_t b, uint32_t c) {
+  return max(max(a, b), c);  // one v_max3_u32
+}
+
+// Candidate signatures.  A chain step compares the lane's own signature with a
+// candidate's and yields the index of the first differing bit (the "matched
+// bits"); its byte is the signature's matched-byte count sigma.
+//
+// SwSig<false>, any stream: the 11 bytes [q, q + 11) in three words.  A
+// record's third word keeps bytes 8..10 (byte 11 zeroed) and the lane's own
+// third word carries a sentinel bit 24, so the xor of the third words always
+// has bit 24 set and the count saturates at 88 (all 11 bytes) by itself.
+// sigma is the match length (>= 3 within a bucket unless the hash collides).
+//
+// SwSig<true>, streams whose bytes are all < 0x80 (text): two words, 8 bytes
+// [X, b3 .. b9].  Bytes 0..2 hash to the bucket; of their 24 bits
+// the 15-bit hash loses 9 -- b0[5:7], and b1[0:2], b1[5:7] (which the hash
+// only has xor-ed with b2[5:7] and b0[0:2]) -- and with bit 7 of every byte
+// clear, the 7 bits X = b0[5:6] | b1[0:2] << 2 | b1[5:6] << 5 recover them: in
+// one bucket, equal X <=> equal first three bytes.  So sigma = 0 means "not a
+// match" (a hash collision) and sigma >= 1 means a match of sigma + 2 bytes;
+// the count saturates at 64 (min3 with 64).  A step is six VALU instead of
+// nine.
+static __device__ __forceinline__ uint32_t sw_x7(uint32_t w) {
+  const uint32_t b0 = w & 0xffu, b1 = (w >> 8) & 0xffu;
+  return ((b0 >> 5) & 3u) | ((b1 & 7u) << 2) | (((b1 >> 5) & 3u) << 5);
+}
+template <bool A7>
+struct SwSig;
+template <>
+struct SwSig<false> {
+  static constexpr uint32_t LONG = 88u;  // all 11 bytes: the exact length needs the window
+  static constexpr uint32_t THR0 = 23u;  // sigma 2 (B << 3 | 7): no match yet
+  static constexpr uint32_t EXT = 11u;   // a long candidate's known bytes
+  uint32_t a, b, c;
+  __device__ __forceinline__ void own(const uint32_t* win, uint32_t p) {
+    a = sw_word(win, p);
+    b = sw_word(win, p + 4);
+    c = (sw_word(win, p + 8) & 0x00ffffffu) | 0x01000000u;
+  }
+  static __device__ __forceinline__ uint4 rec(const uint32_t* win, uint32_t q, uint32_t w0) {
+    return make_uint4(w0, sw_word(win, q + 4), sw_word(win, q + 8) & 0x00ffffffu, 0u);
+  }
+  __device__ __forceinline__ uint32_t mbits(uint32_t x, uint32_t y, uint32_t z) const {
+    uint32_t f0, f1, f2;
+    asm("v_ffbl_b32 %0, %1" : "=v"(f0) : "v"(x ^ a));
+    asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e64 %0, %0, 32 clamp" : "=&v"(f1) : "v"(y ^ b));
+    asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e32 %0, 64, %0" : "=&v"(f2) : "v"(z ^ c));
+    // ffbl(0) = ~0 and the clamped add keep "no difference" at ~0; f2 <= 88 (the sentinel)
+    return min(min(f0, f1), f2);
+  }
+  static __device__ __forceinline__ uint32_t len(uint32_t sigma) { return sigma; }
+};
+template <>
+struct SwSig<true> {
+  static constexpr uint32_t LONG = 64u;  // all 8 signature bytes: a match of >= 10 bytes
+  static constexpr uint32_t THR0 = 7u;   // sigma 0
+  static constexpr uint32_t EXT = 10u;
+  uint32_t a, b;
+  __device__ __forceinline__ void own(const uint32_t* win, uint32_t p) {
+    a = sw_x7(sw_word(win, p)) | (sw_word(win, p + 3) << 8);
+    b = sw_word(win, p + 6);
+  }
+  static __device__ __forceinline__ uint4 rec(const uint32_t* win, uint32_t q, uint32_t w0) {
+    return make_uint4(sw_x7(w0) | (sw_word(win, q + 3) << 8), sw_word(win, q + 6), 0u, 0u);
+  }
+  __device__ __forceinline__ uint32_t mbits(uint32_t x, uint32_t y, uint32_t) const {
+    uint32_t f0, f1;
+    asm("v_ffbl_b32 %0, %1" : "=v"(f0) : "v"(x ^ a));
+    asm("v_ffbl_b32 %0, %1\n\tv_add_u32_e64 %0, %0, 32 clamp" : "=&v"(f1) : "v"(y ^ b));
+    return min(min(f0, f1), 64u);  // one v_min3_u32
+  }
+  static __device__ __forceinline__ uint32_t len(uint32_t sigma) { return sigma ? sigma + 2u : 2u; }
 };
 
-__global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                   const uint32_t* __restrict__ in_len,
-                                                   const uint64_t* __restrict__ pos_base,
-                                                   const uint16_t* __restrict__ members, uint2* __restrict__ mres,
-                                                   int chain, int nice_cfg) {
-  __shared__ __attribute__((aligned(16))) SwRec ring[16][2 * ZS_SW_RING];
-  __shared__ __attribute__((aligned(16))) uint32_t win[ZS_SW_WIN_WORDS];
-  __shared__ uint32_t next;
-  const int s = blockIdx.x;
-  const uint32_t n = in_len[s];
-  if (n > ZS_SWEEP_MAX || n < 3) return;
-  const uint32_t m = n - 2;
-  const uint8_t* src = in + in_off[s];
-  const uint16_t* mem = members + pos_base[s];
-  uint2* out = mres + pos_base[s];
-  // the whole stream in LDS, zero padded (reads run up to 16 bytes past n)
-  if ((((uintptr_t)src) & 15u) == 0) {
-    for (uint32_t i = threadIdx.x; 4 * i < ZS_SW_WIN_WORDS; i += 1024) {
-      const uint32_t b = 16 * i;
-      uint4 v;
-      if (b + 16 <= n) v = ((const uint4*)src)[i];
-      else {
-        uint32_t t[4] = {0, 0, 0, 0};
-        for (uint32_t k = 0; k < 16; k++)
-          if (b + k < n) t[k >> 2] |= (uint32_t)src[b + k] << (8 * (k & 3));
-        v = make_uint4(t[0], t[1], t[2], t[3]);
-      }
-      if (4 * i + 3 < ZS_SW_WIN_WORDS) *(uint4*)(win + 4 * i) = v;
-      else for (uint32_t k = 0; 4 * i + k < ZS_SW_WIN_WORDS; k++) win[4 * i + k] = (&v.x)[k];
-    }
-  } else {
-    for (uint32_t i = threadIdx.x; i < ZS_SW_WIN_WORDS; i += 1024) {
-      uint32_t v = 0;
-      for (uint32_t k = 0; k < 4; k++)
-        if (4 * i + k < n) v |= (uint32_t)src[4 * i + k] << (8 * k);
-      win[i] = v;
-    }
-  }
-  if (threadIdx.x == 0) next = 0;
-  __syncthreads();
+// Per-wave ring of candidate records, as separate dense arrays so that the 64
+// lanes of a step read 64 consecutive elements (conflict-free): signature words
+// 0..1 (8 B), word 2 (the 11-byte form only) and the liveness key
+// hash << 16 | q.  Member j's record lives in slot j mod 128 and again 128
+// slots later, so that a block's 64 steps read slots base .. base + 63 without
+// wrapping.
+struct SwRing {
+  uint2 ab[2 * ZS_SW_RING];
+  uint32_t c[2 * ZS_SW_RING];
+  uint32_t key[2 * ZS_SW_RING];
+};
 
+// The lock-step sweep of one stream (the workgroup), for signature form A7.
+//
+// For chain step t every lane compares its position with the t-th
+// predecessor's signature.  A step's score is its matched bits with the low
+// three bits (the bit within the first differing byte, which must not count)
+// replaced by 7 - u, u = the step's place in its GROUP of steps (8, or 4 where
+// a block end or the chain >> 2 snapshot cuts it): one v_and_or.  The group's
+// maximum score is then its longest candidate and, among equally long ones,
+// the earliest -- the first maximum of deflate.ts:1100-1105 -- and the lane
+// keeps it when it is longer than its best so far (thr = B << 3 | 7 for a best
+// of B signature bytes).  A step costs the compare and the v_and_or; the
+// group's fold is max3s + a compare + three selects.
+//
+// A candidate whose whole signature matches is "long": its exact length needs
+// the window.  Such candidates are rare; when a group holds one for any lane,
+// those lanes extend it on the spot (the record's position is in the ring),
+// keeping the first longest and stopping at the first nice match
+// (deflate.ts:1100-1105).  Long candidates beat every short one.
+//
+// Liveness (deflate.ts:1109, 1376) is monotone in t, so a block of 64 steps in
+// which every live lane's LAST step is live is live throughout for those lanes:
+// such a block runs with the exec mask of the live lanes and no per-step test.
+// A block in which some lane's chain ends runs the masked form (the step's
+// ballot of `key > klim` ands into the live mask, a dead lane's score is 0).
+template <bool A7, bool MW>
+static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, uint16_t* mw, uint32_t* next,
+                                               uint32_t n, const uint16_t* mem, uint2* out, int chain,
+                                               int nice_cfg) {
+  using Sig = SwSig<A7>;
+  const uint32_t m = n - 2;
   const uint32_t lane = threadIdx.x & 63u;
-  SwRec* const R = ring[threadIdx.x >> 6];
   const uint32_t budget = (uint32_t)chain, budget_s = (uint32_t)chain >> 2;
   const uint32_t nchunks = (m + 63) / 64;
-  // Member j's record lives in ring slot j mod 128 and again 128 slots later,
-  // so that a block's 64 steps read slots base .. base + 63 without wrapping.
-  auto put_rec = [&](int j, SwRec r) {
+  auto put_rec = [&](int j, uint4 r) {
     const uint32_t i = (uint32_t)j & (ZS_SW_RING - 1);
-    R[i] = r;
-    R[i + ZS_SW_RING] = r;
-  };
-  auto load_rec = [&](int j) {  // key 0 = no member: fails every liveness test
-    SwRec r = {0, 0, 0, 0};
-    if (j >= 0 && (uint32_t)j < m) {
-      const uint32_t q = mem[j];
-      r.w0 = sw_word(win, q);
-      r.w1 = sw_word(win, q + 4);
-      r.w2 = sw_rec2(sw_word(win, q + 8));
-      r.key = (sw_hash(r.w0) << 16) | q;
+    R->ab[i] = make_uint2(r.x, r.y);
+    R->ab[i + ZS_SW_RING] = make_uint2(r.x, r.y);
+    if (!A7) {
+      R->c[i] = r.z;
+      R->c[i + ZS_SW_RING] = r.z;
     }
-    put_rec(j, r);
+    R->key[i] = r.w;
+    R->key[i + ZS_SW_RING] = r.w;
+  };
+  auto make_rec = [&](uint32_t q) -> uint4 {
+    const uint32_t w0 = sw_word(win, q);
+    uint4 r = Sig::rec(win, q, w0);
+    r.w = (sw_hash(w0) << 16) | q;
+    return r;
+  };
+  // MW: the members k0 - budget .. k0 + 63 of the current chunk are kept in a
+  // per-wave LDS window as their records are built, so the distances after
+  // the sweep read positions from LDS instead of HBM (chain + 64 <= ZS_SW_MW)
+  int mw0 = 0;  // member index of mw[0] (k0 - budget)
+  auto load_rec = [&](int j) {  // key 0 = no member: fails every liveness test
+    const bool in = j >= 0 && (uint32_t)j < m;
+    const uint32_t q = in ? mem[j] : 0u;
+    if (MW && (uint32_t)(j - mw0) < ZS_SW_MW) mw[j - mw0] = (uint16_t)q;  // (block 1 back reaches below k0 - budget when budget < 64)
+    put_rec(j, in ? make_rec(q) : make_uint4(0, 0, 0, 0));
+  };
+  auto member = [&](int j) -> uint32_t { return MW ? (uint32_t)mw[j - mw0] : (uint32_t)mem[j]; };
+  auto rmbits = [&](const Sig& S, uint32_t slot) -> uint32_t {  // a ring record's matched bits
+    const uint2 ab = R->ab[slot];
+    return S.mbits(ab.x, ab.y, A7 ? 0u : R->c[slot]);
   };
   for (;;) {
     uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(&next, 1u);
+    if (lane == 0) c = atomicAdd(next, 1u);
     c = __builtin_amdgcn_readfirstlane(c);
     if (c >= nchunks) break;
     const int k0 = (int)(64 * c);
     const int k = k0 + (int)lane;
     const bool own = (uint32_t)k < m;
     const uint32_t p = own ? mem[k] : 0u;
-    const uint32_t s0 = sw_word(win, p), s1 = sw_word(win, p + 4), s2r = sw_word(win, p + 8);
-    const uint32_t s2 = sw_own2(s2r);
-    const uint32_t h = sw_hash(s0);
+    mw0 = k0 - (int)budget;
+    if (MW) mw[k - mw0] = (uint16_t)p;
+    Sig S;
+    S.own(win, p);
+    const uint32_t h = sw_hash(sw_word(win, p));
     const uint32_t look = n - p;
     const uint32_t maxc = look < ZS_MAX_MATCH ? look : ZS_MAX_MATCH;                 // deflate.ts:1068
     const uint32_t nice = look < (uint32_t)nice_cfg ? look : (uint32_t)nice_cfg;      // deflate.ts:1078-1080
     const bool tail = maxc <= 12u;  // exact re-walk after the sweep
-    const uint32_t long_thr = tail ? 12u : ZS_SW_SIG;  // a tail lane records no long candidates
+    const uint32_t long_m = tail ? 0xffffu : Sig::LONG;  // a tail lane records no long candidates
     const uint32_t limit = p > ZS_MAX_DIST ? p - ZS_MAX_DIST : 0u;                   // deflate.ts:1060
     const uint32_t khead = (h << 16) | (limit > 1u ? limit : 1u);
     const uint32_t klim = (h << 16) | limit;
     // ring: this chunk's block and the one before it
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    put_rec(k, own ? SwRec{s0, s1, sw_rec2(s2r), (h << 16) | p} : SwRec{0, 0, 0, 0});
+    put_rec(k, own ? make_rec(p) : make_uint4(0, 0, 0, 0));
     load_rec(k - 64);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
 
-    uint32_t best = 2u << 16, best_s = 2u << 16;
-    uint32_t nl = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;  // long candidates: t << 16 | pos, in chain order
-    bool ovf = false;
-    // The live lanes as a wave-uniform lane mask (SGPRs): a chain step is a
-    // compare into a mask, scalar ands and one masked select per lane.
+    uint32_t thr = Sig::THR0, thr_s = Sig::THR0;
+    uint32_t bt = 0, bt_s = 0;                  // step of the best short candidate (0: none)
+    // best long candidate: its length (capped at nice) as lthr = len << 3 | 7, its step
+    uint32_t lthr = 7u, lbt = 0, lthr_s = 7u, lbt_s = 0;
+    const uint32_t own_ext = sw_word(win, p + Sig::EXT);  // the lane's bytes past a full signature
     uint64_t alive_m = 0;
     uint32_t head = 0;  // bit 0: head candidate valid; 0x8000: at exactly MAX_DIST
-    auto note_long = [&](uint32_t t, uint32_t key) {
-      if (nl == 4) {  // a fifth: the lane stops (cleared from alive_m by the caller) and re-walks its chain afterwards
-        ovf = true;
-      } else {
-        const uint32_t e = (t << 16) | (key & 0xffffu);
-        l0 = nl == 0 ? e : l0;
-        l1 = nl == 1 ? e : l1;
-        l2 = nl == 2 ? e : l2;
-        l3 = nl == 3 ? e : l3;
-        nl++;
-      }
-    };
-    // t = 1: the head candidate (deflate.ts:1376)
-    {
-      const SwRec r = R[(uint32_t)(k - 1) & (ZS_SW_RING - 1)];
-      bool a1 = false;
-      if (own && r.key >= khead) {
-        a1 = true;
-        head = 1u | ((p - (r.key & 0xffffu)) == ZS_MAX_DIST ? 0x8000u : 0u);
-        const uint32_t kk = sw_lcp(r.w0, r.w1, r.w2, s0, s1, s2);
-        if (kk >= long_thr) note_long(1, r.key);
-        best = max(best, (kk << 16) | (0xffffu - 1u));
-      }
-      alive_m = __builtin_amdgcn_ballot_w64(a1);
-    }
-    // One chain step for every lane: a dead lane's result simply stops
-    // changing (no per-step exit, no exec-mask bookkeeping).
-    // A step returns its score, 0 for a dead lane (below every best).  The
-    // caller takes the maximum of a group's scores (v_max3), folds it into
-    // best with one v_max, and finds the group's long candidates from it: a
-    // live long candidate scores at least long_thr << 16, a dead one 0.
-    const uint32_t long16 = long_thr << 16;
-    auto step = [&](const uint4 r, uint32_t t) -> uint32_t {
-      alive_m &= __builtin_amdgcn_ballot_w64(r.w > klim);  // the chain ends at the first dead step (deflate.ts:1109)
-      const uint32_t kk = sw_lcp(r.x, r.y, r.z, s0, s1, s2);
-      uint32_t sc, sl;
-      // one v_lshl_or (the compiler would otherwise fold the >> 3 into a shift, an and and an or)
-      asm("v_lshl_or_b32 %0, %1, 16, %2" : "=v"(sl) : "v"(kk), "s"(0xffffu - t));
-      asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(sc) : "v"(sl), "s"(alive_m));
-      return sc;
-    };
-    // Long candidates are rare (~1 % of groups): a group with one is re-run
-    // step by step to record them in chain order.
-    auto relong = [&](const SwRec* Rg, uint32_t t0, uint32_t cnt, uint64_t al_m) {
-      bool al = ((al_m >> lane) & 1u) != 0;
-      for (uint32_t u = 0; u < cnt; u++) {
-        const SwRec r = Rg[-(int)u];
-        al = al && r.key > klim;
-        if (al && sw_lcp(r.w0, r.w1, r.w2, s0, s1, s2) >= long_thr) {
-          note_long(t0 + u, r.key);
-          if (ovf) al = false;
+    // step t of block 0's numbering reads ring slot base - t
+    auto score = [&](uint32_t mb, uint32_t u) -> uint32_t { return (mb & ~7u) | (7u - u); };  // one v_and_or_b32
+    // a group's fold: the longest candidate if longer than the best so far.
+    // Long candidates (a full signature match) are rare: when a group holds one
+    // for any lane, those lanes compare the next four bytes of all the group's
+    // long candidates at once (their positions are in the ring), a candidate
+    // matching those too is extended byte-wise (rarer still).  Lengths are
+    // capped at nice: the first nice candidate ends the walk (deflate.ts:1103)
+    // and ties with every later one, so it stays first.
+    auto fold = [&](uint32_t gm, uint32_t t0, const uint32_t* sc, uint32_t cnt, uint32_t base)
+        __attribute__((always_inline)) {
+      const bool up = gm > thr;
+      thr = max(thr, gm | 7u);
+      bt = up ? t0 + 7u - (gm & 7u) : bt;
+#if ZS_SW_EXP & 32
+      if (0) {
+#else
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(gm >= long_m) != 0, 0)) {
+#endif
+        if (gm >= long_m && (lthr >> 3) < nice) {
+          uint32_t gl = 0;
+#pragma unroll
+          for (uint32_t u = 0; u < 8; u++) {
+            if (u < cnt && sc[u] >= long_m) {
+              const uint32_t q = R->key[base - t0 - u] & 0xffffu;
+              const uint32_t x = sw_word(win, q + Sig::EXT) ^ own_ext;
+              uint32_t len = x ? Sig::EXT + ((uint32_t)__builtin_ctz(x) >> 3) : sw_extend(win, p, q, maxc, Sig::EXT + 4u);
+              len = min(min(len, maxc), nice);
+              gl = max(gl, (len << 3) | (7u - u));
+            }
+          }
+          const bool lup = gl > lthr;
+          lthr = max(lthr, gl | 7u);
+          lbt = lup ? t0 + 7u - (gl & 7u) : lbt;
         }
       }
-      alive_m &= ~__builtin_amdgcn_ballot_w64(ovf);
     };
-    // Steps 2..4 (block 0, before the first full group).
-    {
-      const SwRec* const Rg = R + (((uint32_t)(k - 64) & (ZS_SW_RING - 1)) + 64u - 2u);
-      const uint64_t alive0 = alive_m;
-      uint32_t gm = 0;
-      for (uint32_t u = 0; u < 3; u++) gm = max(gm, step(*(const uint4*)(Rg - (int)u), 2u + u));
-      best = max(best, gm);
-      if (__builtin_expect(__builtin_amdgcn_ballot_w64(gm >= long16) != 0, 0)) relong(Rg, 2u, 3u, alive0);
-    }
-    // Steps [ta, tb] of block b in groups of four (ta = 1 mod 4, tb = 0 mod 4,
-    // wave-uniform).  Step t reads slot base_b + 64b + 64 - t: one address per
-    // group, immediate offsets inside, all four records loaded up front.
-    auto run = [&](uint32_t b, uint32_t ta, uint32_t tb) {
-      const uint32_t base_b = (uint32_t)(k - 64 * (int)b - 64) & (ZS_SW_RING - 1);
-      const SwRec* const Rb = R + base_b + 64u * b + 64u;
-      for (uint32_t t0 = ta; t0 <= tb; t0 += 4) {
-        const SwRec* const Rg = Rb - t0;  // step t0 + u reads Rg[-u]
-        const uint4 r0 = *(const uint4*)(Rg), r1 = *(const uint4*)(Rg - 1), r2 = *(const uint4*)(Rg - 2),
-                    r3 = *(const uint4*)(Rg - 3);
-        const uint64_t alive0 = alive_m;
-        const uint32_t c0 = step(r0, t0), c1 = step(r1, t0 + 1);
-        const uint32_t c2 = step(r2, t0 + 2), c3 = step(r3, t0 + 3);
-        const uint32_t gm = max(max(c0, c1), max(c2, c3));
-        best = max(best, gm);
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(gm >= long16) != 0, 0)) relong(Rg, t0, 4u, alive0);
-        if (!alive_m) break;
+    bool snapped = budget_s <= 1u;  // wave-uniform: step chain >> 2 has been folded
+    auto snap = [&](uint32_t t1) __attribute__((always_inline)) {
+      if (t1 == budget_s) {  // the chain >> 2 result (deflate.ts:1075-1077)
+        thr_s = thr;
+        bt_s = bt;
+        lthr_s = lthr;
+        lbt_s = lbt;
+        snapped = true;
       }
     };
-    bool snapped = false;
-    for (uint32_t b = 0;; b++) {
+    const uint32_t base0 = (((uint32_t)(k - 64)) & (ZS_SW_RING - 1)) + 64u;  // block 0: step t at slot base0 - t
+    // t = 1: the head candidate (deflate.ts:1376)
+    {
+      const uint32_t key = R->key[base0 - 1u];
+      bool a1 = false;
+      uint32_t sc[1] = {0};
+      if (own && key >= khead) {
+        a1 = true;
+        head = 1u | ((p - (key & 0xffffu)) == ZS_MAX_DIST ? 0x8000u : 0u);
+        sc[0] = score(rmbits(S, base0 - 1u), 0);
+      }
+      alive_m = __builtin_amdgcn_ballot_w64(a1);
+      fold(sc[0], 1u, sc, 1u, base0);
+      snap(1u);
+    }
+    // masked step (blocks in which a chain ends): 0 for a lane whose chain ended
+    auto mstep = [&](uint32_t slot, uint32_t u) -> uint32_t {
+      alive_m &= __builtin_amdgcn_ballot_w64(R->key[slot] > klim);  // the chain ends at the first dead step (deflate.ts:1109)
+      alive_m = sw_uniform(alive_m);
+      const uint32_t v = score(rmbits(S, slot), u);
+      uint32_t r;
+      asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(alive_m));
+      return r;
+    };
+    // steps 2..4 (masked)
+    if (budget >= 4u) {
+      uint32_t sc[3];
+      for (uint32_t u = 0; u < 3; u++) sc[u] = mstep(base0 - 2u - u, u);
+      fold(max3(sc[0], sc[1], sc[2]), 2u, sc, 3u, base0);
+      snap(4u);
+    }
+    // Steps [ta, tb] of block b (ta = 1 mod 4, tb = 0 mod 4, wave-uniform):
+    // step t reads slot base - t, one address per group, immediate offsets inside.
+    auto group_fast = [&](uint32_t base, uint32_t t0, auto G) __attribute__((always_inline)) {
+      constexpr uint32_t N = decltype(G)::value;
+      // from the group's lowest slot up: one address, immediate offsets
+      const uint32_t lo = base - t0 - (N - 1u);
+      const uint2* const A = R->ab + lo;
+      const uint32_t* const C = R->c + lo;
+      uint32_t sc[N];
+#pragma unroll
+      for (uint32_t u = 0; u < N; u++) {
+        const uint2 ab = A[N - 1u - u];
+        sc[u] = score(S.mbits(ab.x, ab.y, A7 ? 0u : C[N - 1u - u]), u);
+      }
+      uint32_t gm;
+      if constexpr (N == 8)
+        gm = max(max3(sc[0], sc[1], sc[2]), max3(sc[3], sc[4], max3(sc[5], sc[6], sc[7])));
+      else
+        gm = max3(sc[0], sc[1], max(sc[2], sc[3]));
+      fold(gm, t0, sc, N, base);
+    };
+    auto group_masked = [&](uint32_t base, uint32_t t0, uint32_t t1) __attribute__((always_inline)) {
+      uint32_t sc[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) sc[u] = u <= t1 - t0 ? mstep(base - t0 - u, u) : 0u;  // (rare blocks)
+      fold(max(max3(sc[0], sc[1], sc[2]), max3(sc[3], sc[4], max3(sc[5], sc[6], sc[7]))), t0, sc, t1 - t0 + 1u,
+           base);
+    };
+    using G8 = std::integral_constant<uint32_t, 8>;
+    using G4 = std::integral_constant<uint32_t, 4>;
+    // Steps [ta, tb] of a block in groups of 8 (4 where the range or the
+    // snapshot cuts them).  A group in which every live lane is still live at
+    // its last step runs unmasked with the exec mask of the live lanes;
+    // otherwise masked.
+    auto run = [&](uint32_t base, uint32_t ta, uint32_t tb) __attribute__((always_inline)) {
+      for (uint32_t t0 = ta; t0 <= tb && alive_m;) {
+        uint32_t t1 = t0 + 7u <= tb ? t0 + 7u : t0 + 3u;
+        if (t0 <= budget_s && t1 > budget_s) t1 = budget_s;
+        const bool mine = ((alive_m >> lane) & 1u) != 0;
+        const uint64_t last_live = __builtin_amdgcn_ballot_w64(mine && R->key[base - t1] > klim);
+#if ZS_SW_EXP & 4
+        if (0) {
+#elif ZS_SW_EXP & 16
+        if (1) {
+#else
+        if (last_live == alive_m) {
+#endif
+          if (mine) {  // exec = the live lanes
+            if (t1 - t0 == 7u) group_fast(base, t0, G8{});
+            else group_fast(base, t0, G4{});
+          }
+        } else {
+          group_masked(base, t0, t1);
+        }
+        snap(t1);  // (every lane: one whose chain ended has its final best already)
+        t0 = t1 + 1u;
+      }
+    };
+    for (uint32_t b = 0; budget > 4u && alive_m; b++) {
       // block b = steps (64b, 64b + 64]: members k0 - 64b - 64 ... k0 - 64b + 62, i.e. the blocks b and b + 1 back
       if (b >= 1) {
         __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -470,26 +602,27 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
       }
       const uint32_t ta = b == 0 ? 5u : 64u * b + 1u;
       const uint32_t tb = min(64u * b + 64u, budget);
-      if (!snapped && budget_s <= tb) {  // the chain >> 2 result (deflate.ts:1075-1077); budgets are multiples of 4
-        if (budget_s >= ta) run(b, ta, budget_s);
-        best_s = best;
-        snapped = true;
-        if (budget_s + 1u <= tb) run(b, max(ta, budget_s + 1u), tb);
-      } else {
-        run(b, ta, tb);
-      }
-      if (tb >= budget || !alive_m) break;
+      // step t of this block at slot base - t
+      const uint32_t base = (((uint32_t)(k - 64 * (int)b - 64)) & (ZS_SW_RING - 1)) + 64u * b + 64u;
+      run(base, ta, tb);
+      if (tb >= budget) break;
     }
-    if (!snapped) best_s = best;
+    if (!snapped) {  // every chain ended before step chain >> 2
+      thr_s = thr;
+      bt_s = bt;
+      lthr_s = lthr;
+      lbt_s = lbt;
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     if (own) {
       uint32_t rx = 0, ry = 0;
       if (head) {
+        uint32_t L = 2, D = 0, Ls = 2, Ds = 0;
         if (tail) {  // maxc <= 12: min(lcp, maxc) exactly, first maximum in chain order (deflate.ts:1082-1105)
           uint32_t b = 2u << 16, bs = 2u << 16;
           for (uint32_t t = 1; t <= budget && (int)t <= k; t++) {
-            const uint32_t q = mem[k - (int)t];
+            const uint32_t q = member(k - (int)t);
             const uint32_t key = (sw_hash(sw_word(win, q)) << 16) | q;
             if (t == 1u ? key < khead : key <= klim) break;
             uint32_t len = 12;
@@ -501,43 +634,95 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
             b = max(b, sc);
             if (t <= budget_s) bs = max(bs, sc);
           }
-          best = b;
-          best_s = bs;
-        }
-        const uint32_t bl = best >> 16, bsl = best_s >> 16;
-        uint32_t bd = bl > 2u ? p - mem[k - (int)(0xffffu - (best & 0xffffu))] : 0u;
-        uint32_t bsd = bsl > 2u ? p - mem[k - (int)(0xffffu - (best_s & 0xffffu))] : 0u;
-        uint32_t L = bl, Ls = bsl;
-        if (nl) {
-          uint32_t lb = 0, ld = 0, lbs = 0, lds = 0;
-          auto take = [&](uint32_t t, uint32_t q) -> bool {
-            const uint32_t len = sw_extend(win, p, q, maxc);
-            if (len > lb) { lb = len; ld = p - q; }
-            if (t <= budget_s && len > lbs) { lbs = len; lds = p - q; }
-            return len >= nice;  // nice match: the walk ends (deflate.ts:1103)
-          };
-          if (ovf) {  // re-walk the chain from the first long candidate
-            for (uint32_t t = l0 >> 16; t <= budget && (int)t <= k; t++) {
-              const uint32_t q = mem[k - (int)t];
-              const uint32_t w0 = sw_word(win, q), w1 = sw_word(win, q + 4), w2 = sw_rec2(sw_word(win, q + 8));
-              const uint32_t key = (sw_hash(w0) << 16) | q;
-              if (t == 1u ? key < khead : key <= klim) break;
-              if (sw_lcp(w0, w1, w2, s0, s1, s2) < long_thr) continue;
-              if (take(t, q)) break;
-            }
-          } else {
-            if (!take(l0 >> 16, l0 & 0xffffu) && nl > 1 && !take(l1 >> 16, l1 & 0xffffu) && nl > 2 &&
-                !take(l2 >> 16, l2 & 0xffffu) && nl > 3)
-              take(l3 >> 16, l3 & 0xffffu);
+          L = b >> 16;
+          D = L > 2u ? p - member(k - (int)(0xffffu - (b & 0xffffu))) : 0u;
+          Ls = bs >> 16;
+          Ds = Ls > 2u ? p - member(k - (int)(0xffffu - (bs & 0xffffu))) : 0u;
+        } else {
+          if (bt) {
+            L = Sig::len(thr >> 3);
+            D = p - member(k - (int)bt);
           }
-          L = lb;
-          bd = ld;
-          if (lbs) { Ls = lbs; bsd = lds; }
+          if (bt_s) {
+            Ls = Sig::len(thr_s >> 3);
+            Ds = bt_s == bt ? D : p - member(k - (int)bt_s);
+          }
+          // long candidates beat every short one; a nice one's length was capped: measure it
+          auto long_of = [&](uint32_t lt, uint32_t t, uint32_t& len, uint32_t& dist) {
+            const uint32_t q = member(k - (int)t);
+            len = lt >> 3;
+            if (len >= nice) len = sw_extend(win, p, q, maxc, Sig::EXT);
+            dist = p - q;
+          };
+          if (lbt) long_of(lthr, lbt, L, D);
+          if (lbt_s) {
+            if (lbt_s == lbt) {
+              Ls = L;
+              Ds = D;
+            } else {
+              long_of(lthr_s, lbt_s, Ls, Ds);
+            }
+          }
         }
-        rx = (L << 16) | (L > 2u ? bd : 0u) | (head & 0x8000u);
-        ry = (Ls << 16) | (Ls > 2u ? bsd : 0u);
+        rx = (L << 16) | (L > 2u ? D : 0u) | (head & 0x8000u);
+        ry = (Ls << 16) | (Ls > 2u ? Ds : 0u);
       }
       out[p] = make_uint2(rx, ry);
     }
+  }
+}
+
+__global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                   const uint32_t* __restrict__ in_len,
+                                                   const uint64_t* __restrict__ pos_base,
+                                                   const uint16_t* __restrict__ members, uint2* __restrict__ mres,
+                                                   int chain, int nice_cfg) {
+  __shared__ __attribute__((aligned(16))) SwRing ring[16];
+  __shared__ __attribute__((aligned(16))) uint32_t win[ZS_SW_WIN_WORDS];
+  __shared__ uint16_t mwin[16][ZS_SW_MW];
+  __shared__ uint32_t next;
+  const int s = blockIdx.x;
+  const uint32_t n = in_len[s];
+  if (n > ZS_SWEEP_MAX || n < 3) return;
+  const uint8_t* src = in + in_off[s];
+  // the whole stream in LDS, zero padded (reads run up to 16 bytes past n);
+  // the OR of its bytes' top bits picks the signature form
+  uint32_t hi = 0;
+  if ((((uintptr_t)src) & 15u) == 0) {
+    for (uint32_t i = threadIdx.x; 4 * i < ZS_SW_WIN_WORDS; i += 1024) {
+      const uint32_t b = 16 * i;
+      uint4 v;
+      if (b + 16 <= n) v = ((const uint4*)src)[i];
+      else {
+        uint32_t t[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < 16; k++)
+          if (b + k < n) t[k >> 2] |= (uint32_t)src[b + k] << (8 * (k & 3));
+        v = make_uint4(t[0], t[1], t[2], t[3]);
+      }
+      hi |= v.x | v.y | v.z | v.w;
+      if (4 * i + 3 < ZS_SW_WIN_WORDS) *(uint4*)(win + 4 * i) = v;
+      else for (uint32_t k = 0; 4 * i + k < ZS_SW_WIN_WORDS; k++) win[4 * i + k] = (&v.x)[k];
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < ZS_SW_WIN_WORDS; i += 1024) {
+      uint32_t v = 0;
+      for (uint32_t k = 0; k < 4; k++)
+        if (4 * i + k < n) v |= (uint32_t)src[4 * i + k] << (8 * k);
+      hi |= v;
+      win[i] = v;
+    }
+  }
+  if (threadIdx.x == 0) next = 0;
+  const bool a7 = !__syncthreads_or((hi & 0x80808080u) != 0);
+  SwRing* const R = &ring[threadIdx.x >> 6];
+  const uint16_t* mem = members + pos_base[s];
+  uint2* out = mres + pos_base[s];
+  uint16_t* const mw = mwin[threadIdx.x >> 6];
+  if (chain + 64 <= (int)ZS_SW_MW) {
+    if (a7) sw_body<true, true>(win, R, mw, &next, n, mem, out, chain, nice_cfg);
+    else sw_body<false, true>(win, R, mw, &next, n, mem, out, chain, nice_cfg);
+  } else {  // levels 8, 9: positions from HBM
+    if (a7) sw_body<true, false>(win, R, mw, &next, n, mem, out, chain, nice_cfg);
+    else sw_body<false, false>(win, R, mw, &next, n, mem, out, chain, nice_cfg);
   }
 }
