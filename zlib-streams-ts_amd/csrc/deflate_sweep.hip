@@ -377,6 +377,16 @@ struct SwRing {
 // such a block runs with the exec mask of the live lanes and no per-step test.
 // A block in which some lane's chain ends runs the masked form (the step's
 // ballot of `key > klim` ands into the live mask, a dead lane's score is 0).
+#if ZS_SW_EXP & 64  // instrumentation (timing experiments only)
+__device__ unsigned long long zs_sw_stat[8];  // chunks, fast groups, masked groups, long branches, wave steps
+#define SW_STAT(i, v) do { if ((threadIdx.x & 63u) == __builtin_ctzll(__builtin_amdgcn_read_exec())) atomicAdd(&zs_sw_stat[i], (unsigned long long)(v)); } while (0)
+extern "C" int zs_sw_stats(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_sw_stat), sizeof(zs_sw_stat));
+}
+#else
+#define SW_STAT(i, v) do { } while (0)
+#endif
+
 template <bool A7, bool MW>
 static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, uint16_t* mw, uint32_t* next,
                                                uint32_t n, const uint16_t* mem, uint2* out, int chain,
@@ -426,6 +436,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     const int k0 = (int)(64 * c);
     const int k = k0 + (int)lane;
     const bool own = (uint32_t)k < m;
+    SW_STAT(0, 1);
     const uint32_t p = own ? mem[k] : 0u;
     mw0 = k0 - (int)budget;
     if (MW) mw[k - mw0] = (uint16_t)p;
@@ -474,6 +485,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
 #else
       if (__builtin_expect(__builtin_amdgcn_ballot_w64(gm >= long_m) != 0, 0)) {
 #endif
+        SW_STAT(3, 1);
         if (gm >= long_m && (lthr >> 3) < nice) {
           uint32_t gl = 0;
 #pragma unroll
@@ -518,18 +530,25 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
       snap(1u);
     }
     // masked step (blocks in which a chain ends): 0 for a lane whose chain ended
-    auto mstep = [&](uint32_t slot, uint32_t u) -> uint32_t {
-      alive_m &= __builtin_amdgcn_ballot_w64(R->key[slot] > klim);  // the chain ends at the first dead step (deflate.ts:1109)
-      alive_m = sw_uniform(alive_m);
+    // masked step (groups in which a chain ends): liveness is monotone in t
+    // (keys fall with the member index), so a step is live iff its own key is
+    // (and the lane was live when the group began); lm = the live lanes
+    auto mstep = [&](uint32_t slot, uint32_t u, uint64_t& lm) -> uint32_t {
+      const uint32_t key = R->key[slot];
+      asm("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(lm) : "v"(key), "v"(klim));
+      lm &= alive_m;
       const uint32_t v = score(rmbits(S, slot), u);
       uint32_t r;
-      asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(alive_m));
+      asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(lm));
       return r;
     };
     // steps 2..4 (masked)
     if (budget >= 4u) {
       uint32_t sc[3];
-      for (uint32_t u = 0; u < 3; u++) sc[u] = mstep(base0 - 2u - u, u);
+      uint64_t lm = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < 3; u++) sc[u] = mstep(base0 - 2u - u, u, lm);
+      alive_m = sw_uniform(lm);  // the lanes live at step 4
       fold(max3(sc[0], sc[1], sc[2]), 2u, sc, 3u, base0);
       snap(4u);
     }
@@ -556,8 +575,16 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     };
     auto group_masked = [&](uint32_t base, uint32_t t0, uint32_t t1) __attribute__((always_inline)) {
       uint32_t sc[8];
+      uint64_t lm = 0, last = 0;
 #pragma unroll
-      for (uint32_t u = 0; u < 8; u++) sc[u] = u <= t1 - t0 ? mstep(base - t0 - u, u) : 0u;  // (rare blocks)
+      for (uint32_t u = 0; u < 8; u++) {
+        sc[u] = 0u;
+        if (u <= t1 - t0) {
+          sc[u] = mstep(base - t0 - u, u, lm);
+          last = lm;
+        }
+      }
+      alive_m = sw_uniform(last);  // the lanes live at the group's last step
       fold(max(max3(sc[0], sc[1], sc[2]), max3(sc[3], sc[4], max3(sc[5], sc[6], sc[7]))), t0, sc, t1 - t0 + 1u,
            base);
     };
@@ -580,11 +607,15 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
 #else
         if (last_live == alive_m) {
 #endif
+          SW_STAT(1, 1);
+          SW_STAT(4, t1 - t0 + 1u);
           if (mine) {  // exec = the live lanes
             if (t1 - t0 == 7u) group_fast(base, t0, G8{});
             else group_fast(base, t0, G4{});
           }
         } else {
+          SW_STAT(2, 1);
+          SW_STAT(4, t1 - t0 + 1u);
           group_masked(base, t0, t1);
         }
         snap(t1);  // (every lane: one whose chain ended has its final best already)
