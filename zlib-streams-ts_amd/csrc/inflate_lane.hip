@@ -140,6 +140,93 @@ static __device__ __forceinline__ zcode zs_dist_entry(uint32_t d, bool d64) {
   return zpack(f + x, 0, ((2u | (d & 1u)) << x) + 1u);
 }
 
+// Output of one lane, write-combined in registers: the bytes of the current
+// 16-byte aligned unit collect in u0..u2 (its completed words, oldest first)
+// and cw (the word being filled), and a completed unit leaves as ONE 16-byte
+// store instead of sixteen byte stores (one lane's bytes are on one line; 64
+// lanes' byte stores were 64 separate transactions each).  P counts bytes from
+// the unit-aligned base below the member's first byte (out_off is 4-aligned, so
+// the first unit is entered at word w0 = (dst & 15) / 4 and its earlier words
+// -- another member's -- are never stored).
+struct zs_lane_out {
+  uint32_t* base;  // 16-byte aligned, <= dst
+  uint32_t P, w0;
+  uint32_t u0, u1, u2, cw;
+  __device__ __forceinline__ void init(uint8_t* dst) {
+    const uintptr_t a = (uintptr_t)dst;
+    base = reinterpret_cast<uint32_t*>(a & ~(uintptr_t)15);
+    P = (uint32_t)(a & 15u);
+    w0 = P >> 2;
+    u0 = u1 = u2 = cw = 0;
+  }
+  // the completed unit at P - 16 (P a multiple of 16): one 16-byte store, or
+  // dword stores from w0 on for the member's first unit
+  __device__ __forceinline__ void store_unit(uint32_t w3) {
+    uint32_t* q = base + ((P - 16u) >> 2);
+    if (P - 16u >= 16u || w0 == 0) {
+      *reinterpret_cast<uint4*>(q) = make_uint4(u0, u1, u2, w3);
+    } else {
+      if (w0 <= 1) q[1] = u1;
+      if (w0 <= 2) q[2] = u2;
+      q[3] = w3;
+    }
+  }
+  // a completed word (P a multiple of 4 after it)
+  __device__ __forceinline__ void word(uint32_t w) {
+    P += 4;
+    if ((P & 15u) == 0) {
+      store_unit(w);
+    } else {
+      u0 = u1;
+      u1 = u2;
+      u2 = w;
+    }
+  }
+  // n (1..4) bytes, the low bytes of v (bytes above n zero)
+  __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
+    const uint32_t a = P & 3u;
+    cw |= v << (8u * a);
+    if (a + n >= 4u) {
+      const uint32_t w = cw;
+      cw = a ? v >> (32u - 8u * a) : 0u;  // the bytes past the word
+      P -= a;
+      word(w);
+      P += a + n - 4u;
+    } else {
+      P += n;
+    }
+  }
+  __device__ __forceinline__ void byte(uint32_t b) { put(b & 0xffu, 1u); }
+  // the current unit's bytes so far go to memory (dword stores; the last
+  // word's bytes past P are inside the member's capacity and are rewritten
+  // later): after this, every byte below P is in memory
+  __device__ __forceinline__ void spill() {
+    const uint32_t ub = P & ~15u, wi = (P >> 2) & 3u;  // completed words of this unit
+    uint32_t* q = base + (ub >> 2);
+    const uint32_t first = ub == 0 ? w0 : 0u;
+    // word i of the unit (i < wi) is u[3 - wi + i]
+    if (wi >= 3 && first <= 0) q[0] = u0;
+    if (wi >= 2 && first <= wi - 2) q[wi - 2] = u1;
+    if (wi >= 1 && first <= wi - 1) q[wi - 1] = u2;
+    if ((P & 3u) && first <= wi) q[wi] = cw;
+  }
+  // after bytes were stored straight to memory up to P: the current unit's
+  // words back into the registers
+  __device__ __forceinline__ void reload() {
+    const uint32_t ub = P & ~15u, wi = (P >> 2) & 3u;
+    const uint32_t* q = base + (ub >> 2);
+    // only words up to the one holding P are read (the unit may end past the buffer)
+    const uint32_t x0 = q[0], x1 = wi >= 1 ? q[1] : 0u, x2 = wi >= 2 ? q[2] : 0u, x3 = wi >= 3 ? q[3] : 0u;
+    // the shift register holds word i (i < wi) at u[3 - wi + i]
+    u2 = wi == 3 ? x2 : wi == 2 ? x1 : wi == 1 ? x0 : 0u;
+    u1 = wi == 3 ? x1 : wi == 2 ? x0 : 0u;
+    u0 = wi == 3 ? x0 : 0u;
+    const uint32_t a = P & 3u;
+    const uint32_t xw = wi == 0 ? x0 : wi == 1 ? x1 : wi == 2 ? x2 : x3;
+    cw = a ? xw & ((1u << (8u * a)) - 1u) : 0u;
+  }
+};
+
 __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off,
                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -168,6 +255,8 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   R.bits = 0;
   R.pf = zs_lr_load4(R, 0);
   uint8_t* dst = out + out_off[s];
+  zs_lane_out W;
+  W.init(dst);
   // This path decodes a member in one go, without the stream layer's call
   // boundaries.  A member whose input fits one 32 KiB sub-chunk and whose
   // output fits one 64 KiB output buffer is decoded by ONE inflate() call of
@@ -210,7 +299,7 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       zs_lr_align(R);
       const uint32_t len = zs_lr_take(R, 16), nlen = zs_lr_take(R, 16);
       if (len != (nlen ^ 0xffffu) || zs_lr_over(R) || total + len > cap) { bail = true; break; }
-      for (uint32_t i = 0; i < len; i++) dst[total + i] = (uint8_t)zs_lr_take(R, 8);
+      for (uint32_t i = 0; i < len; i++) W.byte(zs_lr_take(R, 8));
       total += len;
       if (zs_lr_over(R)) { bail = true; break; }
       continue;
@@ -290,7 +379,8 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       uint32_t op = C_OP(here);
       if (op == 0) {
         if (total >= cap) { bail = true; break; }
-        dst[total++] = (uint8_t)C_VAL(here);
+        W.byte(C_VAL(here));
+        total++;
         continue;
       }
       if (op & 32) break;                   // end of block
@@ -311,13 +401,39 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
       const uint8_t* from = dst + total - dist;
       uint8_t* to = dst + total;
+      const uint32_t fsh = (uint32_t)((uintptr_t)from & 3u);
+      const uint32_t* fw = reinterpret_cast<const uint32_t*>(from - fsh);
+      if (dist >= 16u + (W.P & 15u)) {
+        // every source byte of every 16-byte round lies below the unit being
+        // combined, so is in memory already: 16 bytes per round trip, into the
+        // write combiner a word at a time
+        for (uint32_t i = 0; i < len; i += 16) {
+          uint32_t x[5];
+#pragma unroll
+          for (int k = 0; k < 5; k++) x[k] = fw[(i >> 2) + (uint32_t)k];
+          const uint32_t rem = len - i;
+#pragma unroll
+          for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t wd = __builtin_amdgcn_alignbyte(x[k + 1], x[k], fsh);
+            if (rem >= 4u * k + 4u) {
+              W.put(wd, 4u);
+            } else if (rem > 4u * k) {
+              const uint32_t nb = rem - 4u * k;
+              W.put(wd & ((1u << (8u * nb)) - 1u), nb);
+            }
+          }
+        }
+        total += len;
+        continue;
+      }
+      // a source within the unit being combined: its bytes go to memory, the
+      // copy stores bytes straight to memory, and the combiner picks the unit up
+      W.spill();
       // A copy waits for its source bytes once per chunk (loads after the
       // stores of the chunk before), so the chunk is as wide as the distance
       // allows.  Source words are aligned loads funnel-shifted into place; a
       // word that is read always holds at least one byte of the output region
       // (so never leaves its pages), and only bytes below `to` are used.
-      const uint32_t fsh = (uint32_t)((uintptr_t)from & 3u);
-      const uint32_t* fw = reinterpret_cast<const uint32_t*>(from - fsh);
       if (dist >= 16) {  // 16 bytes per round trip
         for (uint32_t i = 0; i < len; i += 16) {
           uint32_t x[5];
@@ -352,9 +468,12 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
         }
       }
       total += len;
+      W.P += len;
+      W.reload();
     }
     if (zs_lr_over(R)) bail = true;
   }
+  if (!bail) W.spill();  // the last unit's bytes
   // ---- trailer (inflate.ts:1006-1036)
   if (!bail && wrap) {
     zs_lr_align(R);
