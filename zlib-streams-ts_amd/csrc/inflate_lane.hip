@@ -4,6 +4,11 @@
 #include "zs_common.h"
 #include "zs_inflate.h"
 #include "zs_inftab.h"
+#ifndef ZS_IL_EXP
+#define ZS_IL_EXP 0  // experiment builds (timing only; 0 in the product): 1 no stores, 2 no copy loads, 64 counters
+#endif
+#define IL_ST(x) do { if (!(ZS_IL_EXP & 1)) { x; } } while (0)
+#define IL_LD(x) ((ZS_IL_EXP & 2) ? 0u : (uint32_t)(x))
 
 // One LANE per member.  The exact kernel above spends a whole wave on one
 // stream because it re-enacts the stream layer's call boundaries; a member
@@ -19,9 +24,7 @@
 // gzip header fields, a checksum or length mismatch, or output capacity -- so
 // statuses, phases and messages always come from the exact state machine.
 struct zs_lane_tabs {
-  zcode codes[ENOUGH_LENS + ENOUGH_DISTS_9];
-  uint16_t lens[320];
-  uint16_t work[288];
+  uint16_t lens[320];  // the block's code lengths (lit/len then distance; the header's code-length code first)
 };
 
 struct zs_lane_reader {
@@ -73,52 +76,94 @@ static __device__ __forceinline__ void zs_lr_align(zs_lane_reader& R) {
   R.bits -= d;
 }
 
-// decode one Huffman symbol with a zlib table (root `rbits`); returns the final entry
-static __device__ __forceinline__ zcode zs_lane_decode(zs_lane_reader& R, const zcode* t, uint32_t rbits) {
-  if (R.bits < 32) zs_lr_fill(R);
-  zcode here = t[(uint32_t)R.hold & ((1u << rbits) - 1)];
-  if (C_OP(here) && (C_OP(here) & 0xf0) == 0) {  // second-level table
-    const uint32_t rb = C_BITS(here);
-    const zcode last = here;
-    here = t[C_VAL(last) + (((uint32_t)R.hold & ((1u << (rb + C_OP(last))) - 1)) >> rb)];
-    R.hold >>= rb;
-    R.bits -= rb;
-  }
-  R.hold >>= C_BITS(here);
-  R.bits -= C_BITS(here);
-  return here;
-}
-
-// LDS root tables of one lane: 8-bit lit/len and 6-bit distance roots, u16
-// entries (code length << 12 | symbol), 0 = code longer than the root (the lane
-// then decodes with its zlib table in HBM).  640 B per lane: four 64-lane
-// workgroups fill a CU's 160 KB.
-#define ZS_LROOT 8u
-#define ZS_DROOT 6u
-struct zs_lane_lds {
-  uint16_t lit[1u << ZS_LROOT];
-  uint16_t dist[1u << ZS_DROOT];
+// Canonical Huffman decoding (RFC 1951 3.2.2) with the code's shape in
+// registers.  lim[l-1] is the end of the length-l codes left-justified to 15
+// bits, so with the next 15 input bits read MSB first (rev), a code's length is
+// one more than the number of limits <= rev, and its rank in (length, symbol)
+// order is rev shifted down to that length plus D[length-1].  The symbols by
+// rank are the only table, in LDS.  No memory access before the symbol itself
+// and none in HBM: zlib's two-level tables (8-bit LDS roots before this) sent
+// every code longer than the root to a second-level table in HBM, and some lane
+// of a wave needed one in 68% of the C3 symbol steps -- a full memory latency
+// for the whole wave each time.
+struct zs_canon {
+  uint32_t lim[15];
+  uint32_t D[16];
 };
 
-static __device__ void zs_lane_root(uint16_t* tab, uint32_t rbits, const uint16_t* lens, uint32_t n) {
-  uint32_t count[16], next[16];
-  for (uint32_t l = 0; l < 16; l++) count[l] = 0;
-  for (uint32_t i = 0; i < n; i++) count[lens[i]]++;
-  count[0] = 0;
-  uint32_t code = 0;
-  for (uint32_t l = 1; l < 16; l++) {  // canonical first codes (RFC 1951 3.2.2)
-    code = (code + count[l - 1]) << 1;
-    next[l] = code;
+// A lane's LDS: 548 B (a CU's 160 KB holds four 64-lane workgroups).
+struct zs_lane_lds {
+  uint32_t ring[32];  // the last 128 output bytes (zs_lane_out)
+  uint8_t lsym[288];  // lit/len symbols by rank, low 8 bits
+  uint32_t lhi[9];    // their bit 8, one bit per rank
+  uint8_t dsym[32];   // distance symbols by rank (the header's code-length code first)
+  uint32_t cnt[16];   // codes per length, then the next free rank of each length
+};
+
+// C from lens[0..n) (the member's scratch in HBM); false unless the code is
+// complete.  zlib's inflate_table rejects over-subscribed sets and incomplete
+// ones but for a lone code of length 1 (inftrees.ts:128-139); a lane bails on
+// every incomplete set and leaves that case to the exact path.
+static __device__ bool zs_canon_build(zs_canon& C, uint32_t* cnt, uint8_t* sym8, uint32_t* hi, const uint16_t* lens,
+                                      uint32_t n) {
+#pragma unroll
+  for (int l = 0; l < 16; l++) cnt[l] = 0;
+  if (hi)
+#pragma unroll
+    for (int w = 0; w < 9; w++) hi[w] = 0;
+#pragma unroll 8
+  for (uint32_t i = 0; i < n; i++) atomicAdd(&cnt[lens[i]], 1u);
+  uint32_t code = 0, rank = 0;
+  int left = 1;
+#pragma unroll
+  for (int l = 1; l <= 15; l++) {
+    const uint32_t c = cnt[l];
+    left = 2 * left - (int)c;  // once negative (over-subscribed) it stays so
+    C.lim[l - 1] = (code + c) << (15 - l);
+    C.D[l - 1] = rank - code;
+    cnt[l] = rank;
+    rank += c;
+    code = (code + c) << 1;
   }
-  for (uint32_t k = 0; k < (1u << rbits); k++) tab[k] = 0;
-  for (uint32_t sym = 0; sym < n; sym++) {
-    const uint32_t l = lens[sym];
-    if (l == 0) continue;
-    const uint32_t c = next[l]++;
-    if (l > rbits) continue;
-    const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);  // the stream sends codes MSB first
-    for (uint32_t k = r; k < (1u << rbits); k += 1u << l) tab[k] = (uint16_t)((l << 12) | sym);
+  C.D[15] = 0;
+  if (left != 0) return false;
+#pragma unroll 8
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t l = lens[i];
+    if (l) {
+      const uint32_t k = atomicAdd(&cnt[l], 1u);
+      sym8[k] = (uint8_t)i;
+      if (hi && (i >> 8)) atomicOr(&hi[k >> 5], 1u << (k & 31u));
+    }
   }
+  return true;
+}
+
+// the rank of the code at the front of the bit buffer; L = its length (16: no
+// such code -- the caller bails)
+static __device__ __forceinline__ uint32_t zs_canon_rank(const zs_canon& C, const zs_lane_reader& R, uint32_t& L) {
+  const uint32_t rev = __builtin_bitreverse32((uint32_t)R.hold) >> 17;
+  // the values pass an empty asm so each select below is between registers (the
+  // compiler otherwise selects an address into C and keeps C in scratch)
+  uint32_t d[16];
+#pragma unroll
+  for (int l = 0; l < 16; l++) {
+    d[l] = C.D[l];
+    asm("" : "+v"(d[l]));
+  }
+  uint32_t n = 1, D = d[0];
+#pragma unroll
+  for (int l = 0; l < 15; l++) {
+    const bool c = rev >= C.lim[l];
+    n += c;
+    D = c ? d[l + 1] : D;
+  }
+  L = n;
+  return (rev >> ((15u - n) & 31u)) + D;
+}
+static __device__ __forceinline__ void zs_lr_drop(zs_lane_reader& R, uint32_t k) {
+  R.hold >>= k;
+  R.bits -= k;
 }
 
 // a root-table symbol as the zlib table entry the decoder consumes (zs_lbase /
@@ -140,92 +185,114 @@ static __device__ __forceinline__ zcode zs_dist_entry(uint32_t d, bool d64) {
   return zpack(f + x, 0, ((2u | (d & 1u)) << x) + 1u);
 }
 
-// Output of one lane, write-combined in registers: the bytes of the current
-// 16-byte aligned unit collect in u0..u2 (its completed words, oldest first)
-// and cw (the word being filled), and a completed unit leaves as ONE 16-byte
-// store instead of sixteen byte stores (one lane's bytes are on one line; 64
-// lanes' byte stores were 64 separate transactions each).  P counts bytes from
-// the unit-aligned base below the member's first byte (out_off is 4-aligned, so
-// the first unit is entered at word w0 = (dst & 15) / 4 and its earlier words
-// -- another member's -- are never stored).
+// Output of one lane.  Bytes collect in cw (the word being filled) and each
+// completed word goes to the lane's 128-byte ring in LDS; HBM sees whole
+// 16-byte units, stored from the ring by flush() -- called for every lane of
+// the wave at once when one of them holds 64 unstored bytes, so stores come in
+// rare bursts.  (Every s_waitcnt on a load also waits for the wave's earlier
+// stores; with a store in nearly every symbol step, the input refills and copy
+// loads waited out store latencies: half of C3's time.)  The ring also serves
+// every copy source up to ZS_RING_SRC bytes back.  P counts bytes from the
+// unit-aligned base below the member's first byte (out_off is 4-aligned: the
+// first unit is entered at word w0 and its earlier words -- another member's --
+// are never stored); F is the start of the first unstored unit.  Writing the
+// word at W overwrites the one at W - 128, so W - 124 <= F must hold: room()
+// before a round of up to 16 bytes keeps P - F <= 108, and the partial word a
+// sync() writes leaves [P - 124, P) readable.
+#define ZS_RING 128u
+#define ZS_RING_SRC 124u
 struct zs_lane_out {
   uint32_t* base;  // 16-byte aligned, <= dst
-  uint32_t P, w0;
-  uint32_t u0, u1, u2, cw;
-  __device__ __forceinline__ void init(uint8_t* dst) {
+  uint32_t* ring;  // LDS: output byte X at ring byte X % ZS_RING
+  uint32_t P, F, w0, cw;
+  __device__ __forceinline__ void init(uint8_t* dst, uint32_t* lds_ring) {
     const uintptr_t a = (uintptr_t)dst;
     base = reinterpret_cast<uint32_t*>(a & ~(uintptr_t)15);
+    ring = lds_ring;
     P = (uint32_t)(a & 15u);
     w0 = P >> 2;
-    u0 = u1 = u2 = cw = 0;
+    F = 0;
+    cw = 0;
   }
-  // the completed unit at P - 16 (P a multiple of 16): one 16-byte store, or
-  // dword stores from w0 on for the member's first unit
-  __device__ __forceinline__ void store_unit(uint32_t w3) {
-    uint32_t* q = base + ((P - 16u) >> 2);
-    if (P - 16u >= 16u || w0 == 0) {
-      *reinterpret_cast<uint4*>(q) = make_uint4(u0, u1, u2, w3);
-    } else {
-      if (w0 <= 1) q[1] = u1;
-      if (w0 <= 2) q[2] = u2;
-      q[3] = w3;
-    }
-  }
-  // a completed word (P a multiple of 4 after it)
-  __device__ __forceinline__ void word(uint32_t w) {
-    P += 4;
-    if ((P & 15u) == 0) {
-      store_unit(w);
-    } else {
-      u0 = u1;
-      u1 = u2;
-      u2 = w;
-    }
-  }
+  __device__ __forceinline__ uint32_t& slot(uint32_t x) { return ring[(x >> 2) & (ZS_RING / 4 - 1)]; }
   // n (1..4) bytes, the low bytes of v (bytes above n zero)
   __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
     const uint32_t a = P & 3u;
     cw |= v << (8u * a);
     if (a + n >= 4u) {
-      const uint32_t w = cw;
+      slot(P) = cw;
       cw = a ? v >> (32u - 8u * a) : 0u;  // the bytes past the word
-      P -= a;
-      word(w);
-      P += a + n - 4u;
-    } else {
-      P += n;
     }
+    P += n;
   }
   __device__ __forceinline__ void byte(uint32_t b) { put(b & 0xffu, 1u); }
-  // the current unit's bytes so far go to memory (dword stores; the last
-  // word's bytes past P are inside the member's capacity and are rewritten
-  // later): after this, every byte below P is in memory
-  __device__ __forceinline__ void spill() {
-    const uint32_t ub = P & ~15u, wi = (P >> 2) & 3u;  // completed words of this unit
-    uint32_t* q = base + (ub >> 2);
-    const uint32_t first = ub == 0 ? w0 : 0u;
-    // word i of the unit (i < wi) is u[3 - wi + i]
-    if (wi >= 3 && first <= 0) q[0] = u0;
-    if (wi >= 2 && first <= wi - 2) q[wi - 2] = u1;
-    if (wi >= 1 && first <= wi - 1) q[wi - 1] = u2;
-    if ((P & 3u) && first <= wi) q[wi] = cw;
+  // the partial word into the ring too: the ring then holds every byte in [P - 124, P)
+  __device__ __forceinline__ void sync() {
+    if (P & 3u) slot(P) = cw;
   }
-  // after bytes were stored straight to memory up to P: the current unit's
-  // words back into the registers
-  __device__ __forceinline__ void reload() {
-    const uint32_t ub = P & ~15u, wi = (P >> 2) & 3u;
-    const uint32_t* q = base + (ub >> 2);
-    // only words up to the one holding P are read (the unit may end past the buffer)
-    const uint32_t x0 = q[0], x1 = wi >= 1 ? q[1] : 0u, x2 = wi >= 2 ? q[2] : 0u, x3 = wi >= 3 ? q[3] : 0u;
-    // the shift register holds word i (i < wi) at u[3 - wi + i]
-    u2 = wi == 3 ? x2 : wi == 2 ? x1 : wi == 1 ? x0 : 0u;
-    u1 = wi == 3 ? x1 : wi == 2 ? x0 : 0u;
-    u0 = wi == 3 ? x0 : 0u;
-    const uint32_t a = P & 3u;
-    const uint32_t xw = wi == 0 ? x0 : wi == 1 ? x1 : wi == 2 ? x2 : x3;
-    cw = a ? xw & ((1u << (8u * a)) - 1u) : 0u;
+  // the complete units below P to HBM
+  __device__ __forceinline__ void flush() {
+    while (F + 16u <= P) {
+      const uint32_t x0 = slot(F), x1 = slot(F + 4u), x2 = slot(F + 8u), x3 = slot(F + 12u);
+      uint32_t* q = base + (F >> 2);
+      if (F >= 16u || w0 == 0) {
+        IL_ST(*reinterpret_cast<uint4*>(q) = make_uint4(x0, x1, x2, x3));
+      } else {
+        if (w0 <= 1) IL_ST(q[1] = x1);
+        if (w0 <= 2) IL_ST(q[2] = x2);
+        IL_ST(q[3] = x3);
+      }
+      F += 16u;
+    }
+  }
+  // room for a round of up to 16 bytes
+  __device__ __forceinline__ void room() {
+    if (P - F > ZS_RING - 20u) flush();
+  }
+  // the member's last bytes (the last word's bytes past P are inside its capacity)
+  __device__ __forceinline__ void finish() {
+    sync();
+    flush();
+    uint32_t* q = base + (F >> 2);
+    for (uint32_t i = 0; i < 4; i++)
+      if (F + 4u * i < P && (F >= 16u || i >= w0)) IL_ST(q[i] = slot(F + 4u * i));
+  }
+  // 16 bytes from ring position x (any alignment; x + 16 <= P after a sync)
+  __device__ __forceinline__ void ring16(uint32_t x, uint32_t (&w)[4]) {
+    const uint32_t sh = x & 3u;
+    uint32_t r[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) r[k] = slot(x + 4u * (uint32_t)k);
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(r[k + 1], r[k], sh);
+  }
+  // up to 16 bytes of w (n of them)
+  __device__ __forceinline__ void put16(const uint32_t (&w)[4], uint32_t n) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      if (n >= 4u * k + 4u) {
+        put(w[k], 4u);
+      } else if (n > 4u * k) {
+        const uint32_t nb = n - 4u * k;
+        put(w[k] & ((1u << (8u * nb)) - 1u), nb);
+      }
+    }
   }
 };
+
+#if ZS_IL_EXP & 64
+// per wave (max over its lanes): symbol iterations, ones with a slow lit/len
+// decode, a slow distance decode, a direct copy, a spilled copy; clock cycles in
+// headers+tables, in symbols, in all
+__device__ unsigned long long zs_il_stat[8];
+extern "C" int zs_il_stats(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_il_stat), sizeof(zs_il_stat));
+}
+#define IL_ANY(c) ((__builtin_amdgcn_ballot_w64(c) != 0) ? 1ull : 0ull)
+#define IL_FIRST() ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))
+#define IL_T(v) const unsigned long long v = clock64()
+#define IL_ACC(i, v) do { if (IL_FIRST()) st[i] += clock64() - v; } while (0)
+#endif
 
 __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off,
@@ -254,9 +321,15 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   R.hold = 0;
   R.bits = 0;
   R.pf = zs_lr_load4(R, 0);
+#if ZS_IL_EXP & 64
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long tk0 = clock64();
+  unsigned long long tk = tk0;
+#endif
   uint8_t* dst = out + out_off[s];
+  zs_canon CL, CD;
   zs_lane_out W;
-  W.init(dst);
+  W.init(dst, F.ring);
   // This path decodes a member in one go, without the stream layer's call
   // boundaries.  A member whose input fits one 32 KiB sub-chunk and whose
   // output fits one 64 KiB output buffer is decoded by ONE inflate() call of
@@ -292,52 +365,51 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   while (!bail && !last) {
     last = zs_lr_take(R, 1) != 0;
     const uint32_t type = zs_lr_take(R, 2);
-    const zcode* lt;
-    const zcode* dt;
-    uint32_t lbits, dbits;
     if (type == 0) {  // stored (inflate.ts:615-660)
       zs_lr_align(R);
       const uint32_t len = zs_lr_take(R, 16), nlen = zs_lr_take(R, 16);
       if (len != (nlen ^ 0xffffu) || zs_lr_over(R) || total + len > cap) { bail = true; break; }
-      for (uint32_t i = 0; i < len; i++) W.byte(zs_lr_take(R, 8));
+      for (uint32_t i = 0; i < len; i++) {
+        if (W.P - W.F > ZS_RING - 8u) W.flush();
+        W.byte(zs_lr_take(R, 8));
+      }
       total += len;
       if (zs_lr_over(R)) { bail = true; break; }
       continue;
     }
-    if (type == 1) {  // fixed tables (inflate.ts:218-280)
-      uint32_t sym, used;
-      for (sym = 0; sym < 144; sym++) T.lens[sym] = 8;
-      for (; sym < 256; sym++) T.lens[sym] = 9;
-      for (; sym < 280; sym++) T.lens[sym] = 7;
-      for (; sym < 288; sym++) T.lens[sym] = 8;
-      lbits = 9;
-      zs_inflate_table(LENS, T.lens, 288, T.codes, &lbits, T.work, d64, &used);
-      for (sym = 0; sym < 32; sym++) T.lens[sym] = 5;
-      dbits = 5;
-      zs_inflate_table(DISTS, T.lens, 32, T.codes + used, &dbits, T.work, d64, &sym);
-      lt = T.codes;
-      dt = T.codes + used;
-      for (sym = 0; sym < 288; sym++) T.lens[sym] = sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : 8;
-      zs_lane_root(F.lit, ZS_LROOT, T.lens, 286);  // 286/287 stay out of the root: invalid codes decode via T
-      for (sym = 0; sym < 30; sym++) T.lens[sym] = 5;
-      zs_lane_root(F.dist, ZS_DROOT, T.lens, d64 ? 32 : 30);  // deflate: 30/31 likewise
+    uint32_t nlen, ndist;
+    if (type == 1) {  // fixed codes (inflate.ts:218-280)
+      nlen = 288;
+      ndist = 32;
+      for (uint32_t sym = 0; sym < 320; sym++)
+        T.lens[sym] = sym < 144 ? 8 : sym < 256 ? 9 : sym < 280 ? 7 : sym < 288 ? 8 : 5;
     } else if (type == 2) {  // dynamic (inflate.ts:662-836)
-      const uint32_t nlen = zs_lr_take(R, 5) + 257, ndist = zs_lr_take(R, 5) + 1, ncode = zs_lr_take(R, 4) + 4;
+      nlen = zs_lr_take(R, 5) + 257;
+      ndist = zs_lr_take(R, 5) + 1;
+      const uint32_t ncode = zs_lr_take(R, 4) + 4;
       if (nlen > 286 || (!d64 && ndist > 30)) { bail = true; break; }
       uint32_t i;
       for (i = 0; i < ncode; i++) T.lens[ZS_BL_ORDER[i]] = (uint16_t)zs_lr_take(R, 3);
       for (; i < 19; i++) T.lens[ZS_BL_ORDER[i]] = 0;
-      uint32_t cbits = 7, used;
-      if (zs_inflate_table(CODES, T.lens, 19, T.codes, &cbits, T.work, d64, &used)) { bail = true; break; }
+      if (!zs_canon_build(CD, F.cnt, F.dsym, nullptr, T.lens, 19)) { bail = true; break; }
       i = 0;
+      uint32_t prev = 0;
       while (i < nlen + ndist) {
-        const zcode here = zs_lane_decode(R, T.codes, cbits);
-        const uint32_t v = C_VAL(here);
-        if (v < 16) { T.lens[i++] = (uint16_t)v; continue; }
+        if (R.bits < 32) zs_lr_fill(R);
+        uint32_t L;
+        const uint32_t k = zs_canon_rank(CD, R, L);
+        if (L > 15) { bail = true; break; }
+        zs_lr_drop(R, L);
+        const uint32_t v = F.dsym[k];
+        if (v < 16) {
+          T.lens[i++] = (uint16_t)v;
+          prev = v;
+          continue;
+        }
         uint32_t rep, val = 0;
         if (v == 16) {
           if (i == 0) { bail = true; break; }
-          val = T.lens[i - 1];
+          val = prev;
           rep = 3 + zs_lr_take(R, 2);
         } else if (v == 17) {
           rep = 3 + zs_lr_take(R, 3);
@@ -346,36 +418,45 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
         }
         if (i + rep > nlen + ndist) { bail = true; break; }
         while (rep--) T.lens[i++] = (uint16_t)val;
+        prev = val;
       }
       if (bail || zs_lr_over(R) || T.lens[256] == 0) { bail = true; break; }
-      lbits = 9;
-      uint32_t lused, dused;
-      if (zs_inflate_table(LENS, T.lens, nlen, T.codes, &lbits, T.work, d64, &lused)) { bail = true; break; }
-      dbits = 6;
-      if (zs_inflate_table(DISTS, T.lens + nlen, ndist, T.codes + lused, &dbits, T.work, d64, &dused)) {
-        bail = true;
-        break;
-      }
-      lt = T.codes;
-      dt = T.codes + lused;
-      zs_lane_root(F.lit, ZS_LROOT, T.lens, nlen);
-      zs_lane_root(F.dist, ZS_DROOT, T.lens + nlen, ndist);
     } else {
       bail = true;  // "invalid block type"
       break;
     }
+    if (!zs_canon_build(CL, F.cnt, F.lsym, F.lhi, T.lens, nlen) ||
+        !zs_canon_build(CD, F.cnt, F.dsym, nullptr, T.lens + nlen, ndist)) {
+      bail = true;
+      break;
+    }
+#if ZS_IL_EXP & 64
+    { const unsigned long long t = clock64(); st[5] += t - tk; tk = t; }
+#endif
     // symbols (inffast.ts:5-228 semantics, without the call boundaries)
     for (;;) {
-      if (R.bits < 32) zs_lr_fill(R);
-      zcode here;
-      const uint32_t fe = F.lit[(uint32_t)R.hold & ((1u << ZS_LROOT) - 1)];
-      if (fe >> 12) {
-        R.hold >>= fe >> 12;
-        R.bits -= fe >> 12;
-        here = zs_lit_entry(fe & 0x1ffu, d64);
-      } else {
-        here = zs_lane_decode(R, lt, lbits);
+      // stores in bursts: every lane flushes when one holds 64 unstored bytes
+      if (__builtin_amdgcn_ballot_w64(W.P - W.F >= 64u)) {
+#if ZS_IL_EXP & 64
+        IL_T(tf);
+#endif
+        W.flush();
+#if ZS_IL_EXP & 64
+        IL_ACC(2, tf);
+#endif
       }
+      if (R.bits < 32) zs_lr_fill(R);
+#if ZS_IL_EXP & 64
+      st[0]++;
+      st[1] += IL_FIRST();  // wave steps (summed)
+#endif
+      uint32_t L;
+      uint32_t k = zs_canon_rank(CL, R, L);
+      if (L > 15) { bail = true; break; }  // "invalid literal/length code"
+      zs_lr_drop(R, L);
+      const uint32_t sym = F.lsym[k] | (((F.lhi[k >> 5] >> (k & 31u)) & 1u) << 8);
+      if (sym >= 286) { bail = true; break; }  // fixed codes 286/287: "invalid literal/length code"
+      zcode here = zs_lit_entry(sym, d64);
       uint32_t op = C_OP(here);
       if (op == 0) {
         if (total >= cap) { bail = true; break; }
@@ -387,93 +468,75 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (op & 64) { bail = true; break; }  // "invalid literal/length code"
       uint32_t len = C_VAL(here) + zs_lr_take(R, op & lmask);
       if (R.bits < 32) zs_lr_fill(R);
-      const uint32_t de = F.dist[(uint32_t)R.hold & ((1u << ZS_DROOT) - 1)];
-      if (de >> 12) {
-        R.hold >>= de >> 12;
-        R.bits -= de >> 12;
-        here = zs_dist_entry(de & 0x1fu, d64);
-      } else {
-        here = zs_lane_decode(R, dt, dbits);
-      }
+      k = zs_canon_rank(CD, R, L);
+      if (L > 15) { bail = true; break; }  // "invalid distance code"
+      zs_lr_drop(R, L);
+      const uint32_t dsym = F.dsym[k];
+      if (!d64 && dsym >= 30) { bail = true; break; }  // fixed codes 30/31 likewise
+      here = zs_dist_entry(dsym, d64);
       op = C_OP(here);
-      if (op & 64) { bail = true; break; }  // "invalid distance code"
       const uint32_t dist = C_VAL(here) + zs_lr_take(R, op & 15u);
       if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
-      const uint8_t* from = dst + total - dist;
-      uint8_t* to = dst + total;
-      const uint32_t fsh = (uint32_t)((uintptr_t)from & 3u);
-      const uint32_t* fw = reinterpret_cast<const uint32_t*>(from - fsh);
-      if (dist >= 16u + (W.P & 15u)) {
-        // every source byte of every 16-byte round lies below the unit being
-        // combined, so is in memory already: 16 bytes per round trip, into the
-        // write combiner a word at a time
+      const uint32_t src = W.P - dist;
+#if ZS_IL_EXP & 64
+      IL_T(tc);
+#endif
+      if (dist > ZS_RING_SRC) {
+        // older than the ring: in HBM (room() keeps P - F <= 108 before every
+        // round, so the round's source lies below F), 16 bytes per round trip;
+        // aligned words funnel-shifted into place
+        const uint32_t fsh = src & 3u;
+        const uint32_t* fw = W.base + (src >> 2);
         for (uint32_t i = 0; i < len; i += 16) {
-          uint32_t x[5];
+          W.room();
+          uint32_t x[5], w[4];
 #pragma unroll
-          for (int k = 0; k < 5; k++) x[k] = fw[(i >> 2) + (uint32_t)k];
-          const uint32_t rem = len - i;
+          for (int k = 0; k < 5; k++) x[k] = IL_LD(fw[(i >> 2) + (uint32_t)k]);
 #pragma unroll
-          for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t wd = __builtin_amdgcn_alignbyte(x[k + 1], x[k], fsh);
-            if (rem >= 4u * k + 4u) {
-              W.put(wd, 4u);
-            } else if (rem > 4u * k) {
-              const uint32_t nb = rem - 4u * k;
-              W.put(wd & ((1u << (8u * nb)) - 1u), nb);
-            }
-          }
+          for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], fsh);
+          W.put16(w, min(16u, len - i));
         }
-        total += len;
-        continue;
-      }
-      // a source within the unit being combined: its bytes go to memory, the
-      // copy stores bytes straight to memory, and the combiner picks the unit up
-      W.spill();
-      // A copy waits for its source bytes once per chunk (loads after the
-      // stores of the chunk before), so the chunk is as wide as the distance
-      // allows.  Source words are aligned loads funnel-shifted into place; a
-      // word that is read always holds at least one byte of the output region
-      // (so never leaves its pages), and only bytes below `to` are used.
-      if (dist >= 16) {  // 16 bytes per round trip
+#if ZS_IL_EXP & 64
+        IL_ACC(3, tc);
+#endif
+      } else if (dist >= 16) {  // from the ring, 16 bytes a round
         for (uint32_t i = 0; i < len; i += 16) {
-          uint32_t x[5];
-#pragma unroll
-          for (int k = 0; k < 5; k++) x[k] = fw[(i >> 2) + (uint32_t)k];
-#pragma unroll
-          for (uint32_t j = 0; j < 16; j++) {
-            const uint32_t wd = __builtin_amdgcn_alignbyte(x[(j >> 2) + 1], x[j >> 2], fsh);
-            if (i + j < len) to[i + j] = (uint8_t)(wd >> (8 * (j & 3)));
-          }
+          W.room();
+          W.sync();
+          uint32_t w[4];
+          W.ring16(src + i, w);
+          W.put16(w, min(16u, len - i));
         }
-      } else if (dist >= 8) {  // 8 independent loads, then 8 stores: one memory round trip per 8 bytes
-        for (uint32_t i = 0; i < len; i += 8) {
-          uint8_t b[8];
-#pragma unroll
-          for (int k = 0; k < 8; k++) b[k] = i + k < len ? from[i + k] : 0;
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            if (i + k < len) to[i + k] = b[k];
-        }
+#if ZS_IL_EXP & 64
+        IL_ACC(4, tc);
+#endif
       } else {
-        // overlapping copy, period dist < 8: the dist bytes before `to` are
-        // read once (three words, clamped to the last written one) and the
-        // run is stored from registers -- not a round trip per byte
-        const uint32_t last = (uint32_t)((to - 1) - (from - fsh)) >> 2;
-        const uint32_t x0 = fw[0], x1 = fw[min(1u, last)], x2 = fw[min(2u, last)];
-        const uint32_t p0 = __builtin_amdgcn_alignbyte(x1, x0, fsh), p1 = __builtin_amdgcn_alignbyte(x2, x1, fsh);
-        uint32_t j = 0;
-        for (uint32_t i = 0; i < len; i++) {
-          to[i] = (uint8_t)((j < 4 ? p0 >> (8 * j) : p1 >> (8 * (j - 4))) & 0xffu);
-          j = j + 1 == dist ? 0u : j + 1;
+        // overlapping (period dist < 16): a round copies the md bytes before P,
+        // md a multiple of dist that doubles up to the largest one within 16
+        const uint32_t mmax = (uint32_t)((0xedcba98fdbefeffull >> (4u * (dist - 1u))) & 15u) + 1u;
+        uint32_t md = dist;
+        for (uint32_t i = 0; i < len;) {
+          W.room();
+          W.sync();
+          uint32_t w[4];
+          W.ring16(W.P - md, w);
+          const uint32_t n = min(md, len - i);
+          W.put16(w, n);
+          i += n;
+          md = min(2u * md, mmax);
         }
+#if ZS_IL_EXP & 64
+        IL_ACC(5, tc);
+#endif
       }
       total += len;
-      W.P += len;
-      W.reload();
     }
     if (zs_lr_over(R)) bail = true;
+#if ZS_IL_EXP & 64
+    { const unsigned long long t = clock64(); st[6] += t - tk; tk = t; }
+#endif
   }
-  if (!bail) W.spill();  // the last unit's bytes
+  if (!bail) W.finish();  // the last unit's bytes
   // ---- trailer (inflate.ts:1006-1036)
   if (!bail && wrap) {
     zs_lr_align(R);
@@ -494,6 +557,17 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   }
   res[s] = r;
   lens_out[s] = r.out_len;  // for the checksum pass over the decoded bytes
+#if ZS_IL_EXP & 64
+  st[7] = clock64() - tk0;
+  for (int i = 0; i < 8; i++) {
+    unsigned long long v = st[i];
+    for (int o = 32; o; o >>= 1) {
+      const unsigned long long w = __shfl_xor(v, o);
+      v = (i >= 1 && i <= 5) ? v + w : w > v ? w : v;
+    }
+    if ((threadIdx.x & 63u) == 0) atomicAdd(&zs_il_stat[i], v);
+  }
+#endif
 }
 
 size_t zs_inflate_lane_scratch_bytes() { return sizeof(zs_lane_tabs); }
