@@ -210,7 +210,9 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * "lane_block" (default 0 = by batch size;
  * else 1..64, a power of two): members per workgroup of the inflate lane path;
  * "inflate_wave_min" (default 32768; 0 = never): members with more input bytes
- * decode one per wave (inflate_wave.hip) beside the lane kernel;
+ * decode one per wave (inflate_wave.hip) beside the lane kernel, in every
+ * format (the wave kernel tracks the reference's inflate() calls, so it
+ * reproduces the window-wrap copy below);
  * "parse_waves" (default 0 = two below 2048 streams, else one; 1, 2 or 4):
  * waves per stream of the levels 4..9 lazy parse (two: 512-position segments,
  * two rounds' speculative passes at once);

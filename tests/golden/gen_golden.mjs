@@ -179,6 +179,11 @@ const BATCH = {
   t256_l1_raw: { gen: text, n: 262144, count: 4096, level: 1, format: "deflate-raw" },
   t256_l9_raw: { gen: text, n: 262144, count: 4096, level: 9, format: "deflate-raw" },
   t64_l6_gzip: { gen: text, n: 65536, count: 8192, level: 6, format: "gzip" },
+  t256_l6_raw: { gen: text, n: 262144, count: 4096, level: 6, format: "deflate-raw" },
+  // the same streams decoded back by the reference's DecompressionStream: the
+  // stream layer's call boundaries make its window-wrap copy (inffast.ts:133-147)
+  // emit bytes that are not the source for some of them
+  t256_l6_raw_dec: { gen: text, n: 262144, count: 4096, level: 6, format: "deflate-raw", decode: true },
 };
 
 function genBatchPart(setName, K, P) {
@@ -186,7 +191,12 @@ function genBatchPart(setName, K, P) {
   const lo = Math.floor((set.count * P) / K), hi = Math.floor((set.count * (P + 1)) / K);
   const rec = Buffer.alloc((hi - lo) * 20);
   for (let i = lo; i < hi; i++) {
-    const out = compress(set.format, set.level, set.gen(streamSeed(i), set.n));
+    let out = compress(set.format, set.level, set.gen(streamSeed(i), set.n));
+    if (set.decode) {
+      const d = decompress(set.format, out);
+      if (!d.ok) throw new Error("reference decode failed: " + d.err);
+      out = d.out;
+    }
     rec.writeUInt32LE(out.length, (i - lo) * 20);
     crypto.createHash("sha256").update(out).digest().copy(rec, (i - lo) * 20 + 4, 0, 16);
   }

@@ -212,3 +212,37 @@ def test_c5_gunzip_all_8192_members_with_crc(engine):
     chk = [c & 0xffffffff for c in d_chk.tolist()]
     assert chk == [zlib.crc32(s) for s in src]
     assert d_cons.tolist() == [len(m) for m in gz]
+
+
+def test_large_members_decode_as_the_reference(engine):
+    """4,096 T-corpus 256 KiB streams at deflate-raw L6 (compressed here and
+    checked against the reference's compress golden) decoded with default
+    options, as DecompressionStream decodes them: ~100 KB of input each, so
+    every member goes through the wave kernel (inflate_wave.hip), which tracks
+    the reference's inflate() calls (32 KiB input sub-chunks, 64 KiB output
+    buffers, streams.ts:78-93) and reproduces the window-wrap copy of
+    inffast.ts:127-147.  Bytes = tests/golden/batch_t256_l6_raw_dec.bin (the
+    reference's own decode; it differs from the source for some members);
+    no member falls back to the exact kernel; the exact kernel agrees on the
+    members the copy changes."""
+    import zsamd
+
+    L, N = 262144, 4096
+    buf = bytes(zsamd.corpus("text", 0, N, L))
+    srcs = [buf[i * L:(i + 1) * L] for i in range(N)]
+    comps = engine.compress_batch(srcs, "deflate-raw", 6)
+    recs = golden_io.batch("t256_l6_raw")
+    assert all((len(c), hashlib.sha256(c).digest()[:16]) == recs[i] for i, c in enumerate(comps))
+    assert min(len(c) for c in comps) > 32768
+    outs = engine.decompress_batch(comps, "deflate-raw", [L] * N)
+    assert engine.last_lane_count() == N
+    drecs = golden_io.batch("t256_l6_raw_dec")
+    assert all((len(o), hashlib.sha256(o).digest()[:16]) == drecs[i] for i, o in enumerate(outs))
+    changed = [i for i in range(N) if outs[i] != srcs[i]]
+    assert changed  # the set exercises the window-wrap copy
+    try:
+        engine.set_option("inflate_wave_min", 0)  # the exact kernel
+        exact = engine.decompress_batch([comps[i] for i in changed], "deflate-raw", [L] * len(changed))
+    finally:
+        engine.set_option("inflate_wave_min", 32768)
+    assert all(exact[k] == outs[i] for k, i in enumerate(changed))

@@ -1,14 +1,21 @@
 """Summarize a tools/profile.sh directory into profiles/<round>/summary.json:
 per kernel: calls, average duration (kernel trace), FETCH_SIZE / WRITE_SIZE
 (KiB per dispatch as rocprofv3 reports them) and the HBM bytes per launch.
-gfx950 FETCH_SIZE counts half of the bytes of wide coalesced reads
-(MI355X_MICROARCH.md, HBM): hbm_bytes_corrected doubles the read side."""
+gfx950 FETCH_SIZE counts half of the bytes of wide coalesced reads (16 B per
+lane; MI355X_MICROARCH.md, HBM), and other widths are uncalibrated: the read
+side is doubled only for the kernels whose reads are of that kind (WIDE_READ);
+hbm_bytes_corrected is the raw sum for every other kernel, and each entry says
+which it got ("fetch_correction")."""
 import collections, csv, json, os, re, sys
 
 
 def kname(name):  # "void zs_k_fast<2>(...)" -> "zs_k_fast"
     return re.sub(r"<[^>]*>", "", name.split("(")[0].replace("void ", "")).strip()
 
+
+# kernels whose dominant reads are 16-byte-per-lane coalesced loads of the input
+# (deflate_match.hip zs_k_match, deflate_sweep.hip zs_k_sweep window loads)
+WIDE_READ = {"zs_k_match", "zs_k_sweep"}
 
 src, dst = sys.argv[1], sys.argv[2]
 stats = {}
@@ -32,7 +39,9 @@ for k, v in stats.items():
         e["write_kib"] = sum(w) / len(w)
     if f and w:
         e["hbm_bytes_raw"] = (e["fetch_kib"] + e["write_kib"]) * 1024
-        e["hbm_bytes_corrected"] = (2 * e["fetch_kib"] + e["write_kib"]) * 1024
+        wide = k in WIDE_READ
+        e["fetch_correction"] = "x2 (16-B coalesced reads)" if wide else "none (narrow reads: uncalibrated, raw)"
+        e["hbm_bytes_corrected"] = ((2 if wide else 1) * e["fetch_kib"] + e["write_kib"]) * 1024
     out[k] = e
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'zlib-streams-ts_amd'))
 import zsamd  # noqa: E402
@@ -40,6 +49,6 @@ import zsamd  # noqa: E402
 out['_build_id'] = zsamd.build_id()  # the build these counters belong to
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
-for k, e in sorted(out.items(), key=lambda kv: -kv[1]["total_ns"]):
+for k, e in sorted(((k, e) for k, e in out.items() if not k.startswith("_")), key=lambda kv: -kv[1]["total_ns"]):
     print("%-32s calls %3d avg %10.3f ms  hbm(raw) %s" % (k[:32], e["calls"], e["avg_ns"] / 1e6,
                                                         "%.1f MB" % (e["hbm_bytes_raw"] / 1e6) if "hbm_bytes_raw" in e else "-"))

@@ -947,12 +947,12 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
     HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate_lane, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm));
     // Large members (more than inflate_wave_min input bytes) decode one per wave
     // on the side stream, beside the lane kernel: one lane would take the
-    // batch's whole time on such a member.  Only where the lane path's
-    // straight-through decode is the reference's (deflate64, or no window-wrap
-    // reproduction); the lane kernel skips exactly these members.
+    // batch's whole time on such a member.  The wave kernel tracks the
+    // reference's inflate() calls and reproduces their window-wrap copy
+    // (inflate_wave.hip, zs_refcalls); the lane kernel skips exactly these members.
     uint32_t wave_min = 0;
     c->hwlist.clear();
-    if (c->inflate_wave_min && (wbits == -16 || !c->inflate_ref_wrap)) {
+    if (c->inflate_wave_min) {
       for (uint32_t i = 0; i < n; i++)
         if (in_len[i] > c->inflate_wave_min) c->hwlist.push_back(i);
       if (!c->hwlist.empty()) wave_min = c->inflate_wave_min;
@@ -963,11 +963,18 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       HIPCHK(hipMemcpyAsync(c->wlist.p, c->hwlist.data(), 4ull * nw, hipMemcpyHostToDevice, st));
       HIPCHK(hipEventRecord(c->fork, st));
       HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
-      const size_t wsm = zs_inflate_wave_lds_bytes();
-      HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wsm));
+      const size_t wsm = zs_inflate_wave_lds_bytes(wbits == -16);
+      // deflate64 never runs inflate_fast in the reference: no window-wrap copy to reproduce
+      const bool refw = c->inflate_ref_wrap && wbits != -16;
+      const void* wk = refw ? (const void*)zs_k_inflate_wave<true> : (const void*)zs_k_inflate_wave<false>;
+      HIPCHK(hipFuncSetAttribute(wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wsm));
       if (int r = mark(c, c->side, "start")) return r;
-      zs_k_inflate_wave<<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
-                                                  c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
+      if (refw)
+        zs_k_inflate_wave<true><<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
+                                                          c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
+      else
+        zs_k_inflate_wave<false><<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
+                                                           c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
       HIPCHK(hipGetLastError());
       if (int r = mark(c, c->side, "inflate_wave")) return r;
       HIPCHK(hipEventRecord(c->join, c->side));

@@ -29,26 +29,28 @@
 #include "zs_inflate.h"
 #include "zs_inftab.h"
 
-#define ZS_WRING (1u << 16)  // history ring: the deflate64 window (deflate's 32 KiB fits)
-#define ZS_WMASK (ZS_WRING - 1u)
-
-struct zs_wave_lds {
-  uint8_t ring[ZS_WRING];
-  uint32_t inw[1024];  // ZS_WIN_IN staged input words
+// history ring: the window (32 KiB; deflate64 64 KiB), at the start of the
+// dynamic LDS; then the staged input and zlib's tables.  Deflate: 40,792 B, four
+// workgroups per CU; deflate64: 73,560 B, two.
+#ifndef ZS_WIN_IN
+#define ZS_WIN_IN 256u  // staged input words
+#endif
+struct zs_wave_tabs {
+  uint32_t inw[ZS_WIN_IN];
   zcode codes[ENOUGH_LENS + ENOUGH_DISTS_9];
   uint16_t lens[320];
   uint16_t work[288];
 };
+static __host__ __device__ inline uint32_t zs_wave_ring_bytes(bool d64) { return d64 ? 65536u : 32768u; }
 
 static __device__ __forceinline__ uint32_t zs_u(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // wave-uniform bit reader: the zs_lane_reader scheme (clamped aligned words,
 // one refill ahead) with every value in SGPRs.  The input words are staged in
-// LDS, 4 KiB at a time by the whole wave: a refill is then an LDS read, which
+// LDS, 1 KiB at a time by the whole wave: a refill is then an LDS read, which
 // the table lookups' waits cover, where a direct load would wait behind the
 // output stores (vmcnt) or -- as a scalar load -- make every table lookup's
 // lgkmcnt wait for it.
-#define ZS_WIN_IN 1024u  // staged input words
 struct zs_wave_reader {
   const uint32_t* w4;  // the aligned words holding the member's bytes
   uint32_t* inw;       // LDS: words [qb, qb + ZS_WIN_IN) of w4 (clamped to `last`)
@@ -115,6 +117,135 @@ static __device__ __forceinline__ zcode zs_wr_decode(zs_wave_reader& R, const zc
   return here;
 }
 
+// The reference's inflate() calls, for a deflate / zlib / gzip member decoded
+// straight through here (wave-uniform bookkeeping, no data).  The stream layer
+// (streams.ts:78-93) gives each call the input left in one 32 KiB sub-chunk and
+// a fresh 64 KiB output buffer; a call ends when the sub-chunk runs out (the
+// symbol whose bits cross its end is finished by the next call's slow path) or
+// the buffer is full.  inf_leave's updatewindow (inflate.ts:282-322,1059-1073)
+// then appends the call's output to the 32 KiB window (w_next, w_have).
+// inflate_fast runs a symbol iff the LEN state found >= 6 unread input bytes and
+// >= 258 bytes of buffer left (inflate.ts LEN), or the fast loop went on after
+// the previous symbol (inffast.ts:24, inIndex < last && outIndex < end, its
+// byte refills simulated bit-exactly).  Only inflate_fast has the window-wrap
+// copy (inffast.ts:127-147): when the window part of a copy wraps past
+// window[w_next] and the rest (at most w_next bytes) would come from
+// window[0..], the reference copies output[0..] -- the CURRENT call's buffer,
+// i.e. the call's first bytes -- instead.  wrap() says whether a copy does that.
+struct zs_refcalls {
+  uint32_t B;       // output position where the current call began
+  uint32_t wn, wh;  // w_next, w_have when it began
+  uint32_t cend;    // input byte where the current sub-chunk ends
+  uint32_t fast;    // inside inflate_fast
+  uint32_t fin, fbits;  // inflate_fast's pulled bytes (member offset) and bit count
+  __device__ __forceinline__ void init() {
+    B = 0;
+    wn = 0;
+    wh = 0;
+    cend = 32768u;
+    fast = 0;
+  }
+  __device__ __forceinline__ void end_call(uint32_t at) {
+    const uint32_t produced = at - B;
+    if (produced >= 32768u) {
+      wn = 0;
+      wh = 32768u;
+    } else if (produced) {
+      const uint32_t d = min(32768u - wn, produced), rest = produced - d;
+      if (rest) {
+        wn = rest;
+        wh = 32768u;
+      } else {
+        wn += d;
+        if (wn == 32768u) wn = 0;
+        wh = min(wh + d, 32768u);
+      }
+    }
+    B = at;
+    fast = 0;
+  }
+  __device__ __forceinline__ void pull(uint32_t need) {
+    while (fbits < need) {
+      fin++;
+      fbits += 8u;
+    }
+  }
+  // a symbol with bits [sb, sb + l1 + e1 + l2 + e2) writing len bytes at o;
+  // true iff inflate_fast runs it whole
+  __device__ __forceinline__ bool symbol(uint64_t sb, uint32_t o, uint32_t len, uint32_t l1, uint32_t e1,
+                                         uint32_t l2, uint32_t e2, bool eob) {
+    if (o > B + 65536u) end_call(B + 65536u);  // the copy before filled the buffer
+    while (sb >= 8ull * cend) {  // sub-chunks that ended before the symbol
+      end_call(o);
+      cend += 32768u;
+    }
+    if (sb + l1 + e1 + l2 + e2 > 8ull * cend) {  // crosses the sub-chunk's end: the next call's slow path
+      end_call(o);
+      cend += 32768u;
+      return false;
+    }
+    if (o >= B + 65536u) {  // the buffer is full: the next call's slow path writes it
+      end_call(B + 65536u);
+      return false;
+    }
+    if (!fast) {  // the LEN state (inflate.ts): have >= 6 && left >= 258
+      const uint32_t pulled = (uint32_t)((sb + 7u) >> 3);
+      if (cend - pulled >= 6u && B + 65536u - o >= 258u) {
+        fast = 1;
+        fin = pulled;
+        fbits = (uint32_t)(8ull * pulled - sb);
+      } else {
+        return false;
+      }
+    }
+    pull(15u);
+    fbits -= l1;
+    if (eob) {
+      fast = 0;
+      return true;
+    }
+    if (len > 1u || l2) {  // a length / distance pair
+      pull(e1);
+      fbits -= e1;
+      pull(15u);
+      fbits -= l2;
+      pull(e2);
+      fbits -= e2;
+    }
+    if (!(fin < cend - 5u && o + len < B + 65536u - 257u)) fast = 0;  // the fast loop's condition
+    return true;
+  }
+  // a stored block's len bytes at input byte in, output o (the COPY state: the slow path)
+  __device__ __forceinline__ void stored(uint32_t in, uint32_t o, uint32_t len) {
+    if (o > B + 65536u) end_call(B + 65536u);
+    while (len) {
+      while (in >= cend) {
+        end_call(o);
+        cend += 32768u;
+      }
+      if (o >= B + 65536u) end_call(B + 65536u);
+      const uint32_t take = min(len, min(cend - in, B + 65536u - o));
+      in += take;
+      o += take;
+      len -= take;
+    }
+  }
+  // the window-wrap copy (inffast.ts:127-147) for a copy inflate_fast runs: the
+  // number of bytes (at the copy's end) that come from the call's first output
+  // bytes instead of the window, 0 if none
+  __device__ __forceinline__ uint32_t wrap(uint32_t o, uint32_t len, uint32_t dist) const {
+    if (dist <= o - B || wn == 0) return 0;
+    const uint32_t op2 = dist - (o - B);
+    if (wn >= op2) return 0;
+    const uint32_t op3 = op2 - wn;
+    return (op3 < len && wn >= len - op3) ? len - op3 : 0u;
+  }
+};
+
+// REFW: a deflate / zlib / gzip member with the reference's window-wrap copy
+// reproduced (flags & ZS_INF_REF_WRAP); the other instance (deflate64, or
+// inflate_ref_wrap = 0) carries no call bookkeeping.
+template <bool REFW>
 __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off,
                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -122,8 +253,11 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
                                                         const uint32_t* __restrict__ out_cap, int wbits,
                                                         const uint32_t* __restrict__ list, uint32_t n_list,
                                                         zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out) {
-  extern __shared__ uint8_t zs_wsm[];
-  zs_wave_lds& W = *reinterpret_cast<zs_wave_lds*>(zs_wsm);
+  extern __shared__ __attribute__((aligned(16))) uint8_t zs_wsm[];
+  const bool d64 = wbits == -16;
+  uint8_t* ring = zs_wsm;
+  const uint32_t rmask = zs_wave_ring_bytes(d64) - 1u;
+  zs_wave_tabs& W = *reinterpret_cast<zs_wave_tabs*>(zs_wsm + zs_wave_ring_bytes(d64));
   if (blockIdx.x >= n_list) return;
   const uint32_t lane = threadIdx.x;
   const uint32_t s = zs_u(list[blockIdx.x]);
@@ -140,13 +274,25 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
   R.bits = 0;
   R.pf = zs_wr_load4(R, 0);
   uint8_t* dst = out + out_off[s];
+  uint32_t* dstw = reinterpret_cast<uint32_t*>(dst);  // out_off is 4-aligned
+  const uint32_t* ringw = reinterpret_cast<const uint32_t*>(ring);
   const uint32_t cap = zs_u(out_cap[s]);
-  const bool d64 = wbits == -16;
   const uint32_t lmask = d64 ? 31u : 15u;  // length extra-bit mask (inflate.ts:891)
   const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
-  uint32_t total = 0;
+  // the reference's call boundaries matter for deflate / zlib / gzip (deflate64 never runs inflate_fast)
+  constexpr bool refw = REFW;
+  zs_refcalls C;
+  C.init();
+  uint32_t total = 0, flushed = 0;
   zs_lane_res r = {1u, 0u, 0u, 0u};
   bool bail = false;
+  // output leaves the ring 256 bytes (one dword per lane) at a time
+  auto flush = [&]() {
+    while (total - flushed >= 256u) {
+      dstw[(flushed >> 2) + lane] = ringw[((flushed & rmask) >> 2) + lane];
+      flushed += 256u;
+    }
+  };
   // ---- wrapper header (inflate.ts:377-580): plain zlib / gzip headers only, as the lane path
   if (wrap) {
     const uint32_t b0 = zs_wr_take(R, 8), b1 = zs_wr_take(R, 8);
@@ -171,15 +317,13 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
       const uint32_t len = zs_wr_take(R, 16), nlen = zs_wr_take(R, 16);
       const uint32_t at = (uint32_t)(zs_wr_bitpos(R) >> 3);
       if (len != (nlen ^ 0xffffu) || zs_wr_over(R) || at + len > R.n || total + len > cap) { bail = true; break; }
+      if (refw) C.stored(at, total, len);
       for (uint32_t i = 0; i < len; i += 64) {
         const uint32_t k = i + lane;
-        if (k < len) {
-          const uint8_t b = src[at + k];
-          W.ring[(total + k) & ZS_WMASK] = b;
-          dst[total + k] = b;
-        }
+        if (k < len) ring[(total + lane) & rmask] = src[at + k];
+        total += min(64u, len - i);
+        flush();
       }
-      total += len;
       zs_wr_seek(R, at + len);
       continue;
     }
@@ -237,53 +381,68 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
     dbits = zs_u(dbits);
     const zcode* lt = W.codes;
     const zcode* dt = W.codes + zs_u(lused);
-    // symbols (inffast.ts:5-228 semantics, without the call boundaries)
+    // symbols (inffast.ts:5-228 semantics; the reference's call boundaries tracked by C)
     for (;;) {
+      const uint64_t b0 = zs_wr_bitpos(R);
       zcode here = zs_wr_decode(R, lt, lbits);
       uint32_t op = C_OP(here);
       if (op == 0) {
         if (total >= cap) { bail = true; break; }
-        if (lane == 0) {
-          const uint8_t b = (uint8_t)C_VAL(here);
-          W.ring[total & ZS_WMASK] = b;
-          dst[total] = b;
-        }
+        if (refw) C.symbol(b0, total, 1u, (uint32_t)(zs_wr_bitpos(R) - b0), 0u, 0u, 0u, false);
+        if (lane == 0) ring[total & rmask] = (uint8_t)C_VAL(here);
         total++;
+        flush();
         continue;
       }
-      if (op & 32) break;                   // end of block
+      if (op & 32) {  // end of block
+        if (refw) C.symbol(b0, total, 0u, (uint32_t)(zs_wr_bitpos(R) - b0), 0u, 0u, 0u, true);
+        break;
+      }
       if (op & 64) { bail = true; break; }  // "invalid literal/length code"
+      const uint64_t b1 = zs_wr_bitpos(R);
       const uint32_t len = C_VAL(here) + zs_wr_take(R, op & lmask);
+      const uint64_t b2 = zs_wr_bitpos(R);
       here = zs_wr_decode(R, dt, dbits);
       op = C_OP(here);
       if (op & 64) { bail = true; break; }  // "invalid distance code"
+      const uint64_t b3 = zs_wr_bitpos(R);
       const uint32_t dist = C_VAL(here) + zs_wr_take(R, op & 15u);
       if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
-      if (dist >= 64 || dist >= len) {
+      uint32_t tail = 0;  // bytes the reference takes from its call's first output bytes
+      if (refw && C.symbol(b0, total, len, (uint32_t)(b1 - b0), (uint32_t)(b2 - b1), (uint32_t)(b3 - b2),
+                           (uint32_t)(zs_wr_bitpos(R) - b3), false))
+        tail = C.wrap(total, len, dist);
+      const uint32_t head = len - tail;
+      if (dist >= 64 || dist >= head) {
         // a step's sources lie at least 64 bytes back, i.e. before the step
-        for (uint32_t i = 0; i < len; i += 64) {
+        for (uint32_t i = 0; i < head; i += 64) {
           const uint32_t k = i + lane;
-          if (k < len) {
-            const uint8_t b = W.ring[(total - dist + k) & ZS_WMASK];
-            W.ring[(total + k) & ZS_WMASK] = b;
-            dst[total + k] = b;
-          }
+          if (k < head) ring[(total + k) & rmask] = ring[(total - dist + k) & rmask];
         }
       } else {
         // period dist < 64: lane k < step (a multiple of dist) always stores
         // the byte dist - k % dist before the copy
         const uint32_t per = 64u / dist, step = per * dist;
         const uint32_t m = lane - (lane / dist) * dist;
-        const uint8_t b = W.ring[(total - dist + m) & ZS_WMASK];
-        for (uint32_t i = 0; i < len; i += step) {
+        const uint8_t b = ring[(total - dist + m) & rmask];
+        for (uint32_t i = 0; i < head; i += step) {
           const uint32_t k = i + lane;
-          if (lane < step && k < len) {
-            W.ring[(total + k) & ZS_WMASK] = b;
-            dst[total + k] = b;
+          if (lane < step && k < head) ring[(total + k) & rmask] = b;
+        }
+      }
+      if (tail) {
+        // the window-wrap copy: output[0..tail) of the current call, one byte
+        // at a time (it may overlap the bytes it writes); bytes older than the
+        // ring are in HBM already (flushed <= 256 bytes behind)
+        if (lane == 0) {
+          for (uint32_t i = 0; i < tail; i++) {
+            const uint32_t x = C.B + i, t = total + head + i;
+            ring[t & rmask] = x + rmask + 1u >= t + 1u ? ring[x & rmask] : dst[x];
           }
         }
       }
       total += len;
+      flush();
     }
     if (zs_wr_over(R)) bail = true;
   }
@@ -301,6 +460,9 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
     if (zs_wr_over(R)) bail = true;
   }
   if (!bail) {
+    // the last bytes: whole words (the last one's bytes past total are inside the capacity)
+    const uint32_t wend = (total + 3u) >> 2;
+    for (uint32_t w = (flushed >> 2) + lane; w < wend; w += 64) dstw[w] = ringw[(w & (rmask >> 2))];
     r.bail = 0;
     r.out_len = total;
     r.consumed = (uint32_t)((zs_wr_bitpos(R) + 7u) >> 3);
@@ -311,4 +473,11 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
   }
 }
 
-size_t zs_inflate_wave_lds_bytes() { return sizeof(zs_wave_lds); }
+size_t zs_inflate_wave_lds_bytes(bool d64) { return zs_wave_ring_bytes(d64) + sizeof(zs_wave_tabs); }
+
+template __global__ void zs_k_inflate_wave<false>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
+                                                  const uint64_t*, const uint32_t*, int, const uint32_t*, uint32_t,
+                                                  zs_lane_res*, uint32_t*);
+template __global__ void zs_k_inflate_wave<true>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
+                                                 const uint64_t*, const uint32_t*, int, const uint32_t*, uint32_t,
+                                                 zs_lane_res*, uint32_t*);

@@ -59,6 +59,7 @@ __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, con
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, uint32_t n_members,
                                   zs_lane_tabs* tabs, zs_lane_res* res, uint32_t* lens_out, int flags,
                                   uint32_t wave_min);
+template <bool REFW>
 __global__ void zs_k_inflate_wave(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, const uint32_t* list,
                                   uint32_t n_list, zs_lane_res* res, uint32_t* lens_out);
@@ -66,4 +67,4 @@ __global__ void zs_k_inflate_lane_verify(zs_lane_res* res, const uint32_t* check
 size_t zs_inflate_smem_bytes(int wbits);
 size_t zs_inflate_lane_lds_bytes();
 size_t zs_inflate_lane_scratch_bytes();
-size_t zs_inflate_wave_lds_bytes();
+size_t zs_inflate_wave_lds_bytes(bool d64);

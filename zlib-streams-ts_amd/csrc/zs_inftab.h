@@ -40,7 +40,7 @@ static __device__ __forceinline__ void zs_dbase(uint32_t i, bool d64, uint32_t& 
 
 // inflate_table (inftrees.ts:62-279).  Returns 0 ok, -1 bad code set, 1 over ENOUGH.
 // All lanes execute it on identical values (writes are duplicated, benign).
-static __device__ int zs_inflate_table(int type, const uint16_t* lens, uint32_t codes, zcode* table, uint32_t* bits_io,
+static __device__ __attribute__((unused)) int zs_inflate_table(int type, const uint16_t* lens, uint32_t codes, zcode* table, uint32_t* bits_io,
                                        uint16_t* work, bool d64, uint32_t* used_out) {
   uint32_t len, sym, min, max, root, curr, drop, used, huff, incr, fill, low, mask;
   int left;
