@@ -141,6 +141,8 @@ class Dist:
 def profile_tag(args):
     """The config name the committed profiles carry (profiles/<round>/summary_<tag>.json)."""
     if args.mode == "inflate":
+        if args.format == "deflate-raw" and args.stream_bytes == 262144:
+            return "c4_decode"  # the 4096 x 256 KiB members decoded back
         return {"gzip": "c5_gunzip", "deflate64-raw": "c5_d64"}.get(args.format, "c3")
     if args.format == "gzip":
         return "c5_gzip_l%d" % args.level

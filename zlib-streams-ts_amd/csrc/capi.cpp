@@ -932,19 +932,27 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
   if (c->inflate_fast) {
     // lane-per-member fast path; anything but a clean end of stream goes to the exact kernel.
     // A lane's decode is a dependent chain of loads, so the chip wants many
-    // waves more than full ones: below 1024 waves of 64 members (one per
-    // SIMD), members spread over more, thinner workgroups (one wave each)
-    // until 1024 waves or 8 members per wave.
+    // waves more than full ones: up to 16,384 members, thin workgroups (one
+    // wave each) until ~4096 waves; above, 1024 waves of up to 64 members.
+    // Measured (MI355X): 65,536 members want 64 per workgroup (every lane resident at
+    // once, 548 B of LDS each); 8,192 want two (C5-i 29.5 -> 23.7 ms at 8 -> 2: four
+    // waves per SIMD hide each other's waits, with little divergence inside each).
     uint32_t B = (uint32_t)c->lane_block;
-    if (!B)
-      for (B = 64; B > 8 && (n + B - 1) / B < 1024u;) B >>= 1;
+    if (!B) {
+      if (n <= 16384u)
+        for (B = 1; B < 64 && (n + B - 1) / B > 4096u;) B <<= 1;
+      else
+        for (B = 64; B > 8 && (n + B - 1) / B < 1024u;) B >>= 1;
+    }
     HIPCHK(c->ltabs.ensure(zs_inflate_lane_scratch_bytes() * (size_t)n));
     HIPCHK(c->lres.ensure(sizeof(zs_lane_res) * (size_t)n));
     HIPCHK(c->llen.ensure(8ull * n));
     lres = c->lres.as<zs_lane_res>();
-    while (B > 1 && B * zs_inflate_lane_lds_bytes() > 160u * 1024u) B >>= 1;  // one CU's LDS
-    const size_t lsm = B * zs_inflate_lane_lds_bytes();
-    HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate_lane, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm));
+    // narrow workgroups afford per-lane root tables (inflate_lane.hip)
+    const bool lroot = B <= 16;
+    const size_t lsm = B * zs_inflate_lane_lds_bytes(lroot);
+    const void* lk = lroot ? (const void*)zs_k_inflate_lane<true> : (const void*)zs_k_inflate_lane<false>;
+    HIPCHK(hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm));
     // Large members (more than inflate_wave_min input bytes) decode one per wave
     // on the side stream, beside the lane kernel: one lane would take the
     // batch's whole time on such a member.  The wave kernel tracks the
@@ -979,9 +987,14 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       if (int r = mark(c, c->side, "inflate_wave")) return r;
       HIPCHK(hipEventRecord(c->join, c->side));
     }
-    zs_k_inflate_lane<<<(n + B - 1) / B, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
-                                                    (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
-                                                    c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min);
+    if (lroot)
+      zs_k_inflate_lane<true><<<(n + B - 1) / B, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
+                                                               (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
+                                                               c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min);
+    else
+      zs_k_inflate_lane<false><<<(n + B - 1) / B, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
+                                                                (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
+                                                                c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min);
     MARK("inflate_lane");
     if (wave_min) {
       HIPCHK(hipStreamWaitEvent(st, c->join, 0));

@@ -100,6 +100,20 @@ struct zs_lane_lds {
   uint32_t cnt[16];   // codes per length, then the next free rank of each length
 };
 
+// Narrow workgroups (lane_block <= 16: batches of a few thousand members) have
+// LDS to spare: there each lane also keeps direct root tables -- 9-bit lit/len,
+// 7-bit distance, u16 entries (length << 12 | symbol), 0 = a longer code -- so
+// most codes cost one LDS read instead of the ~45-instruction compare chain;
+// with few lanes per wave the VALU work per symbol is what each SIMD's lone
+// wave waits on (C5-i: 8,192 members, eight lanes per wave).
+#define ZS_LROOT 9u
+#define ZS_DROOT 7u
+struct zs_lane_lds_root {
+  zs_lane_lds b;
+  uint16_t lroot[1u << ZS_LROOT];
+  uint16_t droot[1u << ZS_DROOT];
+};
+
 // C from lens[0..n) (the member's scratch in HBM); false unless the code is
 // complete.  zlib's inflate_table rejects over-subscribed sets and incomplete
 // ones but for a lone code of length 1 (inftrees.ts:128-139); a lane bails on
@@ -137,6 +151,25 @@ static __device__ bool zs_canon_build(zs_canon& C, uint32_t* cnt, uint8_t* sym8,
     }
   }
   return true;
+}
+
+// root[r] for every code of length <= rbits (after zs_canon_build: cnt[l] is
+// the rank past the last length-l code, and a rank k of length l has code k - D[l-1])
+static __device__ void zs_root_fill(uint16_t* root, uint32_t rbits, const zs_canon& C, const uint32_t* cnt,
+                                    const uint8_t* sym8, const uint32_t* hi) {
+  for (uint32_t k = 0; k < (1u << rbits) / 2u; k++) reinterpret_cast<uint32_t*>(root)[k] = 0;
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t l = 1; l <= ZS_LROOT; l++) {
+    if (l > rbits) break;
+    const uint32_t end = cnt[l];
+    for (; k < end; k++) {
+      const uint32_t code = k - C.D[l - 1];
+      const uint32_t r = __builtin_bitreverse32(code) >> (32u - l);  // the stream sends codes MSB first
+      const uint32_t sym = sym8[k] | (hi ? ((hi[k >> 5] >> (k & 31u)) & 1u) << 8 : 0u);
+      for (uint32_t x = r; x < (1u << rbits); x += 1u << l) root[x] = (uint16_t)((l << 12) | sym);
+    }
+  }
 }
 
 // the rank of the code at the front of the bit buffer; L = its length (16: no
@@ -294,6 +327,7 @@ extern "C" int zs_il_stats(unsigned long long* out) {
 #define IL_ACC(i, v) do { if (IL_FIRST()) st[i] += clock64() - v; } while (0)
 #endif
 
+template <bool ROOT>
 __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off,
                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -302,12 +336,15 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
                                                         zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
                                                         uint32_t* __restrict__ lens_out, int flags,
                                                         uint32_t wave_min) {
-  extern __shared__ zs_lane_lds LL[];  // blockDim.x entries
+  extern __shared__ __attribute__((aligned(16))) uint8_t LL[];  // blockDim.x lanes' tables
+  constexpr uint32_t lstride = ROOT ? sizeof(zs_lane_lds_root) : sizeof(zs_lane_lds);
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_members) return;
   if (wave_min && in_len[s] > wave_min) return;  // a large member: zs_k_inflate_wave decodes it (inflate_wave.hip)
   zs_lane_tabs& T = tabs[s];
-  zs_lane_lds& F = LL[threadIdx.x];
+  zs_lane_lds& F = *reinterpret_cast<zs_lane_lds*>(LL + threadIdx.x * lstride);
+  uint16_t* const lroot = ROOT ? reinterpret_cast<zs_lane_lds_root*>(&F)->lroot : nullptr;
+  uint16_t* const droot = ROOT ? reinterpret_cast<zs_lane_lds_root*>(&F)->droot : nullptr;
   zs_lane_reader R;
   {
     const uint8_t* src = in + in_off[s];
@@ -425,11 +462,16 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       bail = true;  // "invalid block type"
       break;
     }
-    if (!zs_canon_build(CL, F.cnt, F.lsym, F.lhi, T.lens, nlen) ||
-        !zs_canon_build(CD, F.cnt, F.dsym, nullptr, T.lens + nlen, ndist)) {
+    if (!zs_canon_build(CL, F.cnt, F.lsym, F.lhi, T.lens, nlen)) {
       bail = true;
       break;
     }
+    if (ROOT) zs_root_fill(lroot, ZS_LROOT, CL, F.cnt, F.lsym, F.lhi);
+    if (!zs_canon_build(CD, F.cnt, F.dsym, nullptr, T.lens + nlen, ndist)) {
+      bail = true;
+      break;
+    }
+    if (ROOT) zs_root_fill(droot, ZS_DROOT, CD, F.cnt, F.dsym, nullptr);
 #if ZS_IL_EXP & 64
     { const unsigned long long t = clock64(); st[5] += t - tk; tk = t; }
 #endif
@@ -450,11 +492,17 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       st[0]++;
       st[1] += IL_FIRST();  // wave steps (summed)
 #endif
-      uint32_t L;
-      uint32_t k = zs_canon_rank(CL, R, L);
-      if (L > 15) { bail = true; break; }  // "invalid literal/length code"
+      uint32_t L, k, sym;
+      const uint32_t le = ROOT ? lroot[(uint32_t)R.hold & ((1u << ZS_LROOT) - 1u)] : 0u;
+      if (le) {
+        L = le >> 12;
+        sym = le & 0x1ffu;
+      } else {
+        k = zs_canon_rank(CL, R, L);
+        if (L > 15) { bail = true; break; }  // "invalid literal/length code"
+        sym = F.lsym[k] | (((F.lhi[k >> 5] >> (k & 31u)) & 1u) << 8);
+      }
       zs_lr_drop(R, L);
-      const uint32_t sym = F.lsym[k] | (((F.lhi[k >> 5] >> (k & 31u)) & 1u) << 8);
       if (sym >= 286) { bail = true; break; }  // fixed codes 286/287: "invalid literal/length code"
       zcode here = zs_lit_entry(sym, d64);
       uint32_t op = C_OP(here);
@@ -468,10 +516,17 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (op & 64) { bail = true; break; }  // "invalid literal/length code"
       uint32_t len = C_VAL(here) + zs_lr_take(R, op & lmask);
       if (R.bits < 32) zs_lr_fill(R);
-      k = zs_canon_rank(CD, R, L);
-      if (L > 15) { bail = true; break; }  // "invalid distance code"
+      uint32_t dsym;
+      const uint32_t de = ROOT ? droot[(uint32_t)R.hold & ((1u << ZS_DROOT) - 1u)] : 0u;
+      if (de) {
+        L = de >> 12;
+        dsym = de & 0x1fu;
+      } else {
+        k = zs_canon_rank(CD, R, L);
+        if (L > 15) { bail = true; break; }  // "invalid distance code"
+        dsym = F.dsym[k];
+      }
       zs_lr_drop(R, L);
-      const uint32_t dsym = F.dsym[k];
       if (!d64 && dsym >= 30) { bail = true; break; }  // fixed codes 30/31 likewise
       here = zs_dist_entry(dsym, d64);
       op = C_OP(here);
@@ -571,5 +626,12 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
 }
 
 size_t zs_inflate_lane_scratch_bytes() { return sizeof(zs_lane_tabs); }
-size_t zs_inflate_lane_lds_bytes() { return sizeof(zs_lane_lds); }
+size_t zs_inflate_lane_lds_bytes(bool root) { return root ? sizeof(zs_lane_lds_root) : sizeof(zs_lane_lds); }
+
+#define ZS_LANE_INST(R)                                                                                              \
+  template __global__ void zs_k_inflate_lane<R>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,          \
+                                                const uint64_t*, const uint32_t*, int, uint32_t, zs_lane_tabs*,       \
+                                                zs_lane_res*, uint32_t*, int, uint32_t);
+ZS_LANE_INST(false)
+ZS_LANE_INST(true)
 

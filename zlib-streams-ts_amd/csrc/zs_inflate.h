@@ -55,6 +55,7 @@ __global__ void zs_k_inflate(const uint8_t* in, const uint64_t* in_off, const ui
                              const uint64_t* out_off, const uint32_t* out_cap, int wbits, zs_inflate_result* res,
                              const zs_lane_res* only, int flags);
 struct zs_lane_tabs;
+template <bool ROOT>
 __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, uint32_t n_members,
                                   zs_lane_tabs* tabs, zs_lane_res* res, uint32_t* lens_out, int flags,
@@ -65,6 +66,6 @@ __global__ void zs_k_inflate_wave(const uint8_t* in, const uint64_t* in_off, con
                                   uint32_t n_list, zs_lane_res* res, uint32_t* lens_out);
 __global__ void zs_k_inflate_lane_verify(zs_lane_res* res, const uint32_t* check, uint32_t n);
 size_t zs_inflate_smem_bytes(int wbits);
-size_t zs_inflate_lane_lds_bytes();
+size_t zs_inflate_lane_lds_bytes(bool root);
 size_t zs_inflate_lane_scratch_bytes();
 size_t zs_inflate_wave_lds_bytes(bool d64);
