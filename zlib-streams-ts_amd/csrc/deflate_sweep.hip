@@ -16,9 +16,15 @@
 // simply members k-1, k-2, ... of its bucket, and the t-th predecessor is the
 // t-th chain step.  zs_k_sweep gives each lane one member and sweeps t = 1,
 // 2, ... for all 64 lanes at once: lane i reads the record of member
-// k0 + i - t from a per-wave LDS ring (consecutive lanes, consecutive 16-byte
-// records: conflict-free, and no load depends on the previous step), compares
-// the 11-byte signatures with xor + ffbl, and keeps the first maximum.
+// k0 + i - t from a per-wave LDS ring (dense arrays: consecutive lanes read
+// consecutive elements, conflict-free, and no load depends on the previous
+// step), compares signatures with xor + ffbl, and keeps the first longest
+// through a group maximum (sw_body below).
+//
+// Signatures: the 11 bytes after the hashed position's first byte, with a
+// sentinel bit (SwSig<false>); for streams of 7-bit bytes (ASCII text) 8
+// bytes [X, b3..b9] where X recovers the 9 bits of b0..b2 the 15-bit hash
+// loses (SwSig<true>: bucket-mates with equal X and hash have equal b0..b2).
 //
 // Exactness (checked off the GPU by tools/emu/emu_bucket_sweep.c against a
 // direct longest_match, and on the GPU by tests/test_gpu_deflate.py):
@@ -26,20 +32,17 @@
 //     key >= hash << 16 | max(limit, 1) (non-NIL, distance <= MAX_DIST,
 //     deflate.ts:1376), the chain (t >= 2) key > hash << 16 | limit
 //     (deflate.ts:1109); a member of another bucket fails both.  Liveness is
-//     monotone in t, so a lane leaves at its first dead step.
-//   * first strictly longer match wins (deflate.ts:1100-1105): the best is the
-//     maximum of (len << 16) | (0xffff - t).  Lengths are clamped to maxc =
-//     min(258, lookahead) (deflate.ts:1068): short candidates match at most
-//     10 bytes, and a lane with maxc <= 12 re-walks its chain exactly.
-//   * a candidate whose 11 signature bytes all match (maxc > 12) is "long":
-//     its exact length needs the window.  Up to four are recorded in chain
-//     order and extended after the sweep, with the nice cut-off (nice >= 16 at
-//     levels 4..9, so no short candidate reaches it unless the stream ends
-//     first, where maxc clamps it); when one exists within the budget the
-//     result is among them (every short one is <= 10).
-//     A fifth long candidate ends the lane's sweep, and the lane re-walks its
-//     chain from the first long one (repetitive data: the first is usually a
-//     nice match).
+//     monotone in t.
+//   * first strictly longer match wins (deflate.ts:1100-1105): the maximum of
+//     a group's scores (matched bits, low bits = 7 - its place in the group)
+//     is its first longest candidate; a group's winner replaces the best only
+//     when longer.  Lengths are clamped to maxc = min(258, lookahead)
+//     (deflate.ts:1068); the last positions of a stream re-walk exactly.
+//   * a candidate whose whole signature matches is "long": the lanes holding
+//     one extend it on the spot from the stream window (nice cut-off,
+//     deflate.ts:1100-1105); long candidates beat every short one.
+//   * both budgets in one sweep: the chain >> 2 result is a snapshot of the
+//     state after step chain >> 2 (groups are cut there).
 #include <hip/hip_runtime.h>
 #include "zs_common.h"
 #include "zs_kernels.h"
