@@ -26,7 +26,13 @@ def lane_host():
     return os.path.join(HOST, "lane_host")
 
 
+def cap4(members):
+    """the C-ABI's output capacities are multiples of 4 (capi.cpp rejects others)"""
+    return [(c, max(4, cap & ~3)) for c, cap in members]
+
+
 def run(exe, members, fmt, flags=1):
+    members = cap4(members)
     data = struct.pack("<I", len(members)) + b"".join(struct.pack("<II", len(c), cap) + c for c, cap in members)
     out = subprocess.run([exe, str(W[fmt]), str(flags)], input=data, capture_output=True, check=True).stdout
     res, p = [], 0
@@ -42,6 +48,7 @@ def run(exe, members, fmt, flags=1):
 def check(exe, members, fmt, flags=1):
     """members: [(compressed, cap)]; returns the bail flags"""
     bails = []
+    members = cap4(members)
     for (c, cap), (bail, olen, cons, want, out) in zip(members, run(exe, members, fmt, flags)):
         # the trailer check runs after the lane kernel (zs_k_inflate_lane_verify):
         # a mismatch sends the member to the exact path too

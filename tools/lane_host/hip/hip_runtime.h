@@ -28,4 +28,17 @@ static inline uint32_t zs_host_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (s & 3u)));
 }
 #define __builtin_amdgcn_alignbyte(hi, lo, s) zs_host_alignbyte(hi, lo, s)
+// one lane: a ballot is the lane's own bit, LDS atomics are plain read-modify-writes
+#define __builtin_amdgcn_ballot_w64(c) ((c) ? 1ull : 0ull)
+static inline uint32_t atomicAdd(uint32_t* p, uint32_t v) {
+  const uint32_t o = *p;
+  *p = o + v;
+  return o;
+}
+static inline uint32_t atomicOr(uint32_t* p, uint32_t v) {
+  const uint32_t o = *p;
+  *p = o | v;
+  return o;
+}
+#define ZS_OPAQUE(x) ((void)0)
 typedef int hipError_t;

@@ -3,17 +3,21 @@
 // HIP names in hip/hip_runtime.h next to this file).  Test tooling: lets the CPU
 // suite check the lane decoder's logic against the oracle without a GPU.
 //
+// Both instances run on every member -- zs_k_inflate_lane<false> (canonical
+// decode only) and <true> (with the per-lane root tables) -- and must agree.
+//
 // usage: lane_host WBITS FLAGS < members > results
 //   stdin:  u32 count, then per member: u32 in_len, u32 out_cap, in_len bytes
 //   stdout: per member: u32 bail, u32 out_len, u32 consumed, u32 want, out_len bytes
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <vector>
 #include "hip/hip_runtime.h"
 zs_dim3 threadIdx, blockIdx, blockDim;
 #include "../../zlib-streams-ts_amd/csrc/inflate_lane.hip"
-zs_lane_lds LL[1];
+alignas(16) uint8_t LL[sizeof(zs_lane_lds_root)];
 
 static void rd(void* p, size_t n) {
   if (fread(p, 1, n, stdin) != n) {
@@ -36,7 +40,7 @@ int main(int argc, char** argv) {
     std::vector<uint4> ib((len + mis + 64) / 16 + 1), ob((cap + mis + 64) / 16 + 1);
     uint8_t* in = (uint8_t*)ib.data();
     rd(in + mis, len);
-    uint64_t ioff = mis, ooff = (i * 5) % 16;
+    uint64_t ioff = mis, ooff = ((i * 5) % 16) & ~3u;  // output offsets are 4-aligned (the C-ABI's contract)
     zs_lane_res r;
     uint32_t lo;
     threadIdx = {0, 0, 0};
@@ -46,7 +50,16 @@ int main(int argc, char** argv) {
     uint8_t* ob8 = (uint8_t*)ob.data();
     const size_t obn = ob.size() * sizeof(uint4);
     for (size_t k = 0; k < obn; k++) ob8[k] = 0xa5;  // guard pattern around the member's output
-    zs_k_inflate_lane(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u);
+    zs_k_inflate_lane<true>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u);
+    const std::vector<uint8_t> out_root(ob8, ob8 + obn);
+    const zs_lane_res r_root = r;
+    for (size_t k = 0; k < obn; k++) ob8[k] = 0xa5;
+    zs_k_inflate_lane<false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u);
+    if (r.bail != r_root.bail || (!r.bail && (r.out_len != r_root.out_len || r.consumed != r_root.consumed ||
+                                              memcmp(ob8 + ooff, out_root.data() + ooff, r.out_len)))) {
+      fprintf(stderr, "lane_host: member %u: root and canonical decoders differ\n", i);
+      exit(4);
+    }
     for (size_t k = 0; k < obn; k++)
       if ((k < ooff || k >= ooff + cap) && ob8[k] != 0xa5) {
         fprintf(stderr, "lane_host: member %u wrote byte %zu outside [%lu, %lu)\n", i, k, (unsigned long)ooff,

@@ -4,6 +4,9 @@
 #include "zs_common.h"
 #include "zs_inflate.h"
 #include "zs_inftab.h"
+#ifndef ZS_OPAQUE  // (the host stand-in of tools/lane_host defines it away)
+#define ZS_OPAQUE(x) asm("" : "+v"(x))
+#endif
 #ifndef ZS_IL_EXP
 #define ZS_IL_EXP 0  // experiment builds (timing only; 0 in the product): 1 no stores, 2 no copy loads, 64 counters
 #endif
@@ -182,7 +185,7 @@ static __device__ __forceinline__ uint32_t zs_canon_rank(const zs_canon& C, cons
 #pragma unroll
   for (int l = 0; l < 16; l++) {
     d[l] = C.D[l];
-    asm("" : "+v"(d[l]));
+    ZS_OPAQUE(d[l]);
   }
   uint32_t n = 1, D = d[0];
 #pragma unroll
