@@ -1,0 +1,136 @@
+"""GPU parity of the split decode of large members (inflate_split.hip): a
+member cut at its block boundaries, the pieces decoded in parallel with
+markers for the unknown history, then resolved in order.  It must produce
+exactly what the one-piece paths produce -- the wave kernel and the exact
+stream-layer kernel (inflate.ts:332-1185) -- bytes, statuses, phases and
+messages, for the reference's deflate64 fixtures (test/data, pinned by
+inflate_small.json) and for raw deflate without the window-wrap copy."""
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+import corpus
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+D64 = os.path.join(ROOT, "tests", "golden", "d64")
+
+
+def _fixtures():
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "inflate_small.json")))
+    return [(c["name"][4:], open(os.path.join(D64, c["name"][4:]), "rb").read(), c["out_len"], c["out_sha256"])
+            for c in g["cases"] if c["name"].startswith("d64_") and c.get("ok")]
+
+
+class _opts:
+    """Engine options for the duration of a block (restored to the defaults after)."""
+
+    DEFAULTS = {"inflate_split": 1, "inflate_wave_min": 32768, "inflate_ref_wrap": 1, "inflate_fast": 1}
+
+    def __init__(self, engine, **kw):
+        self.e, self.kw = engine, kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.e.set_option(k, v)
+
+    def __exit__(self, *a):
+        for k in self.kw:
+            self.e.set_option(k, self.DEFAULTS[k])
+
+
+def _decode(engine, members, fmt, caps, **kw):
+    with _opts(engine, **kw):
+        res = engine.decompress_batch_raw(members, fmt, out_caps=caps)
+        return res, engine.last_lane_count()
+
+
+def test_large_d64_fixture_splits_and_matches_golden(engine):
+    fx = {name: (d, n, h) for name, d, n, h in _fixtures()}
+    d, n, h = fx["100k_lines.deflate64"]
+    engine.set_timing(True)
+    try:
+        res, fast = _decode(engine, [d], "deflate64-raw", [n])
+        split_ms = engine.last_ms("split_resolve")
+    finally:
+        engine.set_timing(False)
+    st, ph, msg, out, cons = res[0]
+    assert st == 1 and len(out) == n and hashlib.sha256(out).hexdigest() == h
+    assert cons == len(d)
+    assert fast == 1, "the member left the split path"
+    assert split_ms >= 0, "no split phase ran"
+
+
+def test_every_d64_fixture_through_the_split_path(engine):
+    # inflate_wave_min = 1: every fixture (even the 369-byte one) is a "large" member
+    fxs = _fixtures()
+    members = [d for _, d, _, _ in fxs]
+    res, fast = _decode(engine, members, "deflate64-raw", [(n + 3) & ~3 for _, _, n, _ in fxs], inflate_wave_min=1)
+    for (name, d, n, h), (st, ph, msg, out, cons) in zip(fxs, res):
+        assert st == 1 and len(out) == n and hashlib.sha256(out).hexdigest() == h, name
+        assert cons == len(d), name
+    assert fast == len(fxs)
+
+
+def test_split_equals_wave_path_on_raw_without_window_wrap(engine):
+    """Raw deflate with inflate_ref_wrap = 0 (zlib semantics): multi-MB and
+    multi-block members at several levels decode to their source."""
+    rng = random.Random(5150)
+    srcs = []
+    for kind, n in (("text", 3 << 20), ("mixed", 1 << 20), ("text", 300000), ("zeros", 2 << 20), ("rand", 200000),
+                    ("text", 70000)):
+        srcs.append(corpus.make({"kind": kind, "n": n, "seed": rng.randrange(1 << 32)}))
+    for level in (1, 6, 9):
+        comps = engine.compress_batch(srcs, "deflate-raw", level)
+        caps = [len(s) + 64 for s in srcs]
+        res, fast = _decode(engine, comps, "deflate-raw", caps, inflate_ref_wrap=0)
+        for s, c, (st, ph, msg, out, cons) in zip(srcs, comps, res):
+            assert st == 1 and out == s and cons == len(c), (level, len(s))
+        assert fast == len(srcs), level
+        res_w, _ = _decode(engine, comps, "deflate-raw", caps, inflate_ref_wrap=0, inflate_split=0)
+        assert [r[3] for r in res_w] == [r[3] for r in res]
+
+
+def test_split_errors_match_the_exact_path(engine):
+    """Corrupted large members: whatever the pieces see, the member's outcome
+    (status, phase, message, bytes, consumed) is the exact kernel's."""
+    fx = {name: d for name, d, _, _ in _fixtures()}
+    base = fx["100k_lines.deflate64"]
+    rng = random.Random(99)
+    members = []
+    for k in range(12):
+        b = bytearray(base)
+        for _ in range(rng.choice([1, 3, 20])):
+            i = rng.randrange(len(b))
+            b[i] ^= 1 << rng.randrange(8)
+        if k % 4 == 3:
+            b = b[:rng.randrange(40000, len(b))]  # truncated
+        members.append(bytes(b))
+    members.append(bytes(rng.randrange(256) for _ in range(70000)))  # noise
+    caps = [2188890 + 1024] * len(members)
+    got, _ = _decode(engine, members, "deflate64-raw", caps)
+    want, _ = _decode(engine, members, "deflate64-raw", caps, inflate_fast=0)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, i
+
+
+def test_split_capacity_short_is_the_exact_paths_error(engine):
+    fx = {name: (d, n) for name, d, n, _ in _fixtures()}
+    d, n = fx["100k_lines.deflate64"]
+    got, _ = _decode(engine, [d], "deflate64-raw", [n // 2])
+    want, _ = _decode(engine, [d], "deflate64-raw", [n // 2], inflate_fast=0)
+    assert got == want and got[0][0] != 1
+
+
+def test_unbounded_decode_of_a_large_member(engine):
+    """decompress_batch without caps (DecompressionStream, streams.ts:132-182):
+    the first capacity guess is too small for the fixture, the retry splits."""
+    fx = {name: (d, n, h) for name, d, n, h in _fixtures()}
+    d, n, h = fx["100k_lines.deflate64"]
+    out = engine.decompress_batch([d, fx["10k_lines.deflate64"][0]], "deflate64-raw")
+    assert hashlib.sha256(out[0]).hexdigest() == h and len(out[1]) == fx["10k_lines.deflate64"][1]

@@ -17,6 +17,7 @@
 #include "zs_common.h"
 #include "zs_kernels.h"
 #include "zs_inflate.h"
+#include "zs_split.h"
 
 
 namespace {
@@ -100,6 +101,10 @@ struct zs_ctx {
   hipEvent_t fork = nullptr, join = nullptr;
   Buf wlist;
   std::vector<uint32_t> hwlist;
+  // split decode of large members (inflate_split.hip): deflate64, or raw deflate without the window-wrap copy
+  bool inflate_split = true;
+  Buf slist, sfound, spres, sscr, smem, sval;
+  std::vector<uint32_t> hslist;
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res, d_pack;
   HostBuf h_in, h_out;
@@ -250,7 +255,8 @@ void zs_ctx_destroy(zs_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (Buf* b : {&c->lstat, &c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
-                 &c->istate, &c->d_in, &c->d_out, &c->d_res, &c->d_pack, &c->wlist})
+                 &c->istate, &c->d_in, &c->d_out, &c->d_res, &c->d_pack, &c->wlist, &c->slist, &c->sfound,
+                 &c->spres, &c->sscr, &c->smem, &c->sval})
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&c->h_in, &c->h_out})
     if (b->p) (void)hipHostFree(b->p);
@@ -276,6 +282,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "fast_group")) c->fast_group = value != 0;
+  else if (!strcmp(name, "inflate_split")) c->inflate_split = value != 0;
   else if (!strcmp(name, "parse_waves")) {
     if (value < 0 || value > 4 || value == 3) return fail(ZS_STREAM_ERROR, "parse_waves must be 0, 1, 2 or 4");
     c->parse_waves = value;
@@ -960,12 +967,69 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
     // (inflate_wave.hip, zs_refcalls); the lane kernel skips exactly these members.
     uint32_t wave_min = 0;
     c->hwlist.clear();
+    c->hslist.clear();
+    // Large raw members whose decode carries no call-boundary behaviour
+    // (deflate64; raw deflate without the window-wrap copy) are cut at their
+    // block boundaries and decoded piecewise (inflate_split.hip); the rest of
+    // the large members take the wave kernel.  The pieces' u16 scratch is
+    // bounded: members past kSplitScratch take the wave kernel too.
+    const bool splittable = c->inflate_split && (wbits == -16 || (wbits == -15 && !c->inflate_ref_wrap));
+    uint32_t piece_cap = 0;
+    uint64_t val_stride = 0;  // u32 values per split member
     if (c->inflate_wave_min) {
-      for (uint32_t i = 0; i < n; i++)
-        if (in_len[i] > c->inflate_wave_min) c->hwlist.push_back(i);
-      if (!c->hwlist.empty()) wave_min = c->inflate_wave_min;
+      constexpr size_t kSplitScratch = 2ull << 30;
+      constexpr uint32_t kPieceCapMax = 4u << 20;  // values per piece
+      for (uint32_t i = 0; i < n; i++) {
+        if (in_len[i] <= c->inflate_wave_min) continue;
+        const uint32_t pc = (std::min(out_cap[i], kPieceCapMax) + 1u) & ~1u;
+        const uint32_t npc = std::max(piece_cap, pc);
+        const uint64_t nvs = std::max<uint64_t>(val_stride, (out_cap[i] + 3ull) & ~3ull);
+        if (splittable && (2ull * ZS_SPLIT_MAX * npc + 4ull * nvs) * (c->hslist.size() + 1) <= kSplitScratch) {
+          c->hslist.push_back(i);
+          piece_cap = npc;
+          val_stride = nvs;
+        } else {
+          c->hwlist.push_back(i);
+        }
+      }
+      if (!c->hwlist.empty() || !c->hslist.empty()) wave_min = c->inflate_wave_min;
     }
-    if (wave_min) {
+    if (!c->hslist.empty()) {
+      const uint32_t ns = (uint32_t)c->hslist.size();
+      HIPCHK(c->slist.ensure(4ull * ns));
+      HIPCHK(c->sfound.ensure(8ull * ZS_SPLIT_MAX * ns));
+      HIPCHK(c->spres.ensure(sizeof(zs_split_piece_res) * ZS_SPLIT_MAX * ns));
+      HIPCHK(c->sscr.ensure(2ull * ZS_SPLIT_MAX * piece_cap * ns));
+      HIPCHK(hipMemcpyAsync(c->slist.p, c->hslist.data(), 4ull * ns, hipMemcpyHostToDevice, st));
+      HIPCHK(hipEventRecord(c->fork, st));
+      HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
+      if (int r = mark(c, c->side, "start")) return r;
+      const uint32_t* sl = c->slist.as<uint32_t>();
+      uint64_t* sf = c->sfound.as<uint64_t>();
+      zs_split_piece_res* sp = c->spres.as<zs_split_piece_res>();
+      zs_k_split_find<<<ns * ZS_SPLIT_MAX, 1024, 0, c->side>>>(d_in, d_ioff, d_ilen, sl, wbits, sf);
+      if (int r = mark(c, c->side, "split_find")) return r;
+      const size_t ssm = zs_split_lds_bytes(wbits == -16);
+      HIPCHK(hipFuncSetAttribute((const void*)zs_k_split_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ssm));
+      zs_k_split_decode<<<ns * ZS_SPLIT_MAX, 64, ssm, c->side>>>(d_in, d_ioff, d_ilen, sl, wbits, sf, sp,
+                                                                  c->sscr.as<uint16_t>(), piece_cap);
+      if (int r = mark(c, c->side, "split_decode")) return r;
+      HIPCHK(c->smem.ensure(sizeof(zs_split_member) * ns));
+      HIPCHK(c->sval.ensure(4ull * val_stride * ns + 16));
+      zs_split_member* sm = c->smem.as<zs_split_member>();
+      uint32_t* sv = c->sval.as<uint32_t>();
+      zs_k_split_chain<<<(ns + 63) / 64, 64, 0, c->side>>>(d_ilen, d_ocap, sl, ns, sp, sm);
+      zs_k_split_place<<<ns * ZS_SPLIT_MAX, 256, 0, c->side>>>(sp, sm, c->sscr.as<uint16_t>(), piece_cap, sv, val_stride);
+      // the jump and write grids cover the largest member (grid-stride beyond)
+      const uint32_t gx = (uint32_t)std::min<uint64_t>(1024, (val_stride + 1023) / 1024);
+      for (int k = 0; k < 6; k++) zs_k_split_jump<<<dim3(gx, ns), 256, 0, c->side>>>(sm, sv, val_stride);
+      zs_k_split_write<<<dim3(gx, ns), 256, 0, c->side>>>(sl, sm, sv, val_stride, d_out, d_ooff);
+      zs_k_split_final<<<(ns + 63) / 64, 64, 0, c->side>>>(sl, ns, sm, lres, c->llen.as<uint32_t>());
+      HIPCHK(hipGetLastError());
+      if (int r = mark(c, c->side, "split_resolve")) return r;
+      if (c->hwlist.empty()) HIPCHK(hipEventRecord(c->join, c->side));
+    }
+    if (!c->hwlist.empty()) {
       const uint32_t nw = (uint32_t)c->hwlist.size();
       HIPCHK(c->wlist.ensure(4ull * nw));
       HIPCHK(hipMemcpyAsync(c->wlist.p, c->hwlist.data(), 4ull * nw, hipMemcpyHostToDevice, st));
