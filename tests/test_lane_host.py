@@ -115,3 +115,32 @@ def test_lane_kernel_on_host_deflate64_fixtures(lane_host):
     for f, (bail, olen, cons, want, out) in zip(names, res):
         assert not bail and corpus.sha256(out) == cases["d64_" + f]["out_sha256"], f
     assert not res[-1][0] and res[-1][4] == b"a" * 66539
+
+
+@pytest.mark.parametrize("fmt", ["deflate-raw", "deflate", "gzip"])
+def test_lane_kernel_on_host_large_members_reference_calls(lane_host, fmt):
+    """The large-member instance (<., true>: more than 32 KiB of input, the
+    reference's inflate() calls tracked per lane) against the oracle with the
+    reference's window-wrap copy reproduced (inffast.ts:133-147), including the
+    256 KiB member whose decode the defect changes (inffast_wrap_defect.json,
+    pinned by the reference's own output)."""
+    import json
+    rng = random.Random(13)
+    members = []
+    for k in range(10):
+        s = corpus.make({"kind": rng.choice(["text", "mixed"]), "n": rng.choice([70000, 150000, 262144, 400000]),
+                         "seed": rng.randrange(1 << 32)})
+        members.append((oracle.compress(s, rng.choice([1, 6, 9]), fmt)[1], len(s) + 64))
+    j = json.load(open(os.path.join(golden_io.GOLDEN, "inffast_wrap_defect.json")))
+    wrap_src = corpus.make(j["source"])
+    if fmt == "deflate-raw":
+        members.append((oracle.compress(wrap_src, 6, fmt)[1], len(wrap_src) + 64))
+    bails = check(lane_host, members, fmt, flags=3)
+    # members the reference decodes cleanly never leave the lane (with the
+    # defect, a zlib / gzip member's trailer can fail: the reference reports
+    # "incorrect data check" and so does the exact path the member goes to)
+    clean = [oracle.decompress(c, fmt, cap=cap & ~3, reference_bugs=True)[0] == 1 for c, cap in members]
+    assert not any(b for b, ok in zip(bails, clean) if ok), (bails, clean)
+    if fmt == "deflate-raw":
+        out = run(lane_host, members[-1:], fmt, flags=3)[0][4]
+        assert corpus.sha256(out) == j["ref_out_sha256"] and out != wrap_src

@@ -3,8 +3,10 @@
 // HIP names in hip/hip_runtime.h next to this file).  Test tooling: lets the CPU
 // suite check the lane decoder's logic against the oracle without a GPU.
 //
-// Both instances run on every member -- zs_k_inflate_lane<false> (canonical
-// decode only) and <true> (with the per-lane root tables) -- and must agree.
+// Both instances run on every member -- zs_k_inflate_lane<false, .> (canonical
+// decode only) and <true, .> (with the per-lane root tables) -- and must agree.
+// FLAGS bit 2 selects the large-member instances <., true> (the reference's
+// inflate() calls tracked per lane, its window-wrap copy reproduced).
 //
 // usage: lane_host WBITS FLAGS < members > results
 //   stdin:  u32 count, then per member: u32 in_len, u32 out_cap, in_len bytes
@@ -50,11 +52,23 @@ int main(int argc, char** argv) {
     uint8_t* ob8 = (uint8_t*)ob.data();
     const size_t obn = ob.size() * sizeof(uint4);
     for (size_t k = 0; k < obn; k++) ob8[k] = 0xa5;  // guard pattern around the member's output
-    zs_k_inflate_lane<true>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u);
+    const uint32_t zero = 0;
+    const bool refw = (flags & 2) != 0;
+    if (refw)
+      zs_k_inflate_lane<true, true>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags & 1, 0u,
+                                    &zero);
+    else
+      zs_k_inflate_lane<true, false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u,
+                                     nullptr);
     const std::vector<uint8_t> out_root(ob8, ob8 + obn);
     const zs_lane_res r_root = r;
     for (size_t k = 0; k < obn; k++) ob8[k] = 0xa5;
-    zs_k_inflate_lane<false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u);
+    if (refw)
+      zs_k_inflate_lane<false, true>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags & 1, 0u,
+                                     &zero);
+    else
+      zs_k_inflate_lane<false, false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u,
+                                      nullptr);
     if (r.bail != r_root.bail || (!r.bail && (r.out_len != r_root.out_len || r.consumed != r_root.consumed ||
                                               memcmp(ob8 + ooff, out_root.data() + ooff, r.out_len)))) {
       fprintf(stderr, "lane_host: member %u: root and canonical decoders differ\n", i);

@@ -97,6 +97,7 @@ struct zs_ctx {
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
   uint32_t inflate_wave_min = 32768;  // members with more input bytes decode one per wave (inflate_wave.hip); 0: never
+  uint32_t lane_large_min = 512;      // this many large members or more: one LANE each (zs_k_inflate_lane<.., true>)
   hipStream_t side = nullptr;         // second stream: the wave-per-member kernel runs beside the lane kernel
   hipEvent_t fork = nullptr, join = nullptr;
   Buf wlist;
@@ -291,6 +292,9 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
     if (value != 0 && (value < 1 || value > 64 || (value & (value - 1))))
       return fail(ZS_STREAM_ERROR, "lane_block must be 0 or a power of two <= 64");
     c->lane_block = value;
+  } else if (!strcmp(name, "lane_large_min")) {
+    if (value < 0) return fail(ZS_STREAM_ERROR, "lane_large_min must be >= 0");
+    c->lane_large_min = (uint32_t)value;
   } else if (!strcmp(name, "inflate_wave_min")) {
     if (value < 0) return fail(ZS_STREAM_ERROR, "inflate_wave_min must be >= 0");
     c->inflate_wave_min = (uint32_t)value;
@@ -958,7 +962,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
     // narrow workgroups afford per-lane root tables (inflate_lane.hip)
     const bool lroot = B <= 16;
     const size_t lsm = B * zs_inflate_lane_lds_bytes(lroot);
-    const void* lk = lroot ? (const void*)zs_k_inflate_lane<true> : (const void*)zs_k_inflate_lane<false>;
+    const void* lk = lroot ? (const void*)zs_k_inflate_lane<true, false> : (const void*)zs_k_inflate_lane<false, false>;
     HIPCHK(hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm));
     // Large members (more than inflate_wave_min input bytes) decode one per wave
     // on the side stream, beside the lane kernel: one lane would take the
@@ -1041,7 +1045,29 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       const void* wk = refw ? (const void*)zs_k_inflate_wave<true> : (const void*)zs_k_inflate_wave<false>;
       HIPCHK(hipFuncSetAttribute(wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wsm));
       if (int r = mark(c, c->side, "start")) return r;
-      if (refw)
+      // Many large members: one lane each (the lane kernel's REFW instance,
+      // the reference's calls tracked per lane) -- a wave per member keeps its
+      // bookkeeping in scalars, and the waves of a CU share one scalar unit
+      // (4,096 x 256 KiB: wave kernel 176 ms)
+      bool lanes = refw && c->lane_large_min && nw >= c->lane_large_min;
+      for (uint32_t i = 0; lanes && i < nw; i++) lanes = in_len[c->hwlist[i]] < (1u << 29);  // 32-bit bit positions
+      if (lanes) {
+        // thin workgroups to ~4096 waves (4,096 x 256 KiB: one lane per wave 95 ms, two 110, four 144)
+        uint32_t B2 = 1;
+        while (B2 < 64 && (nw + B2 - 1) / B2 > 4096u) B2 <<= 1;
+        const bool lroot2 = B2 <= 16;
+        const size_t lsm2 = B2 * zs_inflate_lane_lds_bytes(lroot2);
+        const void* lk2 = lroot2 ? (const void*)zs_k_inflate_lane<true, true> : (const void*)zs_k_inflate_lane<false, true>;
+        HIPCHK(hipFuncSetAttribute(lk2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm2));
+        if (lroot2)
+          zs_k_inflate_lane<true, true><<<(nw + B2 - 1) / B2, B2, lsm2, c->side>>>(
+              d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, nw, (zs_lane_tabs*)c->ltabs.p, lres,
+              c->llen.as<uint32_t>(), ZS_INF_REF_WRAP, 0u, c->wlist.as<uint32_t>());
+        else
+          zs_k_inflate_lane<false, true><<<(nw + B2 - 1) / B2, B2, lsm2, c->side>>>(
+              d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, nw, (zs_lane_tabs*)c->ltabs.p, lres,
+              c->llen.as<uint32_t>(), ZS_INF_REF_WRAP, 0u, c->wlist.as<uint32_t>());
+      } else if (refw)
         zs_k_inflate_wave<true><<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
                                                           c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
       else
@@ -1052,13 +1078,13 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       HIPCHK(hipEventRecord(c->join, c->side));
     }
     if (lroot)
-      zs_k_inflate_lane<true><<<(n + B - 1) / B, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
-                                                               (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
-                                                               c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min);
+      zs_k_inflate_lane<true, false><<<(n + B - 1) / B, B, lsm, st>>>(
+          d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n, (zs_lane_tabs*)c->ltabs.p, lres,
+          c->llen.as<uint32_t>(), c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min, nullptr);
     else
-      zs_k_inflate_lane<false><<<(n + B - 1) / B, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n,
-                                                                (zs_lane_tabs*)c->ltabs.p, lres, c->llen.as<uint32_t>(),
-                                                                c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min);
+      zs_k_inflate_lane<false, false><<<(n + B - 1) / B, B, lsm, st>>>(
+          d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n, (zs_lane_tabs*)c->ltabs.p, lres,
+          c->llen.as<uint32_t>(), c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min, nullptr);
     MARK("inflate_lane");
     if (wave_min) {
       HIPCHK(hipStreamWaitEvent(st, c->join, 0));

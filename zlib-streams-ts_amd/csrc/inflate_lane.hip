@@ -4,6 +4,7 @@
 #include "zs_common.h"
 #include "zs_inflate.h"
 #include "zs_inftab.h"
+#include "zs_refcalls.h"
 #ifndef ZS_OPAQUE  // (the host stand-in of tools/lane_host defines it away)
 #define ZS_OPAQUE(x) asm("" : "+v"(x))
 #endif
@@ -330,20 +331,28 @@ extern "C" int zs_il_stats(unsigned long long* out) {
 #define IL_ACC(i, v) do { if (IL_FIRST()) st[i] += clock64() - v; } while (0)
 #endif
 
-template <bool ROOT>
-__global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
+// REFW: the large-member instance (launched over a list of members with more
+// than inflate_wave_min input bytes): a deflate / zlib / gzip member at any
+// size, the reference's inflate() calls tracked per lane (zs_refcalls) and
+// their window-wrap copy reproduced -- what zs_k_inflate_wave does with a wave
+// per member, here with a lane (many large members: the wave kernel's scalar
+// bookkeeping shares one scalar unit per CU among its waves).
+template <bool ROOT, bool REFW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off,
                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                         const uint64_t* __restrict__ out_off,
                                                         const uint32_t* __restrict__ out_cap, int wbits, uint32_t n_members,
                                                         zs_lane_tabs* __restrict__ tabs, zs_lane_res* __restrict__ res,
                                                         uint32_t* __restrict__ lens_out, int flags,
-                                                        uint32_t wave_min) {
+                                                        uint32_t wave_min, const uint32_t* __restrict__ list) {
   extern __shared__ __attribute__((aligned(16))) uint8_t LL[];  // blockDim.x lanes' tables
   constexpr uint32_t lstride = ROOT ? sizeof(zs_lane_lds_root) : sizeof(zs_lane_lds);
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n_members) return;
-  if (wave_min && in_len[s] > wave_min) return;  // a large member: zs_k_inflate_wave decodes it (inflate_wave.hip)
+  const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= n_members) return;
+  const uint32_t s = REFW ? list[li] : li;
+  // a large member: the REFW instance, zs_k_inflate_wave or the split path decodes it
+  if (!REFW && wave_min && in_len[s] > wave_min) return;
   zs_lane_tabs& T = tabs[s];
   zs_lane_lds& F = *reinterpret_cast<zs_lane_lds*>(LL + threadIdx.x * lstride);
   uint16_t* const lroot = ROOT ? reinterpret_cast<zs_lane_lds_root*>(&F)->lroot : nullptr;
@@ -379,8 +388,10 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
   // deflate64 members never reach inflate_fast in the reference (inflate.ts:841),
   // so they carry no call-boundary behaviour and decode here at any size.
   const bool d64 = wbits == -16;
-  const bool ref_wrap = (flags & ZS_INF_REF_WRAP) != 0 && !d64;
+  const bool ref_wrap = (flags & ZS_INF_REF_WRAP) != 0 && !d64 && !REFW;
   const uint32_t cap = ref_wrap ? min(out_cap[s], 65536u) : out_cap[s];
+  zs_refcalls_t<uint32_t> C;  // (the host routes members of under 512 MB here: bit positions fit 32 bits)
+  C.init();
   const uint32_t lmask = d64 ? 31u : 15u;  // length extra-bit mask (inflate.ts:891)
   uint32_t total = 0;
   zs_lane_res r = {1u, 0u, 0u, 0u};
@@ -409,6 +420,7 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       zs_lr_align(R);
       const uint32_t len = zs_lr_take(R, 16), nlen = zs_lr_take(R, 16);
       if (len != (nlen ^ 0xffffu) || zs_lr_over(R) || total + len > cap) { bail = true; break; }
+      if (REFW) C.stored((uint32_t)(zs_lr_bitpos(R) >> 3), total, len);
       for (uint32_t i = 0; i < len; i++) {
         if (W.P - W.F > ZS_RING - 8u) W.flush();
         W.byte(zs_lr_take(R, 8));
@@ -496,6 +508,7 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       st[1] += IL_FIRST();  // wave steps (summed)
 #endif
       uint32_t L, k, sym;
+      const uint32_t b0 = REFW ? R.pos * 8u - R.bits : 0u;  // the symbol's first bit (zs_refcalls)
       const uint32_t le = ROOT ? lroot[(uint32_t)R.hold & ((1u << ZS_LROOT) - 1u)] : 0u;
       if (le) {
         L = le >> 12;
@@ -506,18 +519,24 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
         sym = F.lsym[k] | (((F.lhi[k >> 5] >> (k & 31u)) & 1u) << 8);
       }
       zs_lr_drop(R, L);
+      const uint32_t l1 = L;
       if (sym >= 286) { bail = true; break; }  // fixed codes 286/287: "invalid literal/length code"
       zcode here = zs_lit_entry(sym, d64);
       uint32_t op = C_OP(here);
       if (op == 0) {
         if (total >= cap) { bail = true; break; }
+        if (REFW) C.symbol(b0, total, 1u, l1, 0u, 0u, 0u, false);
         W.byte(C_VAL(here));
         total++;
         continue;
       }
-      if (op & 32) break;                   // end of block
+      if (op & 32) {  // end of block
+        if (REFW) C.symbol(b0, total, 0u, l1, 0u, 0u, 0u, true);
+        break;
+      }
       if (op & 64) { bail = true; break; }  // "invalid literal/length code"
-      uint32_t len = C_VAL(here) + zs_lr_take(R, op & lmask);
+      const uint32_t e1 = op & lmask;
+      uint32_t len = C_VAL(here) + zs_lr_take(R, e1);
       if (R.bits < 32) zs_lr_fill(R);
       uint32_t dsym;
       const uint32_t de = ROOT ? droot[(uint32_t)R.hold & ((1u << ZS_DROOT) - 1u)] : 0u;
@@ -533,8 +552,19 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
       if (!d64 && dsym >= 30) { bail = true; break; }  // fixed codes 30/31 likewise
       here = zs_dist_entry(dsym, d64);
       op = C_OP(here);
-      const uint32_t dist = C_VAL(here) + zs_lr_take(R, op & 15u);
-      if (dist > total || total + len > cap) { bail = true; break; }  // too far back / capacity
+      const uint32_t dist0 = C_VAL(here) + zs_lr_take(R, op & 15u);
+      if (dist0 > total || total + len > cap) { bail = true; break; }  // too far back / capacity
+      // REFW: a copy inflate_fast runs may end with the reference's window-wrap
+      // copy -- its last `tail` bytes taken from the current call's first output
+      // bytes (C.B on), i.e. a second copy at distance total + head - C.B
+      uint32_t tail = 0;
+      if (REFW && C.symbol(b0, total, len, l1, e1, L, op & 15u, false)) tail = C.wrap(total, len, dist0);
+      const uint32_t len_all = len;
+      for (uint32_t part = 0; part < (REFW ? 2u : 1u); part++) {
+      const uint32_t dist = part == 0 ? dist0 : total - C.B;  // (total has moved past the head)
+      if (part == 0) len -= tail;
+      else len = tail;
+      if (len == 0) continue;
       const uint32_t src = W.P - dist;
 #if ZS_IL_EXP & 64
       IL_T(tc);
@@ -588,6 +618,8 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
 #endif
       }
       total += len;
+      }  // part
+      (void)len_all;
     }
     if (zs_lr_over(R)) bail = true;
 #if ZS_IL_EXP & 64
@@ -631,10 +663,12 @@ __global__ __launch_bounds__(64) void zs_k_inflate_lane(const uint8_t* __restric
 size_t zs_inflate_lane_scratch_bytes() { return sizeof(zs_lane_tabs); }
 size_t zs_inflate_lane_lds_bytes(bool root) { return root ? sizeof(zs_lane_lds_root) : sizeof(zs_lane_lds); }
 
-#define ZS_LANE_INST(R)                                                                                              \
-  template __global__ void zs_k_inflate_lane<R>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,          \
-                                                const uint64_t*, const uint32_t*, int, uint32_t, zs_lane_tabs*,       \
-                                                zs_lane_res*, uint32_t*, int, uint32_t);
-ZS_LANE_INST(false)
-ZS_LANE_INST(true)
+#define ZS_LANE_INST(R, W)                                                                                           \
+  template __global__ void zs_k_inflate_lane<R, W>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,       \
+                                                   const uint64_t*, const uint32_t*, int, uint32_t, zs_lane_tabs*,    \
+                                                   zs_lane_res*, uint32_t*, int, uint32_t, const uint32_t*);
+ZS_LANE_INST(false, false)
+ZS_LANE_INST(true, false)
+ZS_LANE_INST(false, true)
+ZS_LANE_INST(true, true)
 

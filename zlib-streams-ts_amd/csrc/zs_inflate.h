@@ -55,11 +55,11 @@ __global__ void zs_k_inflate(const uint8_t* in, const uint64_t* in_off, const ui
                              const uint64_t* out_off, const uint32_t* out_cap, int wbits, zs_inflate_result* res,
                              const zs_lane_res* only, int flags);
 struct zs_lane_tabs;
-template <bool ROOT>
+template <bool ROOT, bool REFW>
 __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, uint32_t n_members,
                                   zs_lane_tabs* tabs, zs_lane_res* res, uint32_t* lens_out, int flags,
-                                  uint32_t wave_min);
+                                  uint32_t wave_min, const uint32_t* list);
 template <bool REFW>
 __global__ void zs_k_inflate_wave(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, const uint32_t* list,

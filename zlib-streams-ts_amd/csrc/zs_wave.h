@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "zs_inftab.h"
+#include "zs_refcalls.h"
 
 #ifndef ZS_WIN_IN
 #define ZS_WIN_IN 256u  // staged input words
@@ -83,4 +84,3 @@ static __device__ __forceinline__ zcode zs_wr_decode(zs_wave_reader& R, const zc
   R.bits -= C_BITS(here);
   return here;
 }
-
