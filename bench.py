@@ -591,7 +591,8 @@ def main_inflate(args):
         step()  # back to back: the phase events are read after the timed region
     D.barrier()
     elapsed = D.max(time.perf_counter() - t0)
-    for ph in ("inflate_lane", "inflate_wave", "inflate_join", "inflate_check", "inflate", "finish"):
+    for ph in ("inflate_lane", "inflate_wave", "inflate_large", "split_find", "split_decode", "split_resolve",
+               "inflate_join", "inflate_check", "inflate", "finish"):
         v = eng.last_ms(ph)  # summed over the timed steps
         if v >= 0:
             phases[ph] = phases.get(ph, 0.0) + v
@@ -631,13 +632,26 @@ def main_inflate(args):
         dom = max(phase_avg, key=phase_avg.get)
         k_ms = phase_avg[dom]
         alg = in_local + out_local  # compressed_in + uncompressed_out per member
-        if dom == "inflate_wave":  # the wave kernel decodes only the members with more input than inflate_wave_min
+        if dom in ("inflate_wave", "inflate_large"):  # only the members with more input than inflate_wave_min
             opts = dict(o.split("=", 1) for o in args.option)
             wmin = int(opts.get("inflate_wave_min", 32768))
             olen = d_len.cpu().tolist()
             alg = sum(len(m) + olen[i] for i, m in enumerate(members) if len(m) > wmin)
         achieved = alg / (k_ms / 1e3) / 1e9
-        traffic, tsrc = profiled_traffic("zs_k_" + dom, k_ms, profile_tag(args))
+        # the phase's kernel (profiles key template instances on their own: "zs_k_inflate_lane<true,true>")
+        kernels = {"inflate_lane": ["zs_k_inflate_lane<false,false>", "zs_k_inflate_lane<true,false>"],
+                   "inflate_large": ["zs_k_inflate_lane<true,true>", "zs_k_inflate_lane<false,true>"],
+                   "inflate_wave": ["zs_k_inflate_wave<true>", "zs_k_inflate_wave<false>"]}.get(dom, ["zs_k_" + dom])
+        for kern in kernels:
+            traffic, tsrc = profiled_traffic(kern, k_ms, profile_tag(args))
+            if traffic is not None:
+                break
+        ceil = None
+        for kc in kernels:
+            ceil = profiled_ceilings(kc, k_ms, profile_tag(args))
+            if ceil and "source" in ceil and not str(ceil["source"]).startswith(("stale", "no ")):
+                break
+        kern = kern if traffic is not None else kernels[0]
         cpu = None
         if not (args.no_cpu_baseline or D.world > 1):
             import oracle
@@ -658,11 +672,11 @@ def main_inflate(args):
             "verify": {"members_checked": checked, "mismatches": bad, "sources_vs_golden": members_checked,
                        "golden": "tests/golden/batch_%s.bin" % gname if gname else None,
                        "decode_golden": "tests/golden/batch_%s.bin" % dname if dname else None},
-            "roofline": {"bound": "hbm", "kernel": "zs_k_" + dom, "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg,
                          "kernel_ms": round(k_ms, 4), "phase_ms": phase_avg,
-                         "ceilings": profiled_ceilings("zs_k_" + dom, k_ms, profile_tag(args))},
+                         "ceilings": ceil},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -25,11 +25,14 @@ dur = collections.defaultdict(list)
 for f in sorted(glob.glob(os.path.join(d, "sq*", "run_counter_collection.csv"))):
     seen = set()
     for r in csv.DictReader(open(f)):
-        k = re.sub(r"<[^>]*>", "", r["Kernel_Name"].split("(")[0].replace("void ", ""))
-        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-        if (f, r["Dispatch_Id"]) not in seen:
-            seen.add((f, r["Dispatch_Id"]))
-            dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        full = r["Kernel_Name"].split("(")[0].replace("void ", "").replace(" ", "")
+        base = re.sub(r"<[^>]*>", "", full)
+        # the merged kernel and, for templates, each instance on its own
+        for k in ({base, full} if full != base else {base}):
+            agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if (f, r["Dispatch_Id"], k) not in seen:
+                seen.add((f, r["Dispatch_Id"], k))
+                dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 
 
 def derived(v):

@@ -9,8 +9,12 @@ which it got ("fetch_correction")."""
 import collections, csv, json, os, re, sys
 
 
-def kname(name):  # "void zs_k_fast<2>(...)" -> "zs_k_fast"
-    return re.sub(r"<[^>]*>", "", name.split("(")[0].replace("void ", "")).strip()
+def knames(name):
+    """'void zs_k_fast<2>(...)' -> ['zs_k_fast', 'zs_k_fast<2>']: every kernel under its
+    merged name and, for templates, each instance under its own"""
+    full = name.split("(")[0].replace("void ", "").replace(" ", "").strip()
+    base = re.sub(r"<[^>]*>", "", full)
+    return [base] if base == full else [base, full]
 
 
 # kernels whose dominant reads are 16-byte-per-lane coalesced loads of the input
@@ -20,15 +24,19 @@ WIDE_READ = {"zs_k_match", "zs_k_sweep"}
 src, dst = sys.argv[1], sys.argv[2]
 stats = {}
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
-    stats[kname(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                                       "total_ns": float(r["TotalDurationNs"])}
+    for k in knames(r["Name"]):
+        e = stats.setdefault(k, {"calls": 0, "total_ns": 0.0})
+        e["calls"] += int(r["Calls"])
+        e["total_ns"] += float(r["TotalDurationNs"])
+        e["avg_ns"] = e["total_ns"] / e["calls"]
 cnt = collections.defaultdict(lambda: collections.defaultdict(list))
 for kind in ("fetch", "write"):
     p = os.path.join(src, kind, "run_counter_collection.csv")
     if not os.path.exists(p):
         continue
     for r in csv.DictReader(open(p)):
-        cnt[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k in knames(r["Kernel_Name"]):
+            cnt[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
 for k, v in stats.items():
     e = dict(v)
@@ -39,7 +47,7 @@ for k, v in stats.items():
         e["write_kib"] = sum(w) / len(w)
     if f and w:
         e["hbm_bytes_raw"] = (e["fetch_kib"] + e["write_kib"]) * 1024
-        wide = k in WIDE_READ
+        wide = re.sub(r"<[^>]*>", "", k) in WIDE_READ
         e["fetch_correction"] = "x2 (16-B coalesced reads)" if wide else "none (narrow reads: uncalibrated, raw)"
         e["hbm_bytes_corrected"] = ((2 if wide else 1) * e["fetch_kib"] + e["write_kib"]) * 1024
     out[k] = e

@@ -1074,7 +1074,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
         zs_k_inflate_wave<false><<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
                                                            c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
       HIPCHK(hipGetLastError());
-      if (int r = mark(c, c->side, "inflate_wave")) return r;
+      if (int r = mark(c, c->side, lanes ? "inflate_large" : "inflate_wave")) return r;
       HIPCHK(hipEventRecord(c->join, c->side));
     }
     if (lroot)
