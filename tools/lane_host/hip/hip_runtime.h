@@ -41,4 +41,5 @@ static inline uint32_t atomicOr(uint32_t* p, uint32_t v) {
   return o;
 }
 #define ZS_OPAQUE(x) ((void)0)
+#define ZS_LANE_WAVES(n)
 typedef int hipError_t;

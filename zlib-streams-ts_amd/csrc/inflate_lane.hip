@@ -5,8 +5,11 @@
 #include "zs_inflate.h"
 #include "zs_inftab.h"
 #include "zs_refcalls.h"
-#ifndef ZS_OPAQUE  // (the host stand-in of tools/lane_host defines it away)
+#ifndef ZS_OPAQUE  // (the host stand-in of tools/lane_host defines these away)
 #define ZS_OPAQUE(x) asm("" : "+v"(x))
+#endif
+#ifndef ZS_LANE_WAVES
+#define ZS_LANE_WAVES(n) __attribute__((amdgpu_waves_per_eu(n)))
 #endif
 #ifndef ZS_IL_EXP
 #define ZS_IL_EXP 0  // experiment builds (timing only; 0 in the product): 1 no stores, 2 no copy loads, 64 counters
@@ -338,7 +341,7 @@ extern "C" int zs_il_stats(unsigned long long* out) {
 // per member, here with a lane (many large members: the wave kernel's scalar
 // bookkeeping shares one scalar unit per CU among its waves).
 template <bool ROOT, bool REFW>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off,
                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
                                                         const uint64_t* __restrict__ out_off,
