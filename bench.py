@@ -639,8 +639,9 @@ def main_inflate(args):
             alg = sum(len(m) + olen[i] for i, m in enumerate(members) if len(m) > wmin)
         achieved = alg / (k_ms / 1e3) / 1e9
         # the phase's kernel (profiles key template instances on their own: "zs_k_inflate_lane<true,true>")
-        kernels = {"inflate_lane": ["zs_k_inflate_lane<false,false>", "zs_k_inflate_lane<true,false>"],
-                   "inflate_large": ["zs_k_inflate_lane<true,true>", "zs_k_inflate_lane<false,true>"],
+        kernels = {"inflate_lane": ["zs_k_inflate_lane<0,false>", "zs_k_inflate_lane<1,false>",
+                                    "zs_k_inflate_lane<2,false>"],
+                   "inflate_large": ["zs_k_inflate_lane<2,true>", "zs_k_inflate_lane<0,true>"],
                    "inflate_wave": ["zs_k_inflate_wave<true>", "zs_k_inflate_wave<false>"]}.get(dom, ["zs_k_" + dom])
         for kern in kernels:
             traffic, tsrc = profiled_traffic(kern, k_ms, profile_tag(args))

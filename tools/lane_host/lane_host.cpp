@@ -3,8 +3,9 @@
 // HIP names in hip/hip_runtime.h next to this file).  Test tooling: lets the CPU
 // suite check the lane decoder's logic against the oracle without a GPU.
 //
-// Both instances run on every member -- zs_k_inflate_lane<false, .> (canonical
-// decode only) and <true, .> (with the per-lane root tables) -- and must agree.
+// The instances run on every member -- zs_k_inflate_lane<0, .> (canonical
+// decode only), <1, .> (with the per-lane root tables) and <2, false> (root
+// tables, canonical limits in LDS) -- and must agree.
 // FLAGS bit 2 selects the large-member instances <., true> (the reference's
 // inflate() calls tracked per lane, its window-wrap copy reproduced).
 //
@@ -55,24 +56,36 @@ int main(int argc, char** argv) {
     const uint32_t zero = 0;
     const bool refw = (flags & 2) != 0;
     if (refw)
-      zs_k_inflate_lane<true, true>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags & 1, 0u,
+      zs_k_inflate_lane<2, true>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags & 1, 0u,
                                     &zero);
     else
-      zs_k_inflate_lane<true, false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u,
+      zs_k_inflate_lane<1, false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u,
                                      nullptr);
     const std::vector<uint8_t> out_root(ob8, ob8 + obn);
     const zs_lane_res r_root = r;
     for (size_t k = 0; k < obn; k++) ob8[k] = 0xa5;
     if (refw)
-      zs_k_inflate_lane<false, true>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags & 1, 0u,
+      zs_k_inflate_lane<0, true>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags & 1, 0u,
                                      &zero);
     else
-      zs_k_inflate_lane<false, false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u,
+      zs_k_inflate_lane<0, false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u,
                                       nullptr);
     if (r.bail != r_root.bail || (!r.bail && (r.out_len != r_root.out_len || r.consumed != r_root.consumed ||
                                               memcmp(ob8 + ooff, out_root.data() + ooff, r.out_len)))) {
       fprintf(stderr, "lane_host: member %u: root and canonical decoders differ\n", i);
       exit(4);
+    }
+    if (!refw) {  // the instance with the canonical limits in LDS too
+      const std::vector<uint8_t> out_c(ob8, ob8 + obn);
+      const zs_lane_res r_c = r;
+      for (size_t k = 0; k < obn; k++) ob8[k] = 0xa5;
+      zs_k_inflate_lane<2, false>(in, &ioff, &len, ob8, &ooff, &cap, wbits, 1, tabs.data(), &r, &lo, flags, 0u,
+                                  nullptr);
+      if (r.bail != r_c.bail || (!r.bail && (r.out_len != r_c.out_len || r.consumed != r_c.consumed ||
+                                             memcmp(ob8, out_c.data(), obn)))) {
+        fprintf(stderr, "lane_host: member %u: the LDS-canon instance differs\n", i);
+        exit(4);
+      }
     }
     for (size_t k = 0; k < obn; k++)
       if ((k < ooff || k >= ooff + cap) && ob8[k] != 0xa5) {

@@ -962,8 +962,6 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
     // narrow workgroups afford per-lane root tables (inflate_lane.hip)
     const bool lroot = B <= 16;
     const size_t lsm = B * zs_inflate_lane_lds_bytes(lroot);
-    const void* lk = lroot ? (const void*)zs_k_inflate_lane<true, false> : (const void*)zs_k_inflate_lane<false, false>;
-    HIPCHK(hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm));
     // Large members (more than inflate_wave_min input bytes) decode one per wave
     // on the side stream, beside the lane kernel: one lane would take the
     // batch's whole time on such a member.  The wave kernel tracks the
@@ -1057,14 +1055,14 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
         while (B2 < 64 && (nw + B2 - 1) / B2 > 4096u) B2 <<= 1;
         const bool lroot2 = B2 <= 16;
         const size_t lsm2 = B2 * zs_inflate_lane_lds_bytes(lroot2);
-        const void* lk2 = lroot2 ? (const void*)zs_k_inflate_lane<true, true> : (const void*)zs_k_inflate_lane<false, true>;
+        const void* lk2 = lroot2 ? (const void*)zs_k_inflate_lane<2, true> : (const void*)zs_k_inflate_lane<0, true>;
         HIPCHK(hipFuncSetAttribute(lk2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm2));
         if (lroot2)
-          zs_k_inflate_lane<true, true><<<(nw + B2 - 1) / B2, B2, lsm2, c->side>>>(
+          zs_k_inflate_lane<2, true><<<(nw + B2 - 1) / B2, B2, lsm2, c->side>>>(
               d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, nw, (zs_lane_tabs*)c->ltabs.p, lres,
               c->llen.as<uint32_t>(), ZS_INF_REF_WRAP, 0u, c->wlist.as<uint32_t>());
         else
-          zs_k_inflate_lane<false, true><<<(nw + B2 - 1) / B2, B2, lsm2, c->side>>>(
+          zs_k_inflate_lane<0, true><<<(nw + B2 - 1) / B2, B2, lsm2, c->side>>>(
               d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, nw, (zs_lane_tabs*)c->ltabs.p, lres,
               c->llen.as<uint32_t>(), ZS_INF_REF_WRAP, 0u, c->wlist.as<uint32_t>());
       } else if (refw)
@@ -1077,14 +1075,26 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       if (int r = mark(c, c->side, lanes ? "inflate_large" : "inflate_wave")) return r;
       HIPCHK(hipEventRecord(c->join, c->side));
     }
-    if (lroot)
-      zs_k_inflate_lane<true, false><<<(n + B - 1) / B, B, lsm, st>>>(
-          d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n, (zs_lane_tabs*)c->ltabs.p, lres,
-          c->llen.as<uint32_t>(), c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min, nullptr);
+    // Narrow workgroups with large members beside them (side stream): the
+    // LDS-canon instance, 68 VGPRs, so the side stream's waves find slots on
+    // every SIMD (C5-ii: 34 -> 26 ms); alone, the register instance (C5-i:
+    // 24.4 vs 25.7 ms)
+    const int rt = !lroot ? 0 : wave_min ? 2 : 1;
+    const void* lk = rt == 2 ? (const void*)zs_k_inflate_lane<2, false>
+                   : rt == 1 ? (const void*)zs_k_inflate_lane<1, false> : (const void*)zs_k_inflate_lane<0, false>;
+    HIPCHK(hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lsm));
+    const uint32_t lgrid = (n + B - 1) / B;
+    const int lflags = c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0;
+    zs_lane_tabs* const lt = (zs_lane_tabs*)c->ltabs.p;
+    if (rt == 2)
+      zs_k_inflate_lane<2, false><<<lgrid, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n, lt, lres,
+                                                         c->llen.as<uint32_t>(), lflags, wave_min, nullptr);
+    else if (rt == 1)
+      zs_k_inflate_lane<1, false><<<lgrid, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n, lt, lres,
+                                                         c->llen.as<uint32_t>(), lflags, wave_min, nullptr);
     else
-      zs_k_inflate_lane<false, false><<<(n + B - 1) / B, B, lsm, st>>>(
-          d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n, (zs_lane_tabs*)c->ltabs.p, lres,
-          c->llen.as<uint32_t>(), c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0, wave_min, nullptr);
+      zs_k_inflate_lane<0, false><<<lgrid, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n, lt, lres,
+                                                         c->llen.as<uint32_t>(), lflags, wave_min, nullptr);
     MARK("inflate_lane");
     if (wave_min) {
       HIPCHK(hipStreamWaitEvent(st, c->join, 0));

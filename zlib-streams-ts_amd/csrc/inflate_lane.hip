@@ -15,6 +15,12 @@
 #define ZS_IL_EXP 0  // experiment builds (timing only; 0 in the product): 1 no stores, 2 no copy loads, 64 counters
 #endif
 #define IL_ST(x) do { if (!(ZS_IL_EXP & 1)) { x; } } while (0)
+#if ZS_IL_EXP & 128  // per-member clock cycles, start and end (timing experiments)
+__device__ unsigned long long zs_il_mcyc[2 * 65536];
+extern "C" int zs_il_member_cycles(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_il_mcyc), sizeof(unsigned long long) * 2 * n);
+}
+#endif
 #define IL_LD(x) ((ZS_IL_EXP & 2) ? 0u : (uint32_t)(x))
 
 // One LANE per member.  The exact kernel above spends a whole wave on one
@@ -114,11 +120,19 @@ struct zs_lane_lds {
 // with few lanes per wave the VALU work per symbol is what each SIMD's lone
 // wave waits on (C5-i: 8,192 members, eight lanes per wave).
 #define ZS_LROOT 9u
-#define ZS_DROOT 7u
+#ifndef ZS_DROOT
+#define ZS_DROOT 8u
+#endif
 struct zs_lane_lds_root {
   zs_lane_lds b;
   uint16_t lroot[1u << ZS_LROOT];
   uint16_t droot[1u << ZS_DROOT];
+  // the canonical codes' limits too, for the LDS-canon instances (RT = 2; only
+  // codes longer than the roots read them): out of registers the kernel needs
+  // 68 VGPRs instead of 120 and leaves wave slots free on every SIMD, which the
+  // large members' kernels of the same batch (side stream) run in
+  __attribute__((aligned(16))) zs_canon cl;
+  __attribute__((aligned(16))) zs_canon cd;
 };
 
 // C from lens[0..n) (the member's scratch in HBM); false unless the code is
@@ -200,6 +214,25 @@ static __device__ __forceinline__ uint32_t zs_canon_rank(const zs_canon& C, cons
   }
   L = n;
   return (rev >> ((15u - n) & 31u)) + D;
+}
+// the same from a code kept in LDS: the limits in four 16-byte reads, then the
+// one D[] entry of the code's length
+static __device__ __forceinline__ uint32_t zs_canon_rank_lds(const zs_canon& C, const zs_lane_reader& R,
+                                                             uint32_t& L) {
+  const uint32_t rev = __builtin_bitreverse32((uint32_t)R.hold) >> 17;
+  const uint4* l4 = reinterpret_cast<const uint4*>(C.lim);  // lim[0..14] (+ D[0], unused)
+  const uint4 q0 = l4[0], q1 = l4[1], q2 = l4[2], q3 = l4[3];
+  const uint32_t lim[15] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z};
+  uint32_t n = 1;
+#pragma unroll
+  for (int l = 0; l < 15; l++) n += rev >= lim[l] ? 1u : 0u;
+  L = n;
+  return (rev >> ((15u - n) & 31u)) + C.D[(n - 1u) & 15u];
+}
+template <bool LDS>
+static __device__ __forceinline__ uint32_t zs_canon_rank_t(const zs_canon& C, const zs_lane_reader& R, uint32_t& L) {
+  if constexpr (LDS) return zs_canon_rank_lds(C, R, L);
+  else return zs_canon_rank(C, R, L);
 }
 static __device__ __forceinline__ void zs_lr_drop(zs_lane_reader& R, uint32_t k) {
   R.hold >>= k;
@@ -340,7 +373,9 @@ extern "C" int zs_il_stats(unsigned long long* out) {
 // their window-wrap copy reproduced -- what zs_k_inflate_wave does with a wave
 // per member, here with a lane (many large members: the wave kernel's scalar
 // bookkeeping shares one scalar unit per CU among its waves).
-template <bool ROOT, bool REFW>
+// RT: 0 no root tables (wide workgroups), 1 root tables, 2 root tables with
+// the canonical limits in LDS too (batches with large members beside them)
+template <int RT, bool REFW>
 __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off,
                                                         const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -350,6 +385,7 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
                                                         uint32_t* __restrict__ lens_out, int flags,
                                                         uint32_t wave_min, const uint32_t* __restrict__ list) {
   extern __shared__ __attribute__((aligned(16))) uint8_t LL[];  // blockDim.x lanes' tables
+  constexpr bool ROOT = RT > 0, LCAN = RT == 2;
   constexpr uint32_t lstride = ROOT ? sizeof(zs_lane_lds_root) : sizeof(zs_lane_lds);
   const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= n_members) return;
@@ -360,6 +396,9 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
   zs_lane_lds& F = *reinterpret_cast<zs_lane_lds*>(LL + threadIdx.x * lstride);
   uint16_t* const lroot = ROOT ? reinterpret_cast<zs_lane_lds_root*>(&F)->lroot : nullptr;
   uint16_t* const droot = ROOT ? reinterpret_cast<zs_lane_lds_root*>(&F)->droot : nullptr;
+#if ZS_IL_EXP & 128
+  if (s < 65536) zs_il_mcyc[2 * s] = wall_clock64();
+#endif
   zs_lane_reader R;
   {
     const uint8_t* src = in + in_off[s];
@@ -379,7 +418,9 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
   unsigned long long tk = tk0;
 #endif
   uint8_t* dst = out + out_off[s];
-  zs_canon CL, CD;
+  zs_canon CLr, CDr;  // registers (wide workgroups); the root instance keeps them in LDS
+  zs_canon& CL = *(LCAN ? &reinterpret_cast<zs_lane_lds_root*>(&F)->cl : &CLr);
+  zs_canon& CD = *(LCAN ? &reinterpret_cast<zs_lane_lds_root*>(&F)->cd : &CDr);
   zs_lane_out W;
   W.init(dst, F.ring);
   // This path decodes a member in one go, without the stream layer's call
@@ -452,7 +493,7 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
       while (i < nlen + ndist) {
         if (R.bits < 32) zs_lr_fill(R);
         uint32_t L;
-        const uint32_t k = zs_canon_rank(CD, R, L);
+        const uint32_t k = zs_canon_rank_t<LCAN>(CD, R, L);
         if (L > 15) { bail = true; break; }
         zs_lr_drop(R, L);
         const uint32_t v = F.dsym[k];
@@ -517,7 +558,7 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
         L = le >> 12;
         sym = le & 0x1ffu;
       } else {
-        k = zs_canon_rank(CL, R, L);
+        k = zs_canon_rank_t<LCAN>(CL, R, L);
         if (L > 15) { bail = true; break; }  // "invalid literal/length code"
         sym = F.lsym[k] | (((F.lhi[k >> 5] >> (k & 31u)) & 1u) << 8);
       }
@@ -547,7 +588,7 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
         L = de >> 12;
         dsym = de & 0x1fu;
       } else {
-        k = zs_canon_rank(CD, R, L);
+        k = zs_canon_rank_t<LCAN>(CD, R, L);
         if (L > 15) { bail = true; break; }  // "invalid distance code"
         dsym = F.dsym[k];
       }
@@ -649,6 +690,9 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
     r.consumed = (uint32_t)((zs_lr_bitpos(R) + 7u) >> 3);
   }
   res[s] = r;
+#if ZS_IL_EXP & 128
+  if (s < 65536) zs_il_mcyc[2 * s + 1] = wall_clock64();
+#endif
   lens_out[s] = r.out_len;  // for the checksum pass over the decoded bytes
 #if ZS_IL_EXP & 64
   st[7] = clock64() - tk0;
@@ -670,8 +714,9 @@ size_t zs_inflate_lane_lds_bytes(bool root) { return root ? sizeof(zs_lane_lds_r
   template __global__ void zs_k_inflate_lane<R, W>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,       \
                                                    const uint64_t*, const uint32_t*, int, uint32_t, zs_lane_tabs*,    \
                                                    zs_lane_res*, uint32_t*, int, uint32_t, const uint32_t*);
-ZS_LANE_INST(false, false)
-ZS_LANE_INST(true, false)
-ZS_LANE_INST(false, true)
-ZS_LANE_INST(true, true)
+ZS_LANE_INST(0, false)
+ZS_LANE_INST(1, false)
+ZS_LANE_INST(2, false)
+ZS_LANE_INST(0, true)
+ZS_LANE_INST(2, true)
 

@@ -55,7 +55,7 @@ __global__ void zs_k_inflate(const uint8_t* in, const uint64_t* in_off, const ui
                              const uint64_t* out_off, const uint32_t* out_cap, int wbits, zs_inflate_result* res,
                              const zs_lane_res* only, int flags);
 struct zs_lane_tabs;
-template <bool ROOT, bool REFW>
+template <int RT, bool REFW>
 __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, uint32_t n_members,
                                   zs_lane_tabs* tabs, zs_lane_res* res, uint32_t* lens_out, int flags,
