@@ -104,6 +104,21 @@ static __device__ __forceinline__ zs_pstate zs_read_state(const zs_pstate& x, ui
 
 #define ZS_GATHER 16  // pass C: 64-symbol chunks loaded before any is stored
 
+#ifndef ZS_PARSE_PROF
+#define ZS_PARSE_PROF 0  // timing experiments: cycles per pass summed over waves (0 in the product)
+#endif
+#if ZS_PARSE_PROF
+__device__ unsigned long long zs_pp_stat[8];  // pass A, phase 1 (B + counts), splice, block cuts, records, waves
+extern "C" int zs_parse_stats(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_pp_stat), sizeof(zs_pp_stat));
+}
+#define PP_T(v) unsigned long long v = wall_clock64()
+#define PP_ACC(i, v) do { if ((threadIdx.x & 63u) == 0) atomicAdd(&zs_pp_stat[i], wall_clock64() - v); } while (0)
+#else
+#define PP_T(v) do { } while (0)
+#define PP_ACC(i, v) do { } while (0)
+#endif
+
 template <uint32_t WIN, uint32_t SEG, uint32_t NWV>
 static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_seg_tab& T, zs_round_state& RS,
                                                      const uint8_t* __restrict__ in,
@@ -148,6 +163,7 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
     uint32_t* fix = sync + CF::SYNC;
 
     // ---- pass A: speculative parse of the lane's segment from the position-0 state
+    PP_T(tA);
     zs_pstate st = {a, 0, ZS_MIN_MATCH - 1, 0};
     uint32_t cnt = 0;
     {
@@ -236,6 +252,7 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
       }
     }
 
+    PP_ACC(0, tA);
     // Phase 1 (pass B + the round's symbol count) needs the true state entering
     // the round: the waves run it in round order.  Phase 2 (the splice) needs
     // only this round's results, so a wave's phase 2 overlaps the next wave's
@@ -245,6 +262,7 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
     for (uint32_t k = 0; k < NWV + (NWV > 1 ? 1u : 0u); k++) {
     if (NWV > 1) __syncthreads();
     if (nr != 0 && k == wave) {
+    PP_T(tB);
     if (NWV > 1) {
       t = RS.t;
       total = RS.total;
@@ -323,9 +341,11 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
       RS.t = t;
       RS.total = total;
     }
+    PP_ACC(1, tB);
     }  // phase 1
     if (nr != 0 && k == wave + (NWV > 1 ? 1u : 0u)) {
     ZS_WAVE_SYNC();
+    PP_T(tC);
     uint32_t js = 0, lastv = 0;
     for (uint32_t g0 = 0; g0 < R; g0 += 64 * ZS_GATHER) {
       uint32_t v[ZS_GATHER];
@@ -352,6 +372,8 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
       if (NWV > 1 && lane == 0) RS.last_sym = last_sym;  // rounds' phases 2 run in order
     }
 
+    PP_ACC(2, tC);
+    PP_T(tD);
     // block cuts: FLUSH_BLOCK after every 16383rd tallied symbol (deflate.ts:336,
     // 1120-1124) -- but not after the final deferred literal, which is tallied
     // after the loop (deflate.ts:1429-1432)
@@ -381,6 +403,7 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
         blk[bi].pad = zs_slides(end - li + 1, n);
       }
     }
+    PP_ACC(3, tD);
     ZS_WAVE_SYNC();
     }  // phase 2
     }  // handoff
@@ -393,6 +416,7 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
     last_sym = RS.last_sym;
   }
 
+  PP_T(tE);
   // ---- block records (deflate.ts:1434-1440: the final block takes the rest, possibly empty)
   const bool final_lit = nseg > 0 && t.ma != 0;
   const uint32_t checked = final_lit ? total - 1 : total;
@@ -425,6 +449,10 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
     streams[s].nsym = total;
     streams[s].nblk = nflush + 1;
   }
+  PP_ACC(4, tE);
+#if ZS_PARSE_PROF
+  if (lane == 0) atomicAdd(&zs_pp_stat[5], 1ull);
+#endif
 }
 
 #define ZS_PARSE_KERNEL(name, WIN, SEG, NWV)                                                                        \
