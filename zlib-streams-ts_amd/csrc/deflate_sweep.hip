@@ -78,6 +78,18 @@ static __device__ __forceinline__ uint32_t sw_hash(uint32_t w) {  // SURVEY A1, 
 // in registers, pass 2 a 4 KiB LDS stage of the input.  Results of the
 // positions that are not inserted (the last two) are zeroed.
 #define ZS_BK_THREADS 256u
+#ifndef ZS_BK_PROF
+#define ZS_BK_PROF 0  // timing experiments: wall-clock per pass summed over workgroups (0 in the product)
+#endif
+#if ZS_BK_PROF
+__device__ unsigned long long zs_bk_stat[4];  // pass 1, scan, pass 2, workgroups
+extern "C" int zs_bucket_stats(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_bk_stat), sizeof(zs_bk_stat));
+}
+#define BK_MARK(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); atomicAdd(&zs_bk_stat[i], t_ - bk_t); bk_t = t_; } } while (0)
+#else
+#define BK_MARK(i) do { } while (0)
+#endif
 #define ZS_BK_INFLIGHT 8  // pass 2: wave instructions (x 64 positions) per wait
 #define ZS_BK_CHUNK 2048u  // pass 2: positions per chunk (input bytes staged in LDS, slots queued)
 
@@ -102,6 +114,10 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
   if (m == 0) return;
   for (uint32_t i = tid; i < 16384 / 4; i += ZS_BK_THREADS) reinterpret_cast<uint4*>(cnt)[i] = make_uint4(0, 0, 0, 0);
   const bool aligned = ((uintptr_t)src & 3u) == 0;
+#if ZS_BK_PROF
+  unsigned long long bk_t = wall_clock64();
+  if (threadIdx.x == 0) atomicAdd(&zs_bk_stat[3], 1ull);
+#endif
   __syncthreads();
   // pass 1: bucket sizes (unordered adds, all waves).  Thread t hashes the 16
   // positions [p0 + 16 t, +16) from 5 input words; the next 4 KiB block's words
@@ -127,6 +143,7 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
     }
   }
   __syncthreads();
+  BK_MARK(0);
   // exclusive scan: thread i owns words [64i, 64i + 64) (buckets 128i ...)
   {
     uint32_t sum = 0;
@@ -162,6 +179,7 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
     }
   }
   __syncthreads();
+  BK_MARK(1);
   // pass 2: wave 0 claims the slots in position order, ZS_BK_CHUNK positions
   // at a time, into an LDS queue (slot of chunk position o at q[c & 1][o]);
   // waves 1..3 scatter the previous chunk's positions to their slots while it
@@ -242,6 +260,7 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
     }
     __syncthreads();
   }
+  BK_MARK(2);
 }
 
 // --------------------------------------------------------------- zs_k_sweep
