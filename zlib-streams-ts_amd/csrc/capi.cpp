@@ -951,7 +951,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
     uint32_t B = (uint32_t)c->lane_block;
     if (!B) {
       if (n <= 16384u)
-        for (B = 1; B < 64 && (n + B - 1) / B > 4096u;) B <<= 1;
+        for (B = 1; B < 64 && (n + B - 1) / B > 4608u;) B <<= 1;  // (~4096 waves; a few members over 8,192 keep two per wave)
       else
         for (B = 64; B > 8 && (n + B - 1) / B < 1024u;) B >>= 1;
     }
