@@ -210,9 +210,15 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * "lane_block" (default 0 = by batch size;
  * else 1..64, a power of two): members per workgroup of the inflate lane path;
  * "inflate_wave_min" (default 32768; 0 = never): members with more input bytes
- * decode one per wave (inflate_wave.hip) beside the lane kernel, in every
- * format (the wave kernel tracks the reference's inflate() calls, so it
- * reproduces the window-wrap copy below);
+ * are "large" and decode beside the lane kernel (side stream): deflate64 (and
+ * raw deflate with inflate_ref_wrap 0) by the split decode (inflate_split.hip:
+ * cut at block boundaries, pieces in parallel), the other formats one per wave
+ * (inflate_wave.hip) or, when a batch has lane_large_min of them or more, one
+ * per lane (the lane kernel's large-member instance) -- both track the
+ * reference's inflate() calls and so reproduce the window-wrap copy below;
+ * "inflate_split" (default 1; 0: large deflate64 members take the wave kernel);
+ * "lane_large_min" (default 512; 0: never): large-member count from which the
+ * lanes replace the wave kernel;
  * "parse_waves" (default 0 = two below 2048 streams, else one; 1, 2 or 4):
  * waves per stream of the levels 4..9 lazy parse (two: 512-position segments,
  * two rounds' speculative passes at once);
