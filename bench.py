@@ -163,6 +163,12 @@ def build_id():
 
 
 def profiled_traffic(kernel, kernel_ms, tag=None):
+    """`kernel`: a name or a list of names (template instances) tried in each file in turn."""
+    names = [kernel] if isinstance(kernel, str) else list(kernel)
+    return _profiled_traffic(names, kernel_ms, tag)
+
+
+def _profiled_traffic(names, kernel_ms, tag=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3
     summary (profiles/*/summary*.json: FETCH_SIZE / WRITE_SIZE passes, gfx950
     read correction by tools/summarize_profile.py) -- used only when that
@@ -172,33 +178,36 @@ def profiled_traffic(kernel, kernel_ms, tag=None):
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary*.json")))  # round directories sort in order
     files = _tagged_first(files, tag)
-    stale, hit = None, None
+    stale = None
     bid = build_id()
     for f in reversed(files):  # this config's files first, newest round first; the first matching duration
         try:
             j = json.load(open(f))
         except (OSError, ValueError):
             continue
-        e = j.get(kernel)
-        if not e or "hbm_bytes_corrected" not in e:
-            continue
-        if j.get("_build_id") != bid:
-            stale = stale or "stale: %s is of build %s, this is build %s" % (os.path.relpath(f, ROOT),
-                                                                              j.get("_build_id"), bid)
-            continue
-        prof_ms = e["avg_ns"] / 1e6
         src = os.path.relpath(f, ROOT)
-        if abs(prof_ms - kernel_ms) > 0.1 * kernel_ms:
-            stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
-            continue
-        if hit is None:  # this config's newest matching profile, else the newest matching one
-            hit = (0, int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms))
-    if hit:
-        return hit[1], hit[2]
-    return None, stale or "no committed profile for %s" % kernel
+        for kernel in names:
+            e = j.get(kernel)
+            if not e or "hbm_bytes_corrected" not in e:
+                continue
+            if j.get("_build_id") != bid:
+                stale = stale or "stale: %s is of build %s, this is build %s" % (src, j.get("_build_id"), bid)
+                continue
+            prof_ms = e["avg_ns"] / 1e6
+            if abs(prof_ms - kernel_ms) > 0.1 * kernel_ms:
+                stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
+                continue
+            return int(e["hbm_bytes_corrected"]), "%s (%s avg %.3f ms)" % (src, kernel, prof_ms)
+    return None, stale or "no committed profile for %s" % " / ".join(names)
 
 
 def profiled_ceilings(kernel, kernel_ms, tag=None):
+    """`kernel`: a name or a list of names (template instances) tried in each file in turn."""
+    names = [kernel] if isinstance(kernel, str) else list(kernel)
+    return _profiled_ceilings(names, kernel_ms, tag)
+
+
+def _profiled_ceilings(names, kernel_ms, tag=None):
     """The SQ-counter ratios that bound `kernel` below the HBM roofline, from the
     newest committed tools/pmc_sq.sh summary (profiles/*/sq_summary*.json,
     written by tools/sq_summary.py --json): LDS bank-conflict cycles over LDS
@@ -210,32 +219,30 @@ def profiled_ceilings(kernel, kernel_ms, tag=None):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sq_summary*.json")) +
                    glob.glob(os.path.join(ROOT, "profiles", "*", "*", "sq_summary*.json")))
     files = _tagged_first(files, tag)
-    stale, hit = None, None
+    stale = None
     bid = build_id()
     for f in reversed(files):  # this config's files first, newest round first; the first matching duration
         try:
             j = json.load(open(f))
         except (OSError, ValueError):
             continue
-        e = j.get(kernel)
-        if not e:
-            continue
         src = os.path.relpath(f, ROOT)
-        if j.get("_build_id") != bid:
-            stale = stale or "stale: %s is of build %s, this is build %s" % (src, j.get("_build_id"), bid)
-            continue
-        prof_ms = e["avg_ns"] / 1e6
-        if abs(prof_ms - kernel_ms) > 0.15 * kernel_ms:
-            stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
-            continue
-        if hit is None:
+        for kernel in names:
+            e = j.get(kernel)
+            if not e:
+                continue
+            if j.get("_build_id") != bid:
+                stale = stale or "stale: %s is of build %s, this is build %s" % (src, j.get("_build_id"), bid)
+                continue
+            prof_ms = e["avg_ns"] / 1e6
+            if abs(prof_ms - kernel_ms) > 0.15 * kernel_ms:
+                stale = stale or "stale: %s has %s at %.3f ms, this run %.3f ms" % (src, kernel, prof_ms, kernel_ms)
+                continue
             out = {k: e[k] for k in ("lds_bank_conflict_frac", "valu_busy", "active_frac_of_wave_cycles",
                                      "wait_frac_of_wave_cycles", "wait_inst_frac_of_wave_cycles") if k in e}
             out["source"] = "%s (%s avg %.3f ms under --pmc)" % (src, kernel, prof_ms)
-            hit = (0, out)
-    if hit:
-        return hit[1]
-    return {"source": stale or "no committed SQ summary for %s" % kernel}
+            return out
+    return {"source": stale or "no committed SQ summary for %s" % " / ".join(names)}
 
 
 def timed_port(fn, items, seconds, threads):
@@ -457,7 +464,8 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = in_total / (elapsed / args.steps) / 1e6
         phase_avg = {k: round(v / args.steps, 4) for k, v in phases.items()}
-        dom = max(phase_avg, key=phase_avg.get) if phase_avg else None
+        # the dominant KERNEL phase (inflate_join is the caller's stream waiting for the side stream)
+        dom = max((k for k in phase_avg if k not in ("inflate_join", "finish")), key=phase_avg.get) if phase_avg else None
         roof = None
         if dom:
             # bytes_in + bytes_out per stream x streams per launch (this rank's shard)
@@ -629,7 +637,8 @@ def main_inflate(args):
         assert bad == 0, "%d of %d members decode wrong" % (bad, checked)
     if D.rank == 0:
         phase_avg = {k: round(v / args.steps, 4) for k, v in phases.items()}
-        dom = max(phase_avg, key=phase_avg.get)
+        # the dominant KERNEL phase (inflate_join is the caller's stream waiting for the side stream)
+        dom = max((k for k in phase_avg if k not in ("inflate_join", "finish")), key=phase_avg.get)
         k_ms = phase_avg[dom]
         alg = in_local + out_local  # compressed_in + uncompressed_out per member
         if dom in ("inflate_wave", "inflate_large"):  # only the members with more input than inflate_wave_min
@@ -643,16 +652,9 @@ def main_inflate(args):
                                     "zs_k_inflate_lane<2,false>"],
                    "inflate_large": ["zs_k_inflate_lane<2,true>", "zs_k_inflate_lane<0,true>"],
                    "inflate_wave": ["zs_k_inflate_wave<true>", "zs_k_inflate_wave<false>"]}.get(dom, ["zs_k_" + dom])
-        for kern in kernels:
-            traffic, tsrc = profiled_traffic(kern, k_ms, profile_tag(args))
-            if traffic is not None:
-                break
-        ceil = None
-        for kc in kernels:
-            ceil = profiled_ceilings(kc, k_ms, profile_tag(args))
-            if ceil and "source" in ceil and not str(ceil["source"]).startswith(("stale", "no ")):
-                break
-        kern = kern if traffic is not None else kernels[0]
+        traffic, tsrc = profiled_traffic(kernels, k_ms, profile_tag(args))
+        ceil = profiled_ceilings(kernels, k_ms, profile_tag(args))
+        kern = tsrc.split(" (")[1].split(" avg")[0] if traffic is not None else kernels[0]
         cpu = None
         if not (args.no_cpu_baseline or D.world > 1):
             import oracle
