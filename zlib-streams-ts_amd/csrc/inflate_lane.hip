@@ -435,6 +435,11 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
   const bool ref_wrap = (flags & ZS_INF_REF_WRAP) != 0 && !d64 && !REFW;
   const uint32_t cap = ref_wrap ? min(out_cap[s], 65536u) : out_cap[s];
   zs_refcalls_t<uint32_t> C;  // (the host routes members of under 512 MB here: bit positions fit 32 bits)
+#if ZS_IL_EXP & 256  // timing experiments: the bookkeeping skipped (wrong bytes where the defect applies)
+#define REFW_SYM(...) false
+#else
+#define REFW_SYM(...) C.symbol(__VA_ARGS__)
+#endif
   C.init();
   const uint32_t lmask = d64 ? 31u : 15u;  // length extra-bit mask (inflate.ts:891)
   uint32_t total = 0;
@@ -569,13 +574,13 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
       uint32_t op = C_OP(here);
       if (op == 0) {
         if (total >= cap) { bail = true; break; }
-        if (REFW) C.symbol(b0, total, 1u, l1, 0u, 0u, 0u, false);
+        if (REFW) REFW_SYM(b0, total, 1u, l1, 0u, 0u, 0u, false);
         W.byte(C_VAL(here));
         total++;
         continue;
       }
       if (op & 32) {  // end of block
-        if (REFW) C.symbol(b0, total, 0u, l1, 0u, 0u, 0u, true);
+        if (REFW) REFW_SYM(b0, total, 0u, l1, 0u, 0u, 0u, true);
         break;
       }
       if (op & 64) { bail = true; break; }  // "invalid literal/length code"
@@ -602,7 +607,7 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
       // copy -- its last `tail` bytes taken from the current call's first output
       // bytes (C.B on), i.e. a second copy at distance total + head - C.B
       uint32_t tail = 0;
-      if (REFW && C.symbol(b0, total, len, l1, e1, L, op & 15u, false)) tail = C.wrap(total, len, dist0);
+      if (REFW && REFW_SYM(b0, total, len, l1, e1, L, op & 15u, false)) tail = C.wrap(total, len, dist0);
       const uint32_t len_all = len;
       for (uint32_t part = 0; part < (REFW ? 2u : 1u); part++) {
       const uint32_t dist = part == 0 ? dist0 : total - C.B;  // (total has moved past the head)

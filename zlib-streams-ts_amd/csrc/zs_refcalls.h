@@ -28,7 +28,7 @@ struct zs_refcalls_t {
   uint32_t wn, wh;  // w_next, w_have when it began
   uint32_t cend;    // input byte where the current sub-chunk ends
   uint32_t fast;    // inside inflate_fast
-  uint32_t fin, fbits;  // inflate_fast's pulled bytes (member offset) and bit count
+  uint32_t fin;  // inflate_fast's pulled bytes (member offset); its bit count is 8 fin - the bits consumed
   __device__ __forceinline__ void init() {
     B = 0;
     wn = 0;
@@ -55,12 +55,10 @@ struct zs_refcalls_t {
     B = at;
     fast = 0;
   }
-  __device__ __forceinline__ void pull(uint32_t need) {  // whole bytes until fbits >= need
-    if (fbits < need) {
-      const uint32_t k = (need - fbits + 7u) >> 3;
-      fin += k;
-      fbits += 8u * k;
-    }
+  // inflate_fast pulls whole bytes until it holds `need` bits past bit position pos: with its bit count
+  // 8 fin - pos, that is fin = max(fin, ceil((pos + need) / 8))
+  __device__ __forceinline__ void pull_to(PT pos_plus_need) {
+    fin = max(fin, (uint32_t)((pos_plus_need + 7u) >> 3));
   }
   // a symbol with bits [sb, sb + l1 + e1 + l2 + e2) writing len bytes at o;
   // true iff inflate_fast runs it whole
@@ -93,24 +91,23 @@ struct zs_refcalls_t {
       if (cend - pulled >= 6u && B + 65536u - o >= 258u) {
         fast = 1;
         fin = pulled;
-        fbits = (uint32_t)((PT)8u * pulled - sb);
       } else {
         return false;
       }
     }
-    pull(15u);
-    fbits -= l1;
+    // pulls: 15 bits at the code (sb), then for a length / distance pair e1 at
+    // sb + l1, 15 at sb + l1 + e1 and e2 at sb + l1 + e1 + l2 -- whose largest
+    // requirement is one of the last two
     if (eob) {
+      pull_to(sb + 15u);
       fast = 0;
       return true;
     }
-    if (len > 1u || l2) {  // a length / distance pair
-      pull(e1);
-      fbits -= e1;
-      pull(15u);
-      fbits -= l2;
-      pull(e2);
-      fbits -= e2;
+    if (len > 1u || l2) {
+      const PT d = sb + l1 + e1;
+      pull_to(max(d + 15u, d + l2 + e2));
+    } else {
+      pull_to(sb + 15u);
     }
     if (!(fin < cend - 5u && o + len < B + 65536u - 257u)) fast = 0;  // the fast loop's condition
     return true;
