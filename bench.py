@@ -599,7 +599,7 @@ def main_inflate(args):
         step()  # back to back: the phase events are read after the timed region
     D.barrier()
     elapsed = D.max(time.perf_counter() - t0)
-    for ph in ("inflate_lane", "inflate_wave", "inflate_large", "split_find", "split_decode", "split_resolve",
+    for ph in ("inflate_lane", "inflate_long", "inflate_wave", "inflate_large", "split_find", "split_decode", "split_resolve",
                "inflate_join", "inflate_check", "inflate", "finish"):
         v = eng.last_ms(ph)  # summed over the timed steps
         if v >= 0:

@@ -4,7 +4,8 @@ markers for the unknown history, then resolved in order.  It must produce
 exactly what the one-piece paths produce -- the wave kernel and the exact
 stream-layer kernel (inflate.ts:332-1185) -- bytes, statuses, phases and
 messages, for the reference's deflate64 fixtures (test/data, pinned by
-inflate_small.json) and for raw deflate without the window-wrap copy."""
+inflate_small.json) and for raw deflate without the window-wrap copy; and of
+the lane kernel's large-member instance, which tracks the reference's calls."""
 import hashlib
 import json
 import os
@@ -30,7 +31,8 @@ def _fixtures():
 class _opts:
     """Engine options for the duration of a block (restored to the defaults after)."""
 
-    DEFAULTS = {"inflate_split": 1, "inflate_wave_min": 32768, "inflate_ref_wrap": 1, "inflate_fast": 1}
+    DEFAULTS = {"inflate_split": 1, "inflate_wave_min": 32768, "inflate_ref_wrap": 1, "inflate_fast": 1,
+                "lane_large_min": 512}
 
     def __init__(self, engine, **kw):
         self.e, self.kw = engine, kw
@@ -134,3 +136,43 @@ def test_unbounded_decode_of_a_large_member(engine):
     d, n, h = fx["100k_lines.deflate64"]
     out = engine.decompress_batch([d, fx["10k_lines.deflate64"][0]], "deflate64-raw")
     assert hashlib.sha256(out[0]).hexdigest() == h and len(out[1]) == fx["10k_lines.deflate64"][1]
+
+
+@pytest.mark.parametrize("fmt", ["deflate-raw", "deflate", "gzip"])
+def test_large_member_lanes_equal_the_reference_and_the_exact_path(engine, fmt):
+    """The lane kernel's large-member instance (the reference's inflate() calls
+    tracked per lane; used when a batch has lane_large_min large members, here
+    forced with a small minimum) in every wrapped format: clean members equal the
+    oracle with the reference's window-wrap copy (reference_bugs), damaged ones
+    the exact kernel's status / phase / message / bytes."""
+    rng = random.Random(4242)
+    members, caps = [], []
+    for k in range(24):
+        s = corpus.make({"kind": rng.choice(["text", "mixed"]), "n": rng.choice([70000, 150000, 262144]),
+                         "seed": rng.randrange(1 << 32)})
+        c = oracle.compress(s, rng.choice([1, 6, 9]), fmt)[1]
+        if k % 6 == 5:  # damaged: a bit flip or a truncation
+            b = bytearray(c)
+            if k % 12 == 5:
+                b[rng.randrange(len(b) // 2, len(b))] ^= 1 << rng.randrange(8)
+            else:
+                b = b[:rng.randrange(len(b) // 2, len(b))]
+            c = bytes(b)
+        members.append(c)
+        caps.append((len(s) + 64 + 3) & ~3)
+    j = json.load(open(os.path.join(ROOT, "tests", "golden", "inffast_wrap_defect.json")))
+    if fmt == "deflate-raw":  # the member whose decode the reference's defect changes
+        src = corpus.make(j["source"])
+        members.append(oracle.compress(src, 6, fmt)[1])
+        caps.append((len(src) + 64 + 3) & ~3)
+    got, fast = _decode(engine, members, fmt, caps, lane_large_min=4)
+    want, _ = _decode(engine, members, fmt, caps, inflate_fast=0)
+    for i, (g, w, c, cap) in enumerate(zip(got, want, members, caps)):
+        assert g == w, i
+        ost, oout, ocons, oph, omsg = oracle.decompress(c, fmt, cap=cap, reference_bugs=True)
+        assert g[0] == ost, (i, g[0], g[1], g[2], ost, oph, omsg)
+        if ost == 1:
+            assert g[3] == oout and g[4] == ocons, (i, len(g[3]), len(oout))
+    assert fast >= sum(1 for w in want if w[0] == 1)  # every clean member finished on the lanes
+    if fmt == "deflate-raw":
+        assert corpus.sha256(got[-1][3]) == j["ref_out_sha256"]

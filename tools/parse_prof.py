@@ -9,6 +9,8 @@ import zsamd
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 e = zsamd.Engine(0)
+if len(sys.argv) > 2:
+    e.set_option("parse_waves", int(sys.argv[2]))
 buf = bytes(zsamd.corpus("text", 0, n, 65536))
 ins = [buf[i * 65536:(i + 1) * 65536] for i in range(n)]
 e.compress_batch_raw(ins, "deflate-raw", 6)

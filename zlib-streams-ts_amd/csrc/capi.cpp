@@ -1096,6 +1096,18 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       zs_k_inflate_lane<0, false><<<lgrid, B, lsm, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, n, lt, lres,
                                                          c->llen.as<uint32_t>(), lflags, wave_min, nullptr);
     MARK("inflate_lane");
+    // Members the single-call instance bailed on whose cap allows more than one
+    // inflate() call of the reference (more than 32 KiB of input, or output past
+    // 64 KiB): re-run by the call-tracking instance, here, before the exact kernel
+    if (c->inflate_ref_wrap && wbits != -16) {
+      const size_t lsmr = 64 * zs_inflate_lane_lds_bytes(false);
+      HIPCHK(hipFuncSetAttribute((const void*)zs_k_inflate_lane<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lsmr));
+      zs_k_inflate_lane<0, true><<<(n + 63) / 64, 64, lsmr, st>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
+                                                                  n, lt, lres, c->llen.as<uint32_t>(), ZS_INF_REF_WRAP,
+                                                                  wave_min, nullptr);
+      MARK("inflate_long");
+    }
     if (wave_min) {
       HIPCHK(hipStreamWaitEvent(st, c->join, 0));
       MARK("inflate_join");  // the caller's stream waiting for the wave kernel beyond the lane kernel

@@ -389,7 +389,12 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
   constexpr uint32_t lstride = ROOT ? sizeof(zs_lane_lds_root) : sizeof(zs_lane_lds);
   const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= n_members) return;
-  const uint32_t s = REFW ? list[li] : li;
+  // REFW with a list: the large members; without one (retry mode): every member the
+  // single-call instance bailed on that may be longer than one inflate() call of the
+  // reference (a caller's cap past 64 KiB), except large ones.  A member that fails
+  // for another reason fails here again and goes on to the exact path.
+  const uint32_t s = REFW && list ? list[li] : li;
+  if (REFW && !list && (res[s].bail == 0 || out_cap[s] <= 65536u || (wave_min && in_len[s] > wave_min))) return;
   // a large member: the REFW instance, zs_k_inflate_wave or the split path decodes it
   if (!REFW && wave_min && in_len[s] > wave_min) return;
   zs_lane_tabs& T = tabs[s];
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
   uint32_t total = 0;
   zs_lane_res r = {1u, 0u, 0u, 0u};
   const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
-  bool bail = ref_wrap && R.n > 32768u;  // several sub-chunks: exact path
+  bool bail = ref_wrap && R.n > 32768u;  // several sub-chunks: the call-tracking instance
   // ---- wrapper header (inflate.ts:377-580): plain zlib / gzip headers only
   if (!bail && wrap) {
     const uint32_t b0 = zs_lr_take(R, 8), b1 = zs_lr_take(R, 8);
