@@ -3,7 +3,7 @@
 # BASELINE config's bench line, then rocprofv3 kernel trace + FETCH/WRITE passes
 # and SQ counter passes per config.  Logs and summaries under $1; copy the
 # summaries into profiles/<round>/ (tools/collect_r03.sh).
-# usage: tools/measure_r03.sh OUTDIR [benches|profiles|sq|all]
+# usage: tools/measure_r03.sh OUTDIR [benches|profiles|sq|sq2|all]   (sq2: the SQ passes of the C4-L9 / C5 configs only)
 set -u
 OUT=$1
 WHAT=${2:-all}
@@ -49,5 +49,11 @@ run sq_c2 500 tools/pmc_sq.sh "$OUT/sq_c2"
 run sq_c3 500 tools/pmc_sq.sh "$OUT/sq_c3" $C3
 run sq_c4_l1 500 tools/pmc_sq.sh "$OUT/sq_c4_l1" $C4L1
 run sq_c4_decode 500 tools/pmc_sq.sh "$OUT/sq_c4_decode" $C4D
+fi
+if [ "$WHAT" = sq ] || [ "$WHAT" = sq2 ] || [ "$WHAT" = all ]; then
+run sq_c5_gunzip 500 tools/pmc_sq.sh "$OUT/sq_c5_gunzip" $C5I
+run sq_c5_d64 500 tools/pmc_sq.sh "$OUT/sq_c5_d64" $C5D
+run sq_c5_gzip_l6 500 tools/pmc_sq.sh "$OUT/sq_c5_gzip_l6" $C5G
+run sq_c4_l9 500 tools/pmc_sq.sh "$OUT/sq_c4_l9" $C4L9
 fi
 echo measure-done
