@@ -28,13 +28,21 @@ struct zs_refcalls_t {
   uint32_t wn, wh;  // w_next, w_have when it began
   uint32_t cend;    // input byte where the current sub-chunk ends
   uint32_t fast;    // inside inflate_fast
-  uint32_t fin;  // inflate_fast's pulled bytes (member offset); its bit count is 8 fin - the bits consumed
+  // symbols starting below both are far from the call's ends (see symbol())
+  PT sfar;        // 8 cend - 96
+  uint32_t ofar;  // B + 65536 - 516
   __device__ __forceinline__ void init() {
     B = 0;
     wn = 0;
     wh = 0;
     cend = 32768u;
     fast = 0;
+    sfar = (PT)8u * cend - 96u;
+    ofar = 65536u - 516u;
+  }
+  __device__ __forceinline__ void next_chunk() {
+    cend += 32768u;
+    sfar = (PT)8u * cend - 96u;
   }
   __device__ __forceinline__ void end_call(uint32_t at) {
     const uint32_t produced = at - B;
@@ -53,29 +61,32 @@ struct zs_refcalls_t {
       }
     }
     B = at;
+    ofar = at + 65536u - 516u;
     fast = 0;
-  }
-  // inflate_fast pulls whole bytes until it holds `need` bits past bit position pos: with its bit count
-  // 8 fin - pos, that is fin = max(fin, ceil((pos + need) / 8))
-  __device__ __forceinline__ void pull_to(PT pos_plus_need) {
-    fin = max(fin, (uint32_t)((pos_plus_need + 7u) >> 3));
   }
   // a symbol with bits [sb, sb + l1 + e1 + l2 + e2) writing len bytes at o;
   // true iff inflate_fast runs it whole
-  // (the common case -- inside the current call's sub-chunk and buffer --
-  // skips the boundary logic)
   __device__ __forceinline__ bool symbol(PT sb, uint32_t o, uint32_t len, uint32_t l1, uint32_t e1, uint32_t l2,
                                          uint32_t e2, bool eob) {
-    if (__builtin_expect(o < B + 65536u && sb + l1 + e1 + l2 + e2 <= (PT)8u * cend, 1))
-      return in_call(sb, o, len, l1, e1, l2, e2, eob);
+    // Far from both ends of the call (sb + 96 bits below the sub-chunk's end, o
+    // + 516 below the buffer's): the LEN state's test passes (>= 12 bytes and
+    // >= 516 bytes left) and so does the fast loop's after the symbol (its
+    // pulls reach at most sb + 48 bits, below 8 (cend - 5) - 7; o + len <= o +
+    // 258 < B + 65279), so inflate_fast runs it and goes on unless it is the
+    // end of block -- nothing else to track.
+    if (__builtin_expect(sb < sfar && o < ofar, 1)) {
+      fast = !eob;
+      return true;
+    }
+    if (o < B + 65536u && sb + l1 + e1 + l2 + e2 <= (PT)8u * cend) return in_call(sb, o, len, l1, e1, l2, e2, eob);
     if (o > B + 65536u) end_call(B + 65536u);  // the copy before filled the buffer
     while (sb >= (PT)8u * cend) {  // sub-chunks that ended before the symbol
       end_call(o);
-      cend += 32768u;
+      next_chunk();
     }
     if (sb + l1 + e1 + l2 + e2 > (PT)8u * cend) {  // crosses the sub-chunk's end: the next call's slow path
       end_call(o);
-      cend += 32768u;
+      next_chunk();
       return false;
     }
     if (o >= B + 65536u) {  // the buffer is full: the next call's slow path writes it
@@ -88,28 +99,23 @@ struct zs_refcalls_t {
                                           uint32_t e2, bool eob) {
     if (!fast) {  // the LEN state (inflate.ts): have >= 6 && left >= 258
       const uint32_t pulled = (uint32_t)((sb + 7u) >> 3);
-      if (cend - pulled >= 6u && B + 65536u - o >= 258u) {
-        fast = 1;
-        fin = pulled;
-      } else {
-        return false;
-      }
+      if (!(cend - pulled >= 6u && B + 65536u - o >= 258u)) return false;
+      fast = 1;
     }
-    // pulls: 15 bits at the code (sb), then for a length / distance pair e1 at
-    // sb + l1, 15 at sb + l1 + e1 and e2 at sb + l1 + e1 + l2 -- whose largest
-    // requirement is one of the last two
     if (eob) {
-      pull_to(sb + 15u);
       fast = 0;
       return true;
     }
-    if (len > 1u || l2) {
-      const PT d = sb + l1 + e1;
-      pull_to(max(d + 15u, d + l2 + e2));
-    } else {
-      pull_to(sb + 15u);
-    }
-    if (!(fin < cend - 5u && o + len < B + 65536u - 257u)) fast = 0;  // the fast loop's condition
+    // inflate_fast pulls whole bytes until it holds the bits a step needs: 15 at
+    // the code (sb), then for a length / distance pair e1 at sb + l1, 15 at
+    // sb + l1 + e1 and e2 at sb + l1 + e1 + l2 -- the largest requirement is one
+    // of the last two.  Its pulled count fin = max(fin, ceil(req / 8)) only
+    // grows and passed the loop's test fin < cend - 5 at the previous step (or
+    // is the LEN state's, below it), so after this step the test is this
+    // step's own: ceil(req / 8) < cend - 5, i.e. req + 7 < 8 (cend - 5).
+    const PT d = sb + l1 + e1;
+    const PT req = (len > 1u || l2) ? max(d + 15u, d + l2 + e2) : sb + 15u;
+    if (!(req + 7u < (PT)8u * (cend - 5u) && o + len < B + 65536u - 257u)) fast = 0;  // the fast loop's condition
     return true;
   }
   // a stored block's len bytes at input byte in, output o (the COPY state: the slow path)
@@ -118,7 +124,7 @@ struct zs_refcalls_t {
     while (len) {
       while (in >= cend) {
         end_call(o);
-        cend += 32768u;
+        next_chunk();
       }
       if (o >= B + 65536u) end_call(B + 65536u);
       const uint32_t take = min(len, min(cend - in, B + 65536u - o));
