@@ -176,3 +176,29 @@ def test_large_member_lanes_equal_the_reference_and_the_exact_path(engine, fmt):
     assert fast >= sum(1 for w in want if w[0] == 1)  # every clean member finished on the lanes
     if fmt == "deflate-raw":
         assert corpus.sha256(got[-1][3]) == j["ref_out_sha256"]
+
+
+@pytest.mark.parametrize("fmt", ["deflate-raw", "gzip"])
+def test_retry_pass_decodes_large_members_on_the_lanes(engine, fmt):
+    """inflate_wave_min = 0: every member starts on the single-call lanes, which
+    bail on those longer than one reference inflate() call; the retry pass (the
+    call-tracking instance, no member list) must finish the clean ones -- equal
+    to the exact kernel and to the oracle with the reference's defect -- and
+    leave damaged ones to the exact path."""
+    rng = random.Random(777)
+    members, caps = [], []
+    for k in range(16):
+        s = corpus.make({"kind": rng.choice(["text", "mixed"]), "n": rng.choice([20000, 70000, 150000]),
+                         "seed": rng.randrange(1 << 32)})
+        c = oracle.compress(s, rng.choice([1, 6, 9]), fmt)[1]
+        if k % 8 == 7:
+            c = c[:len(c) * 3 // 4]  # truncated
+        members.append(c)
+        caps.append((len(s) + 64 + 3) & ~3)
+    got, fast = _decode(engine, members, fmt, caps, inflate_wave_min=0)
+    want, _ = _decode(engine, members, fmt, caps, inflate_fast=0)
+    assert got == want
+    for g, c, cap in zip(got, members, caps):
+        ost, oout, ocons, oph, omsg = oracle.decompress(c, fmt, cap=cap, reference_bugs=True)
+        assert g[0] == ost and (ost != 1 or (g[3] == oout and g[4] == ocons))
+    assert fast >= sum(1 for w in want if w[0] == 1)
