@@ -217,7 +217,7 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * per lane (the lane kernel's large-member instance) -- both track the
  * reference's inflate() calls and so reproduce the window-wrap copy below;
  * "inflate_split" (default 1; 0: large deflate64 members take the wave kernel);
- * "lane_large_min" (default 512; 0: never): large-member count from which the
+ * "lane_large_min" (default 2304; 0: never): large-member count from which the
  * lanes replace the wave kernel;
  * "parse_waves" (default 0 = two below 2048 streams, else one; 1, 2 or 4):
  * waves per stream of the levels 4..9 lazy parse (two: 512-position segments,

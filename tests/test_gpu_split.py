@@ -32,7 +32,7 @@ class _opts:
     """Engine options for the duration of a block (restored to the defaults after)."""
 
     DEFAULTS = {"inflate_split": 1, "inflate_wave_min": 32768, "inflate_ref_wrap": 1, "inflate_fast": 1,
-                "lane_large_min": 512}
+                "lane_large_min": 2304}
 
     def __init__(self, engine, **kw):
         self.e, self.kw = engine, kw

@@ -97,7 +97,7 @@ struct zs_ctx {
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
   uint32_t inflate_wave_min = 32768;  // members with more input bytes decode one per wave (inflate_wave.hip); 0: never
-  uint32_t lane_large_min = 512;      // this many large members or more: one LANE each (zs_k_inflate_lane<.., true>)
+  uint32_t lane_large_min = 2304;     // this many large members or more: one LANE each (zs_k_inflate_lane<.., true>); 256 KiB members: wave kernel 26.9 / 68.5 / 128 ms at 1024 / 2048 / 4096, lanes 68.6 / 78.3 / 77.7
   hipStream_t side = nullptr;         // second stream: the wave-per-member kernel runs beside the lane kernel
   hipEvent_t fork = nullptr, join = nullptr;
   Buf wlist;
