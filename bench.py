@@ -635,6 +635,32 @@ def main_inflate(args):
             bad += not ok
         checked, bad = D.sum(checked), D.sum(bad)
         assert bad == 0, "%d of %d members decode wrong" % (bad, checked)
+    extra = {}
+    if D.world == 1 and D.rank == 0 and not args.no_shard_sweep:
+        # what rank 0 decodes at 8 / 4 / 2 GPUs: the first shard_range(., G, 0) members of the same
+        # global list (same device buffers, one GPU), each size timed over --steps back-to-back batches
+        def step_n(m):
+            eng.decompress_device(dec_fmt, m, d_in.data_ptr(), in_off, in_len, d_out.data_ptr(), out_off, out_cap,
+                                  d_status.data_ptr(), d_phase.data_ptr(), d_msg.data_ptr(), d_len.data_ptr(),
+                                  d_cons.data_ptr(), stream.cuda_stream)
+        sweep = {}
+        for g in (8, 4, 2):
+            m = shard.shard_range(N, g, 0)[1]
+            if m < 1 or m >= N:
+                continue
+            step_n(m)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                step_n(m)
+            torch.cuda.synchronize()
+            sweep[str(m)] = round((time.perf_counter() - t1) / args.steps * 1e3, 4)
+            assert int((d_status[:m] != 1).sum()) == 0, "shard of %d members failed" % m
+        sweep[str(N)] = round(elapsed / args.steps * 1e3, 4)
+        extra["shard_sweep_ms"] = sweep
+        m8 = str(shard.shard_range(N, 8, 0)[1])
+        if m8 in sweep:
+            extra["implied_1_to_8_speedup"] = round(sweep[str(N)] / sweep[m8], 3)
     if D.rank == 0:
         phase_avg = {k: round(v / args.steps, 4) for k, v in phases.items()}
         # the dominant KERNEL phase (inflate_join is the caller's stream waiting for the side stream)
@@ -682,6 +708,7 @@ def main_inflate(args):
                          "ceilings": ceil},
             "cpu_baseline": cpu,
         }
+        line.update(extra)
         print(json.dumps(line), flush=True)
     D.close()
 

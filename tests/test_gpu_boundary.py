@@ -218,13 +218,14 @@ def test_large_members_decode_as_the_reference(engine):
     """4,096 T-corpus 256 KiB streams at deflate-raw L6 (compressed here and
     checked against the reference's compress golden) decoded with default
     options, as DecompressionStream decodes them: ~100 KB of input each, so
-    every member goes through the wave kernel (inflate_wave.hip), which tracks
-    the reference's inflate() calls (32 KiB input sub-chunks, 64 KiB output
-    buffers, streams.ts:78-93) and reproduces the window-wrap copy of
-    inffast.ts:127-147.  Bytes = tests/golden/batch_t256_l6_raw_dec.bin (the
-    reference's own decode; it differs from the source for some members);
-    no member falls back to the exact kernel; the exact kernel agrees on the
-    members the copy changes."""
+    every member is "large" and takes the path the host picks for a batch of
+    4,096 large members (capi.cpp), which tracks the reference's inflate()
+    calls (32 KiB input sub-chunks, 64 KiB output buffers, streams.ts:78-93)
+    and reproduces the window-wrap copy of inffast.ts:127-147.  Bytes =
+    tests/golden/batch_t256_l6_raw_dec.bin (the reference's own decode; it
+    differs from the source for some members); no member falls back to the
+    exact kernel; the exact kernel agrees on the members the copy changes.
+    The per-rank shard sizes of the 8-GPU configs are test_large_member_shard_*."""
     import zsamd
 
     L, N = 262144, 4096
@@ -247,3 +248,81 @@ def test_large_members_decode_as_the_reference(engine):
     finally:
         engine.set_option("inflate_fast", 1)
     assert all(exact[k] == outs[i] for k, i in enumerate(changed))
+
+
+def _t256_l6_raw(engine, lo, hi):
+    import zsamd
+
+    L = 262144
+    buf = bytes(zsamd.corpus("text", lo, hi - lo, L))
+    srcs = [buf[i * L:(i + 1) * L] for i in range(hi - lo)]
+    comps = engine.compress_batch(srcs, "deflate-raw", 6)
+    recs = golden_io.batch("t256_l6_raw")[lo:hi]
+    assert all((len(c), hashlib.sha256(c).digest()[:16]) == r for c, r in zip(comps, recs))
+    return srcs, comps
+
+
+@pytest.mark.parametrize("n", [512, 64, 1])
+def test_large_member_shard_decodes_as_the_reference(engine, n):
+    """BASELINE configs[3] at the per-rank size of 8 GPUs: a shard of the 4,096
+    T-corpus 256 KiB L6 streams (streams 0..n-1) decoded with default options
+    -- the path the host picks for a batch of few large members -- against the
+    reference's OWN decode of each (batch_t256_l6_raw_dec.bin, DecompressionStream
+    with one write(), window-wrap copy of inffast.ts:127-147 included), every
+    member finished without the exact kernel."""
+    L = 262144
+    srcs, comps = _t256_l6_raw(engine, 0, n)
+    outs = engine.decompress_batch(comps, "deflate-raw", [L] * n)
+    assert engine.last_lane_count() == n
+    drecs = golden_io.batch("t256_l6_raw_dec")[:n]
+    bad = [i for i, o in enumerate(outs) if (len(o), hashlib.sha256(o).digest()[:16]) != drecs[i]]
+    assert not bad, bad[:10]
+
+
+def test_mixed_large_members_with_window_wrap_copies(engine):
+    """M-corpus members of 200-500 KB at L6 / L9: the reference's window-wrap
+    copy (inffast.ts:127-147) fires in most of them (short inflate() calls in
+    output over the incompressible kilobytes).  Every member equals the oracle
+    with the reference's defect (reference_bugs) and the exact kernel."""
+    import random
+
+    rng = random.Random(2024)
+    members, caps, want, srcs = [], [], [], []
+    for k in range(24):
+        n = rng.choice([200000, 262144, 500000])
+        s = corpus.mixed(corpus.stream_seed(rng.randrange(4096)), n)
+        c = oracle.compress(s, rng.choice([6, 9]), "deflate-raw")[1]
+        members.append(c)
+        srcs.append(s)
+        caps.append((n + 3) & ~3)
+        want.append(oracle.decompress(c, "deflate-raw", cap=n, reference_bugs=True))
+    assert any(w[1] != s for w, s in zip(want, srcs))  # the set exercises the window-wrap copy
+    got = engine.decompress_batch_raw(members, "deflate-raw", caps)
+    assert engine.last_lane_count() == len(members)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g[0] == 1 and g[3] == w[1] and g[4] == w[2], i
+    try:
+        engine.set_option("inflate_fast", 0)
+        exact = engine.decompress_batch_raw(members, "deflate-raw", caps)
+    finally:
+        engine.set_option("inflate_fast", 1)
+    assert exact == got
+
+
+@pytest.mark.slow
+def test_c5_gunzip_shard_of_1024_members(engine):
+    """C5-i at the per-rank size of 8 GPUs: gzip members 0..1023 of the C5 set
+    (pinned by the reference golden batch_t64_l6_gzip) gunzipped with default
+    options, each equal to its source with its CRC-32 check value."""
+    import zsamd
+
+    N, L = 1024, 65536
+    host = zsamd.corpus("text", 0, N, L)
+    src = [bytes(host[i * L:(i + 1) * L]) for i in range(N)]
+    gz = engine.compress_batch(src, "gzip", 6)
+    recs = golden_io.batch("t64_l6_gzip")[:N]
+    assert all((len(c), hashlib.sha256(c).digest()[:16]) == r for c, r in zip(gz, recs))
+    res = engine.decompress_batch_detailed(gz, "gzip", [L] * N)
+    assert engine.last_lane_count() == N
+    for s, r in zip(src, res):
+        assert r[0] == 1 and r[3] == s and (r[5] & 0xffffffff) == zlib.crc32(s)

@@ -202,3 +202,25 @@ def test_retry_pass_decodes_large_members_on_the_lanes(engine, fmt):
         ost, oout, ocons, oph, omsg = oracle.decompress(c, fmt, cap=cap, reference_bugs=True)
         assert g[0] == ost and (ost != 1 or (g[3] == oout and g[4] == ocons))
     assert fast >= sum(1 for w in want if w[0] == 1)
+
+
+@pytest.mark.parametrize("path", ["lanes", "wave", "split", "exact"])
+def test_deflate64_copies_longer_than_the_window(engine, path):
+    """deflate64 length code 285 (3 + 16 extra bits, inflate/constants.ts:12,28):
+    copies of 65,537 / 65,538 bytes -- longer than the 64 KiB history ring of the
+    wave and split decoders -- at distances that do not divide 65,536, and
+    distance 65,536 behind them (tests/bitbuild.py builds the streams; the
+    expected bytes are the plain LZ77 expansion, checked against the oracle)."""
+    import bitbuild
+
+    cases = bitbuild.long_copies()
+    members = [c for c, _ in cases]
+    caps = [(len(e) + 3) & ~3 for _, e in cases]
+    kw = {"lanes": {}, "wave": {"inflate_wave_min": 1, "inflate_split": 0},
+          "split": {"inflate_wave_min": 1, "inflate_split": 1}, "exact": {"inflate_fast": 0}}[path]
+    res, fast = _decode(engine, members, "deflate64-raw", caps, **kw)
+    for (c, e), (st, ph, msg, out, cons) in zip(cases, res):
+        assert st == 1 and out == e and cons == len(c), (path, len(e), st, msg)
+        assert oracle.decompress(c, "deflate64-raw", cap=len(e) + 16)[1] == e
+    if path != "exact":
+        assert fast == len(cases), "a member left the %s path" % path

@@ -118,3 +118,18 @@ def test_batch_golden_totals_match_survey():
     assert sum(l for l, _ in golden_io.batch("t64_l6_raw")) == 91855591
     assert sum(l for l, _ in golden_io.batch("m64_l6_raw")) == 123877078
     assert sum(l for l, _ in golden_io.batch("t64_l6_gzip")) == 183855998
+
+
+def test_oracle_decodes_long_deflate64_copies():
+    """The hand-built deflate64 members of tests/bitbuild.py (length code 285 up to
+    65,538 bytes, distance 65,536): the oracle gives their plain LZ77 expansion,
+    and the reference's own length-285 KAT (test-inflate9-length-code-285.spec.ts:9-15)
+    goes through the same builder's path."""
+    import bitbuild
+
+    for comp, exp in bitbuild.long_copies():
+        st, out, cons, ph, msg = oracle.decompress(comp, "deflate64-raw", cap=len(exp) + 16)
+        assert st == 1 and out == exp and cons == len(comp)
+    kat = bytes.fromhex("4b1cfdff07a3e5030000")
+    st, out, cons, _, _ = oracle.decompress(kat, "deflate64-raw", cap=70000)
+    assert st == 1 and out == b"a" * 66539

@@ -920,6 +920,10 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
+  // every decoder stores whole dwords: up to 3 bytes past a member's end, inside its
+  // capacity rounded up to a multiple of 4 -- which the next 4-aligned offset cannot overlap
+  for (uint32_t i = 0; i < n; i++)
+    if (out_off[i] & 3) return fail(ZS_STREAM_ERROR, "output offsets must be multiples of 4");
   MetaLayout ml(n);
   c->hmeta.resize(ml.bytes);
   c->last_n = n;

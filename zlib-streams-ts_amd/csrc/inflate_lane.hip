@@ -394,7 +394,10 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
   // reference (a caller's cap past 64 KiB), except large ones.  A member that fails
   // for another reason fails here again and goes on to the exact path.
   const uint32_t s = REFW && list ? list[li] : li;
-  if (REFW && !list && (res[s].bail == 0 || out_cap[s] <= 65536u || (wave_min && in_len[s] > wave_min))) return;
+  // (members of 512 MB or more too: the bookkeeping's bit positions are 32-bit; the exact path takes them)
+  if (REFW && !list &&
+      (res[s].bail == 0 || out_cap[s] <= 65536u || (wave_min && in_len[s] > wave_min) || in_len[s] >= (1u << 29)))
+    return;
   // a large member: the REFW instance, zs_k_inflate_wave or the split path decodes it
   if (!REFW && wave_min && in_len[s] > wave_min) return;
   zs_lane_tabs& T = tabs[s];

@@ -442,24 +442,30 @@ __global__ __launch_bounds__(64) void zs_k_split_decode(const uint8_t* __restric
       const uint32_t dist = C_VAL(here) + zs_wr_take(R, op & 15u);
       if (dist > wsize || total + len > piece_cap) { bail = true; break; }
       bool bad = false;
-      if (dist >= 64 || dist >= len) {
-        for (uint32_t i = 0; i < len; i += 64) {
-          const uint32_t j = i + lane;
-          if (j < len) ring[(total + j) & rmask] = (uint16_t)hist(total + j, dist, bad);
+      // in pieces of at most half the ring, each flushed before the next (a
+      // deflate64 length-285 copy is up to 65,538 values: longer than the ring)
+      for (uint32_t left = len; left;) {
+        const uint32_t pn = min(left, 32768u);
+        if (dist >= 64 || dist >= pn) {
+          for (uint32_t i = 0; i < pn; i += 64) {
+            const uint32_t j = i + lane;
+            if (j < pn) ring[(total + j) & rmask] = (uint16_t)hist(total + j, dist, bad);
+          }
+        } else {
+          // period dist < 64: lane j < step (a multiple of dist) stores the value dist - j % dist back
+          const uint32_t per = 64u / dist, step = per * dist;
+          const uint32_t mm = lane - (lane / dist) * dist;
+          const uint16_t b = (uint16_t)hist(total + mm, dist, bad);
+          for (uint32_t i = 0; i < pn; i += step) {
+            const uint32_t j = i + lane;
+            if (lane < step && j < pn) ring[(total + j) & rmask] = b;
+          }
         }
-      } else {
-        // period dist < 64: lane j < step (a multiple of dist) stores the value dist - j % dist back
-        const uint32_t per = 64u / dist, step = per * dist;
-        const uint32_t mm = lane - (lane / dist) * dist;
-        const uint16_t b = (uint16_t)hist(total + mm, dist, bad);
-        for (uint32_t i = 0; i < len; i += step) {
-          const uint32_t j = i + lane;
-          if (lane < step && j < len) ring[(total + j) & rmask] = b;
-        }
+        total += pn;
+        left -= pn;
+        flush();
       }
       if (__builtin_amdgcn_ballot_w64(bad)) { bail = true; break; }
-      total += len;
-      flush();
     }
     if (zs_wr_over(R)) bail = true;
   }

@@ -211,23 +211,32 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
       if (refw && C.symbol(b0, total, len, (uint32_t)(b1 - b0), (uint32_t)(b2 - b1), (uint32_t)(b3 - b2),
                            (uint32_t)(zs_wr_bitpos(R) - b3), false))
         tail = C.wrap(total, len, dist);
-      const uint32_t head = len - tail;
-      if (dist >= 64 || dist >= head) {
-        // a step's sources lie at least 64 bytes back, i.e. before the step
-        for (uint32_t i = 0; i < head; i += 64) {
-          const uint32_t k = i + lane;
-          if (k < head) ring[(total + k) & rmask] = ring[(total - dist + k) & rmask];
+      // A deflate64 copy can be longer than the ring (length code 285: up to
+      // 65,538 bytes): it goes in pieces of at most half the ring, the complete
+      // words stored after each, so no piece overwrites bytes not yet in HBM
+      // (the sources stay right: the ring holds the latest 64 KiB, dist <= 64 KiB).
+      for (uint32_t left = len - tail; left;) {
+        const uint32_t pn = min(left, 32768u);
+        if (dist >= 64 || dist >= pn) {
+          // a step's sources lie at least 64 bytes back, i.e. before the step
+          for (uint32_t i = 0; i < pn; i += 64) {
+            const uint32_t k = i + lane;
+            if (k < pn) ring[(total + k) & rmask] = ring[(total - dist + k) & rmask];
+          }
+        } else {
+          // period dist < 64: lane k < step (a multiple of dist) always stores
+          // the byte dist - k % dist before the copy
+          const uint32_t per = 64u / dist, step = per * dist;
+          const uint32_t m = lane - (lane / dist) * dist;
+          const uint8_t b = ring[(total - dist + m) & rmask];
+          for (uint32_t i = 0; i < pn; i += step) {
+            const uint32_t k = i + lane;
+            if (lane < step && k < pn) ring[(total + k) & rmask] = b;
+          }
         }
-      } else {
-        // period dist < 64: lane k < step (a multiple of dist) always stores
-        // the byte dist - k % dist before the copy
-        const uint32_t per = 64u / dist, step = per * dist;
-        const uint32_t m = lane - (lane / dist) * dist;
-        const uint8_t b = ring[(total - dist + m) & rmask];
-        for (uint32_t i = 0; i < head; i += step) {
-          const uint32_t k = i + lane;
-          if (lane < step && k < head) ring[(total + k) & rmask] = b;
-        }
+        total += pn;
+        left -= pn;
+        flush();
       }
       if (tail) {
         // the window-wrap copy: output[0..tail) of the current call, one byte
@@ -235,13 +244,13 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
         // ring are in HBM already (flushed <= 256 bytes behind)
         if (lane == 0) {
           for (uint32_t i = 0; i < tail; i++) {
-            const uint32_t x = C.B + i, t = total + head + i;
+            const uint32_t x = C.B + i, t = total + i;
             ring[t & rmask] = x + rmask + 1u >= t + 1u ? ring[x & rmask] : dst[x];
           }
         }
+        total += tail;
+        flush();
       }
-      total += len;
-      flush();
     }
     if (zs_wr_over(R)) bail = true;
   }

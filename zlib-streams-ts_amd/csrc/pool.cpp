@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -62,10 +63,16 @@ extern "C" int zs_inflate_batch_auto(zs_ctx* c, int wbits, uint32_t n, const uin
   if (!out || !out_off) return ZS_STREAM_ERROR;
   *out = nullptr;
   // pass buffers: pass 0 holds every member, later passes the retried ones
+  // (buffers uninitialised: the host entry writes only the produced bytes, so
+  // pages of capacity a member does not use are never touched)
   struct Pass {
     std::vector<uint32_t> idx, cap;
     std::vector<uint64_t> off;
-    std::vector<uint8_t> buf;
+    std::unique_ptr<uint8_t, decltype(&free)> buf{nullptr, &free};
+    bool alloc(uint64_t bytes) {
+      buf.reset((uint8_t*)malloc(bytes));
+      return buf != nullptr;
+    }
   };
   std::vector<Pass> passes(1);
   std::vector<uint32_t> where(n, 0);   // the pass a member's final output is in
@@ -83,8 +90,8 @@ extern "C" int zs_inflate_batch_auto(zs_ctx* c, int wbits, uint32_t n, const uin
       o += p.cap[i];
       slot[i] = i;
     }
-    p.buf.resize(o + 4);
-    const int r = zs_inflate_batch_ex(c, wbits, n, in, in_off, in_len, p.buf.data(), p.off.data(), p.cap.data(),
+    if (!p.alloc(o + 4)) return ZS_MEM_ERROR;
+    const int r = zs_inflate_batch_ex(c, wbits, n, in, in_off, in_len, p.buf.get(), p.off.data(), p.cap.data(),
                                       status, phase, msg, out_len, consumed, check);
     if (r != ZS_OK) return r;
   }
@@ -110,8 +117,8 @@ extern "C" int zs_inflate_batch_auto(zs_ctx* c, int wbits, uint32_t n, const uin
       ioff[k] = in_off[nx.idx[k]];
       ilen[k] = in_len[nx.idx[k]];
     }
-    nx.buf.resize(o + 4);
-    const int r = zs_inflate_batch_ex(c, wbits, m, in, ioff.data(), ilen.data(), nx.buf.data(), nx.off.data(),
+    if (!nx.alloc(o + 4)) return ZS_MEM_ERROR;
+    const int r = zs_inflate_batch_ex(c, wbits, m, in, ioff.data(), ilen.data(), nx.buf.get(), nx.off.data(),
                                       nx.cap.data(), st.data(), ph.data(), ms.data(), olen.data(), cons.data(),
                                       check ? chk.data() : nullptr);
     if (r != ZS_OK) return r;
@@ -138,7 +145,7 @@ extern "C" int zs_inflate_batch_auto(zs_ctx* c, int wbits, uint32_t n, const uin
   for (uint32_t i = 0; i < n; i++)
     if (out_len[i]) {
       const Pass& p = passes[where[i]];
-      memcpy(res + out_off[i], p.buf.data() + p.off[slot[i]], out_len[i]);
+      memcpy(res + out_off[i], p.buf.get() + p.off[slot[i]], out_len[i]);
     }
   *out = res;
   return ZS_OK;

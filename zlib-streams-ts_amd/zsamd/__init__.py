@@ -424,6 +424,8 @@ class Pool:
         L = lib()
         mask = 0
         for d in devices or []:
+            if not 0 <= int(d) < 64:  # the C mask is 64 bits (ctypes would truncate it to "every device")
+                raise ValueError("device index %r outside 0..63" % (d,))
             mask |= 1 << int(d)
         p = _P()
         r = L.zs_pool_create(mask, ctypes.byref(p))
