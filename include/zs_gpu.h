@@ -200,6 +200,10 @@ double zs_last_batch_ms(zs_ctx *ctx);
  * (the rest went through the exact stream-layer state machine).  Synchronizes
  * the batch's stream.  For tests and tuning. */
 uint32_t zs_last_inflate_lane_count(zs_ctx *ctx);
+/* Members of the last inflate batch that the segmented decode finished
+ * (inflate_seg.hip; the others of its members went on to the wave kernel).
+ * Synchronizes.  For tests and tuning. */
+uint32_t zs_last_inflate_seg_count(zs_ctx *ctx);
 double zs_last_phase_ms(zs_ctx *ctx, const char *phase);
 void zs_set_timing(zs_ctx *ctx, int on);
 /* Engine options: "timing" (0/1, as zs_set_timing); "inflate_fast" (default 1):

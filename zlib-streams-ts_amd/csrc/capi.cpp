@@ -18,6 +18,7 @@
 #include "zs_kernels.h"
 #include "zs_inflate.h"
 #include "zs_split.h"
+#include "zs_seg.h"
 
 
 namespace {
@@ -106,6 +107,15 @@ struct zs_ctx {
   bool inflate_split = true;
   Buf slist, sfound, spres, sscr, smem, sval;
   std::vector<uint32_t> hslist;
+  // segmented decode (inflate_seg.hip): a member's blocks cut into lane-sized pieces that synchronise
+  bool inflate_seg = true;
+  uint32_t seg_bits = 4096;         // bits of input per piece at least (> 2 ZS_SEG_W)
+  uint32_t seg_small_batch = 16384; // batches of at most this many members ...
+  uint32_t seg_small_min = 4096;    // ... send members with more input bytes than this to it too
+  Buf glist, gfound, gcidx, gblk, glanes, gtab, gmem, gpbase, gplist, gsbase, gscr, gcnt;
+  std::vector<uint32_t> hglist, hgpbase;
+  bool seg_used = false;            // the last inflate batch ran it
+  std::vector<uint64_t> hgsbase;
   // host staging for the host-buffer entry points
   Buf d_in, d_out, d_res, d_pack;
   HostBuf h_in, h_out;
@@ -257,7 +267,8 @@ void zs_ctx_destroy(zs_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   for (Buf* b : {&c->lstat, &c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
                  &c->istate, &c->d_in, &c->d_out, &c->d_res, &c->d_pack, &c->wlist, &c->slist, &c->sfound,
-                 &c->spres, &c->sscr, &c->smem, &c->sval})
+                 &c->spres, &c->sscr, &c->smem, &c->sval, &c->glist, &c->gfound, &c->gcidx, &c->gblk,
+                 &c->glanes, &c->gtab, &c->gmem, &c->gpbase, &c->gplist, &c->gsbase, &c->gscr, &c->gcnt})
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&c->h_in, &c->h_out})
     if (b->p) (void)hipHostFree(b->p);
@@ -284,6 +295,17 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "fast_group")) c->fast_group = value != 0;
   else if (!strcmp(name, "inflate_split")) c->inflate_split = value != 0;
+  else if (!strcmp(name, "inflate_seg")) c->inflate_seg = value != 0;
+  else if (!strcmp(name, "seg_bits")) {
+    if (value < (int)(2 * ZS_SEG_W) || value > (1 << 24)) return fail(ZS_STREAM_ERROR, "seg_bits must be 4096 .. 2^24");
+    c->seg_bits = (uint32_t)value;
+  } else if (!strcmp(name, "seg_small_batch")) {
+    if (value < 0) return fail(ZS_STREAM_ERROR, "seg_small_batch must be >= 0");
+    c->seg_small_batch = (uint32_t)value;
+  } else if (!strcmp(name, "seg_small_min")) {
+    if (value < 0) return fail(ZS_STREAM_ERROR, "seg_small_min must be >= 0");
+    c->seg_small_min = (uint32_t)value;
+  }
   else if (!strcmp(name, "parse_waves")) {
     if (value < 0 || value > 4 || value == 3) return fail(ZS_STREAM_ERROR, "parse_waves must be 0, 1, 2 or 4");
     c->parse_waves = value;
@@ -308,6 +330,13 @@ double zs_last_batch_ms(zs_ctx* c) {
 uint32_t zs_last_inflate_lane_count(zs_ctx* c) {
   if (!c || !c->lane_count_host || hipEventSynchronize(c->lane_ev) != hipSuccess) return 0;
   return *(volatile uint32_t*)c->lane_count_host;
+}
+uint32_t zs_last_inflate_seg_count(zs_ctx* c) {
+  uint32_t v = 0;
+  if (!c || !c->seg_used || !c->gcnt.p || hipStreamSynchronize(c->side) != hipSuccess ||
+      hipMemcpy(&v, c->gcnt.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return v;
 }
 double zs_last_phase_ms(zs_ctx* c, const char* phase) {
   collect_marks(c);
@@ -900,6 +929,99 @@ __global__ void zs_k_inflate_check(const uint8_t* in, const uint64_t* in_off, co
   out[s] = v;
 }
 
+// The segmented decode of the members in c->hglist (inflate_seg.hip) on the side
+// stream, after the caller's stream reaches this point; then the wave kernel over
+// the same members for any the pieces could not finish (skip_done: the others
+// return at once), the exact kernel after it for whatever fails there.
+static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* d_ioff,
+                      const uint32_t* d_ilen, uint8_t* d_out, const uint64_t* d_ooff, const uint32_t* d_ocap,
+                      const uint32_t* in_len, const uint32_t* out_cap, zs_lane_res* lres) {
+  const uint32_t ng = (uint32_t)c->hglist.size();
+  const bool d64 = wbits == -16;
+  const bool refw = c->inflate_ref_wrap && !d64;
+  // per member: the finder's candidates (at most one per range of >= 16,384 bits), the
+  // pieces' bound and their u16 scratch (each piece 16-byte aligned and padded)
+  c->hgpbase.assign(ng + 1, 0);
+  c->hgsbase.assign(ng + 1, 0);
+  uint64_t cap_blocks = 0;
+  for (uint32_t k = 0; k < ng; k++) {
+    const uint32_t i = c->hglist[k];
+    const uint64_t nbits = 8ull * in_len[i];
+    cap_blocks += std::min<uint64_t>(ZS_SPLIT_MAX, (nbits + zs_split_span(in_len[i]) - 1) / zs_split_span(in_len[i]));
+    const uint32_t pmax = (uint32_t)(nbits / c->seg_bits + ZS_SPLIT_MAX + 1);
+    c->hgpbase[k + 1] = c->hgpbase[k] + pmax;
+    c->hgsbase[k + 1] = c->hgsbase[k] + ((((uint64_t)out_cap[i] + 7) & ~7ull) + ZS_SEG_PAD * (uint64_t)pmax + 16);
+  }
+  HIPCHK(c->glist.ensure(4ull * ng));
+  HIPCHK(c->gfound.ensure(8ull * ZS_SPLIT_MAX * ng));
+  HIPCHK(c->gcidx.ensure(4ull * ZS_SPLIT_MAX * ng));
+  HIPCHK(c->gblk.ensure(sizeof(zs_seg_blk) * cap_blocks));
+  HIPCHK(c->glanes.ensure(sizeof(zs_seg_lane) * ZS_SEG_LANES * cap_blocks));
+  HIPCHK(c->gtab.ensure(sizeof(zcode) * ZS_SEG_TAB * cap_blocks));
+  HIPCHK(c->gmem.ensure(sizeof(zs_seg_mem) * ng));
+  HIPCHK(c->gpbase.ensure(4ull * (ng + 1)));
+  HIPCHK(c->gplist.ensure(4ull * c->hgpbase[ng] + 16));
+  HIPCHK(c->gsbase.ensure(8ull * (ng + 1)));
+  HIPCHK(c->gscr.ensure(2ull * c->hgsbase[ng] + 64));
+  HIPCHK(c->gcnt.ensure(16));
+  HIPCHK(hipMemcpyAsync(c->glist.p, c->hglist.data(), 4ull * ng, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->gpbase.p, c->hgpbase.data(), 4ull * (ng + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->gsbase.p, c->hgsbase.data(), 8ull * (ng + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(c->gcnt.p, 0, 8, st));  // the block counter, the members finished
+  HIPCHK(hipEventRecord(c->fork, st));
+  HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
+  hipStream_t sd = c->side;
+  if (int r = mark(c, sd, "start")) return r;
+  const uint32_t* gl = c->glist.as<uint32_t>();
+  uint64_t* gf = c->gfound.as<uint64_t>();
+  uint32_t* cnt = c->gcnt.as<uint32_t>();
+  zs_seg_blk* gb = c->gblk.as<zs_seg_blk>();
+  zs_seg_lane* gln = c->glanes.as<zs_seg_lane>();
+  zcode* gt = c->gtab.as<zcode>();
+  zs_seg_mem* gm = c->gmem.as<zs_seg_mem>();
+  const uint32_t nb = (uint32_t)cap_blocks;
+  zs_k_split_find<<<ng * ZS_SPLIT_MAX, 1024, 0, sd>>>(d_in, d_ioff, d_ilen, gl, wbits, gf);
+  zs_k_seg_alloc<<<ng, 64, 0, sd>>>(gf, ng, c->gcidx.as<uint32_t>(), gb, cnt, nb, gm);
+  if (int r = mark(c, sd, "seg_find")) return r;
+  if (d64)
+    zs_k_seg_sync<true><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, wbits, gf, cnt, gb, gln, gt, c->seg_bits);
+  else
+    zs_k_seg_sync<false><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, wbits, gf, cnt, gb, gln, gt, c->seg_bits);
+  if (int r = mark(c, sd, "seg_sync")) return r;
+  zs_k_seg_plan<<<ng, 64, 0, sd>>>(d_in, d_ioff, d_ilen, d_ocap, gl, ng, wbits, refw ? 1 : 0,
+                                   c->gcidx.as<uint32_t>(), gb, gln, gm, c->gpbase.as<uint32_t>(),
+                                   c->gplist.as<uint32_t>());
+  if (int r = mark(c, sd, "seg_plan")) return r;
+  const uint64_t* sb = c->gsbase.as<uint64_t>();
+  uint16_t* scr = c->gscr.as<uint16_t>();
+  if (d64)
+    zs_k_seg_decode<true, false><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt, gb, gln, gt, gm, sb, scr);
+  else if (refw)
+    zs_k_seg_decode<false, true><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt, gb, gln, gt, gm, sb, scr);
+  else
+    zs_k_seg_decode<false, false><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt, gb, gln, gt, gm, sb, scr);
+  if (int r = mark(c, sd, "seg_decode")) return r;
+  HIPCHK(hipFuncSetAttribute((const void*)zs_k_seg_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+  zs_k_seg_resolve<<<ng, 256, 65536, sd>>>(gl, gm, gln, c->gpbase.as<uint32_t>(), c->gplist.as<uint32_t>(), sb, scr,
+                                           d_out, d_ooff, lres, c->llen.as<uint32_t>(), cnt + 1);
+  if (int r = mark(c, sd, "seg_resolve")) return r;
+  // members the pieces could not finish: the wave kernel (skip_done), then the exact kernel
+  const size_t wsm = zs_inflate_wave_lds_bytes(d64);
+  const void* wk = refw ? (const void*)zs_k_inflate_wave<true> : (const void*)zs_k_inflate_wave<false>;
+  HIPCHK(hipFuncSetAttribute(wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wsm));
+  if (refw)
+    zs_k_inflate_wave<true><<<ng, 64, wsm, sd>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, gl, ng, lres,
+                                                 c->llen.as<uint32_t>(), 1u);
+  else
+    zs_k_inflate_wave<false><<<ng, 64, wsm, sd>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, gl, ng, lres,
+                                                  c->llen.as<uint32_t>(), 1u);
+  HIPCHK(hipGetLastError());
+  if (int r = mark(c, sd, "seg_fallback")) return r;
+  (void)n;
+  (void)d_ocap;
+  return ZS_OK;
+}
+
 extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
                                        const uint32_t* in_len, uint8_t* d_out, const uint64_t* out_off,
                                        const uint32_t* out_cap, int32_t* d_status, int32_t* d_phase, int32_t* d_msg,
@@ -920,6 +1042,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
+  c->seg_used = false;
   // every decoder stores whole dwords: up to 3 bytes past a member's end, inside its
   // capacity rounded up to a multiple of 4 -- which the next 4-aligned offset cannot overlap
   for (uint32_t i = 0; i < n; i++)
@@ -974,6 +1097,13 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
     uint32_t wave_min = 0;
     c->hwlist.clear();
     c->hslist.clear();
+    c->hglist.clear();
+    // "Large" members decode beside the lane kernel.  With the segmented decode on,
+    // a small batch's members are large from seg_small_min bytes on: one lane each
+    // would leave most of the chip idle (the per-rank shards of the 8-GPU configs).
+    uint32_t big_min = c->inflate_wave_min;
+    if (c->inflate_seg && n <= c->seg_small_batch && c->seg_small_min && (!big_min || c->seg_small_min < big_min))
+      big_min = c->seg_small_min;
     // Large raw members whose decode carries no call-boundary behaviour
     // (deflate64; raw deflate without the window-wrap copy) are cut at their
     // block boundaries and decoded piecewise (inflate_split.hip); the rest of
@@ -982,11 +1112,15 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
     const bool splittable = c->inflate_split && (wbits == -16 || (wbits == -15 && !c->inflate_ref_wrap));
     uint32_t piece_cap = 0;
     uint64_t val_stride = 0;  // u32 values per split member
-    if (c->inflate_wave_min) {
+    if (big_min) {
       constexpr size_t kSplitScratch = 2ull << 30;
       constexpr uint32_t kPieceCapMax = 4u << 20;  // values per piece
       for (uint32_t i = 0; i < n; i++) {
-        if (in_len[i] <= c->inflate_wave_min) continue;
+        if (in_len[i] <= big_min) continue;
+        if (c->inflate_seg && in_len[i] < (1u << 29)) {  // (bit positions in 32 bits)
+          c->hglist.push_back(i);
+          continue;
+        }
         const uint32_t pc = (std::min(out_cap[i], kPieceCapMax) + 1u) & ~1u;
         const uint32_t npc = std::max(piece_cap, pc);
         const uint64_t nvs = std::max<uint64_t>(val_stride, (out_cap[i] + 3ull) & ~3ull);
@@ -998,7 +1132,14 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
           c->hwlist.push_back(i);
         }
       }
-      if (!c->hwlist.empty() || !c->hslist.empty()) wave_min = c->inflate_wave_min;
+      if (!c->hwlist.empty() || !c->hslist.empty() || !c->hglist.empty()) wave_min = big_min;
+    }
+    c->seg_used = !c->hglist.empty();
+    if (!c->hglist.empty()) {
+      const int r = seg_launch(c, st, wbits, n, d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, in_len, out_cap, lres);
+      if (r != ZS_OK) return r;
+      // (the join below waits for the side stream's last kernel)
+      if (c->hslist.empty() && c->hwlist.empty()) HIPCHK(hipEventRecord(c->join, c->side));
     }
     if (!c->hslist.empty()) {
       const uint32_t ns = (uint32_t)c->hslist.size();
@@ -1071,10 +1212,10 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
               c->llen.as<uint32_t>(), ZS_INF_REF_WRAP, 0u, c->wlist.as<uint32_t>());
       } else if (refw)
         zs_k_inflate_wave<true><<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
-                                                          c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
+                                                          c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>(), 0u);
       else
         zs_k_inflate_wave<false><<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
-                                                           c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>());
+                                                           c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>(), 0u);
       HIPCHK(hipGetLastError());
       if (int r = mark(c, c->side, lanes ? "inflate_large" : "inflate_wave")) return r;
       HIPCHK(hipEventRecord(c->join, c->side));

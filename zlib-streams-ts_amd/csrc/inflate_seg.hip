@@ -1,0 +1,1054 @@
+// inflate_seg.hip -- the segmented decode: one member's symbols decoded by many
+// LANES at once, for batches whose members are too few to fill the chip one lane
+// (inflate_lane.hip) or one wave (inflate_wave.hip) per member -- the per-rank
+// shards of the 8-GPU configs (512 x 256 KiB, 1,024 x 64 KiB).
+//
+// A member's decode is one serial chain of Huffman lookups; three facts cut it:
+//  * block starts can be found by testing every bit offset (zs_k_split_find);
+//  * inside a block, Huffman decoding started at an arbitrary bit falls into
+//    step with the true symbol stream after a few symbols (median 100 bits,
+//    max ~1,750 over 7,800 trials on the benchmark corpora): a lane decoding
+//    from the block's true start reaches, past the next lane's start, a symbol
+//    start that lane also visited -- from there both are the true stream;
+//  * a copy reaching back before a piece's start can be written as a MARKER
+//    (u16 255 + k: "the value k positions before the piece"), propagated by
+//    later copies like a byte, and resolved once the earlier pieces are known.
+// The reference's window-wrap copy (inffast.ts:127-147, reproduced by default)
+// depends on its inflate() call boundaries (32 KiB input sub-chunks, 64 KiB
+// output buffers, streams.ts:78-93): they move only at "events" -- the first
+// symbol ending past a sub-chunk end, the first symbol reaching a full buffer
+// -- so the call state at every piece start follows from each piece's output
+// count, events and last symbol length (tools/emu/emu_seg.py checks this plan
+// against the serial bookkeeping and the oracle), and each piece replays the
+// bookkeeping (zs_refcalls) from its start.
+//
+// Kernels, each over the whole batch:
+//  zs_k_split_find  candidate block starts (inflate_split.hip), one per bit range
+//  zs_k_seg_alloc   compact indices for the candidates
+//  zs_k_seg_sync    one wave per candidate block: the header and tables, then
+//                   lane j decodes from bit sym0 + j S, recording the symbol
+//                   starts of its first ZS_SEG_W bits; it stops at the first
+//                   of its positions (past the next lane's start) that the next
+//                   lane recorded.  Output counts, crossing events, the block's end.
+//  zs_k_seg_plan    one wave per member: blocks chained by their ends, pieces
+//                   placed (prefix sum), trailer and capacity checked, call state
+//                   per piece (REFW)
+//  zs_k_seg_decode  one wave per block: each lane decodes its piece into u16
+//                   values (bytes or markers) with the window-wrap copy replayed
+//  zs_k_seg_resolve one workgroup per member: pieces in order, markers looked up
+//                   in the bytes already final (a 64 KiB LDS ring), bytes written
+// Any doubt -- no chain of blocks, a stored block, a lane that never
+// synchronises, an invalid code or "too far back" in a piece, a marker further
+// back than a u16 says -- marks the member bad; the host then runs the
+// wave kernel over it (and that the exact kernel), so outcomes stay the reference's.
+#include <hip/hip_runtime.h>
+#include "zs_common.h"
+#include "zs_inflate.h"
+#include "zs_inftab.h"
+#include "zs_wave.h"
+#include "zs_refcalls.h"
+#include "zs_seg.h"
+
+// ------------------------------------------------------------------ alloc
+// One wave per member, lane r = the finder's range r: the member's candidates
+// get consecutive block indices from a global counter (the order of members is
+// free); a member whose blocks do not fit is marked bad.
+__global__ __launch_bounds__(64) void zs_k_seg_alloc(const uint64_t* __restrict__ found, uint32_t n_list,
+                                                     uint32_t* __restrict__ cidx, zs_seg_blk* __restrict__ blk,
+                                                     uint32_t* __restrict__ counter, uint32_t cap_blocks,
+                                                     zs_seg_mem* __restrict__ mem) {
+  const uint32_t m = blockIdx.x, r = threadIdx.x;
+  if (m >= n_list) return;
+  const bool cand = found[m * ZS_SPLIT_MAX + r] != ~0ull;
+  const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+  const uint32_t cnt = (uint32_t)__builtin_popcountll(bal);
+  uint32_t base = 0;
+  if (r == 0) base = atomicAdd(counter, cnt);
+  base = (uint32_t)__shfl(base, 0);
+  const uint32_t idx = base + (uint32_t)__builtin_popcountll(bal & ((1ull << r) - 1ull));
+  const bool fits = base + cnt <= cap_blocks;
+  cidx[m * ZS_SPLIT_MAX + r] = cand && fits ? idx : ZS_SEG_NONE;
+  if (cand && idx < cap_blocks) {
+    blk[idx].m = fits ? m : ZS_SEG_NONE;
+    blk[idx].r = r;
+    blk[idx].flags = 0;
+  }
+  if (r == 0) {
+    zs_seg_mem z = {fits ? 0u : 1u, 0u, 0u, 0u, 0u, {0u, 0u, 0u}};
+    mem[m] = z;
+  }
+}
+
+// ------------------------------------------------------------- lane reader
+// One lane's bit reader (the lane kernel's scheme: clamped aligned words, one
+// refill ahead, zero past the end), started at any bit; member bit positions
+// fit 32 bits (the host sends members under 512 MB here).
+struct zs_sg_reader {
+  const uint32_t* w4;
+  uint32_t sh, last, n;
+  uint32_t pos;  // bytes moved into hold (a multiple of 4)
+  uint64_t hold;
+  uint32_t bits;
+  uint32_t pf;
+};
+static __device__ __forceinline__ uint32_t zs_sg_load4(const zs_sg_reader& R, uint32_t at) {
+  const uint32_t q = (at + R.sh) >> 2;
+  const uint32_t lo = R.w4[min(q, R.last)], hi = R.w4[min(q + 1u, R.last)];
+  const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, R.sh);
+  const uint32_t valid = at < R.n ? R.n - at : 0u;
+  return valid >= 4u ? v : v & ((1u << (8u * valid)) - 1u);
+}
+static __device__ __forceinline__ void zs_sg_fill(zs_sg_reader& R) {
+  R.hold |= (uint64_t)R.pf << R.bits;
+  R.bits += 32;
+  R.pos += 4;
+  R.pf = zs_sg_load4(R, R.pos);
+}
+static __device__ __forceinline__ void zs_sg_drop(zs_sg_reader& R, uint32_t k) {
+  R.hold >>= k;
+  R.bits -= k;
+}
+static __device__ __forceinline__ void zs_sg_seek(zs_sg_reader& R, uint32_t bit) {
+  R.pos = (bit >> 5) << 2;
+  R.hold = 0;
+  R.bits = 0;
+  R.pf = zs_sg_load4(R, R.pos);
+  zs_sg_fill(R);
+  zs_sg_drop(R, bit & 31u);
+}
+static __device__ __forceinline__ uint32_t zs_sg_bitpos(const zs_sg_reader& R) { return R.pos * 8u - R.bits; }
+static __device__ __forceinline__ uint32_t zs_sg_take(zs_sg_reader& R, uint32_t k) {  // k <= 32
+  if (R.bits < k) zs_sg_fill(R);
+  const uint32_t v = (uint32_t)R.hold & (k == 32 ? 0xffffffffu : ((1u << k) - 1u));
+  zs_sg_drop(R, k);
+  return v;
+}
+static __device__ __forceinline__ void zs_sg_init(zs_sg_reader& R, const uint8_t* src, uint32_t n) {
+  R.n = n;
+  R.sh = (uint32_t)((uintptr_t)src & 3u);
+  R.w4 = reinterpret_cast<const uint32_t*>(src - R.sh);
+  R.last = (R.sh + n - 1u) >> 2;
+}
+// a code from a zlib table (second level included); nb: its bits
+static __device__ __forceinline__ zcode zs_sg_code(zs_sg_reader& R, const zcode* t, uint32_t mask, uint32_t& nb) {
+  zcode here = t[(uint32_t)R.hold & mask];
+  uint32_t b = C_BITS(here);
+  if (C_OP(here) && (C_OP(here) & 0xf0) == 0) {
+    const uint32_t rb = b;
+    here = t[C_VAL(here) + (((uint32_t)R.hold & ((1u << (rb + C_OP(here))) - 1u)) >> rb)];
+    b = rb + C_BITS(here);
+  }
+  zs_sg_drop(R, b);
+  nb = b;
+  return here;
+}
+// one symbol (inffast.ts:5-228 decode, inflate.ts LEN..DISTEXT for deflate64)
+#define ZS_SG_LIT 0u
+#define ZS_SG_COPY 1u
+#define ZS_SG_EOB 2u
+#define ZS_SG_BAD 3u
+struct zs_sg_sym {
+  uint32_t kind, val, len;  // literal: val; copy: len, val = distance
+  uint32_t l1, e1, l2, e2;  // the bit fields (zs_refcalls)
+};
+static __device__ __forceinline__ zs_sg_sym zs_sg_decode(zs_sg_reader& R, const zcode* lt, uint32_t lmask,
+                                                        const zcode* dt, uint32_t dmask, uint32_t emask) {
+  zs_sg_sym y = {ZS_SG_BAD, 0u, 0u, 0u, 0u, 0u, 0u};
+  if (R.bits < 32) zs_sg_fill(R);
+  zcode here = zs_sg_code(R, lt, lmask, y.l1);
+  uint32_t op = C_OP(here);
+  if (op == 0) {
+    y.kind = ZS_SG_LIT;
+    y.val = C_VAL(here);
+    y.len = 1;
+    return y;
+  }
+  if (op & 32) {
+    y.kind = ZS_SG_EOB;
+    return y;
+  }
+  if (op & 64) return y;  // "invalid literal/length code"
+  y.e1 = op & emask;
+  y.len = C_VAL(here) + zs_sg_take(R, y.e1);
+  if (R.bits < 32) zs_sg_fill(R);
+  here = zs_sg_code(R, dt, dmask, y.l2);
+  op = C_OP(here);
+  if (op & 64) return y;  // "invalid distance code"
+  y.e2 = op & 15u;
+  y.val = C_VAL(here) + zs_sg_take(R, y.e2);
+  y.kind = ZS_SG_COPY;
+  return y;
+}
+
+// The block header at the wave reader's position (inflate.ts:600-836) into
+// zlib's tables (inflate_table) in LDS, as zs_k_inflate_wave; false for a
+// stored block or anything invalid (the member then takes the other paths).
+static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* lens, uint16_t* work, bool d64,
+                                    uint32_t& last, uint32_t& lbits, uint32_t& dbits, uint32_t& dofs,
+                                    uint32_t& ntab) {
+  last = zs_wr_take(R, 1);
+  const uint32_t type = zs_wr_take(R, 2);
+  uint32_t lused = 0, dused = 0;
+  if (type == 1) {  // fixed tables (inflate.ts:218-280)
+    uint32_t sym;
+    for (sym = 0; sym < 144; sym++) lens[sym] = 8;
+    for (; sym < 256; sym++) lens[sym] = 9;
+    for (; sym < 280; sym++) lens[sym] = 7;
+    for (; sym < 288; sym++) lens[sym] = 8;
+    lbits = 9;
+    zs_inflate_table(LENS, lens, 288, codes, &lbits, work, d64, &lused);
+    for (sym = 0; sym < 32; sym++) lens[sym] = 5;
+    dbits = 5;
+    zs_inflate_table(DISTS, lens, 32, codes + lused, &dbits, work, d64, &dused);
+  } else if (type == 2) {  // dynamic (inflate.ts:662-836)
+    const uint32_t nlen = zs_wr_take(R, 5) + 257, ndist = zs_wr_take(R, 5) + 1, ncode = zs_wr_take(R, 4) + 4;
+    if (nlen > 286 || (!d64 && ndist > 30)) return false;
+    uint32_t i;
+    for (i = 0; i < ncode; i++) lens[ZS_BL_ORDER[i]] = (uint16_t)zs_wr_take(R, 3);
+    for (; i < 19; i++) lens[ZS_BL_ORDER[i]] = 0;
+    uint32_t cbits = 7, used;
+    if (zs_inflate_table(CODES, lens, 19, codes, &cbits, work, d64, &used)) return false;
+    i = 0;
+    while (i < nlen + ndist) {
+      const zcode here = zs_wr_decode(R, codes, cbits);
+      const uint32_t v = C_VAL(here);
+      if (v < 16) {
+        lens[i++] = (uint16_t)v;
+        continue;
+      }
+      uint32_t rep, val = 0;
+      if (v == 16) {
+        if (i == 0) return false;
+        val = zs_u(lens[i - 1]);
+        rep = 3 + zs_wr_take(R, 2);
+      } else if (v == 17) {
+        rep = 3 + zs_wr_take(R, 3);
+      } else {
+        rep = 11 + zs_wr_take(R, 7);
+      }
+      if (i + rep > nlen + ndist) return false;
+      while (rep--) lens[i++] = (uint16_t)val;
+    }
+    if (zs_wr_over(R) || zs_u(lens[256]) == 0) return false;
+    lbits = 9;
+    if (zs_inflate_table(LENS, lens, nlen, codes, &lbits, work, d64, &lused)) return false;
+    dbits = 6;
+    if (zs_inflate_table(DISTS, lens + nlen, ndist, codes + lused, &dbits, work, d64, &dused)) return false;
+  } else {
+    return false;  // stored (the other paths copy it) or "invalid block type"
+  }
+  lbits = zs_u(lbits);
+  dbits = zs_u(dbits);
+  dofs = zs_u(lused);
+  ntab = zs_u(lused + dused);
+  return true;
+}
+
+// ------------------------------------------------------------------- sync
+struct zs_sg_sync_lds {
+  uint32_t inw[ZS_WIN_IN];
+  zcode codes[ZS_SEG_TAB];
+  uint16_t lens[320];
+  uint16_t work[288];
+  uint32_t bm[ZS_SEG_LANES][ZS_SEG_W / 32];  // each lane's visited symbol starts in its window
+  uint32_t ckp[ZS_SEG_LANES][ZS_SEG_NCK];    // checkpoints: a visited position per 128-bit bucket ...
+  uint32_t ckc[ZS_SEG_LANES][ZS_SEG_NCK];    // ... and the lane's output count there
+  uint32_t prog[ZS_SEG_LANES];   // a lane's current position (ZS_SEG_NONE once stopped)
+  uint32_t conf[ZS_SEG_LANES];   // on the true chain (lane 0, or synced into by a confirmed lane)
+  uint32_t absorbed[ZS_SEG_LANES];
+  uint32_t kind[ZS_SEG_LANES], to[ZS_SEG_LANES], onchain[ZS_SEG_LANES];
+  unsigned long long from[ZS_SEG_LANES];  // (lane << 32 | bit) of the lane that synced into it (the lowest lane wins)
+  uint32_t done, ok, bend;
+};
+#define ZS_SG_K_NONE 0u
+#define ZS_SG_K_SYNC 1u
+#define ZS_SG_K_BEND 2u
+#define ZS_SG_K_STOP 3u
+
+// one wave per candidate block
+template <bool D64>
+__global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                    const uint32_t* __restrict__ in_len,
+                                                    const uint32_t* __restrict__ list, int wbits,
+                                                    const uint64_t* __restrict__ found,
+                                                    const uint32_t* __restrict__ counter, zs_seg_blk* __restrict__ blk,
+                                                    zs_seg_lane* __restrict__ lanes, zcode* __restrict__ tcache,
+                                                    uint32_t smin) {
+  __shared__ zs_sg_sync_lds L;
+  volatile zs_sg_sync_lds& V = L;
+  const uint32_t b = blockIdx.x, lane = threadIdx.x;
+  if (b >= *counter) return;
+  zs_seg_blk& Bk = blk[b];
+  const uint32_t m = zs_u(Bk.m), r = zs_u(Bk.r);
+  if (m == ZS_SEG_NONE) return;
+  const uint32_t s = zs_u(list[m]);
+  const uint32_t n = zs_u(in_len[s]);
+  const uint32_t nbits = 8u * n;
+  const uint32_t f = (uint32_t)found[m * ZS_SPLIT_MAX + r];
+  // the nominal end: the next candidate's start
+  uint32_t nend = nbits;
+  {
+    const uint64_t fx = found[m * ZS_SPLIT_MAX + lane];
+    const uint64_t later = __builtin_amdgcn_ballot_w64(lane > r && fx != ~0ull);
+    if (later) nend = (uint32_t)found[m * ZS_SPLIT_MAX + (uint32_t)__builtin_ctzll(later)];
+    nend = zs_u(nend);
+  }
+  const uint8_t* src = in + in_off[s];
+  // ---- header (wave-uniform)
+  zs_wave_reader R;
+  R.n = n;
+  R.sh = (uint32_t)((uintptr_t)src & 3u);
+  R.w4 = reinterpret_cast<const uint32_t*>(src - R.sh);
+  R.last = (R.sh + n - 1u) >> 2;
+  R.inw = L.inw;
+  zs_wr_stage(R, ((f >> 3) + R.sh) >> 2);
+  zs_wr_seek(R, f >> 3);
+  zs_wr_take(R, f & 7u);
+  bool good = true;
+  const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
+  if (r == 0 && wrap) {  // plain zlib / gzip headers only (inflate.ts:377-580), as the lane path
+    const uint32_t b0 = zs_wr_take(R, 8), b1 = zs_wr_take(R, 8);
+    if ((wrap & 2) && b0 == 0x1f && b1 == 0x8b) {
+      const uint32_t cm = zs_wr_take(R, 8), flg = zs_wr_take(R, 8);
+      zs_wr_take(R, 32);
+      zs_wr_take(R, 16);
+      good = cm == 8 && flg == 0;
+    } else if (wrap & 1) {
+      good = !(((b0 << 8) | b1) % 31 || (b0 & 15) != 8 || (b0 >> 4) + 8 > 15 || (b1 & 0x20));
+    } else {
+      good = false;
+    }
+  }
+  const uint32_t hdr = (uint32_t)zs_wr_bitpos(R);
+  uint32_t last = 0, lbits = 0, dbits = 0, dofs = 0, ntab = 0;
+  if (good) good = zs_sg_header(R, L.codes, L.lens, L.work, D64, last, lbits, dbits, dofs, ntab);
+  const uint32_t sym0 = (uint32_t)zs_wr_bitpos(R);
+  if (good && sym0 > nbits) good = false;
+  if (!good) {
+    if (lane == 0) Bk.flags = 0;
+    return;
+  }
+  for (uint32_t i = lane; i < ntab; i += 64) tcache[(size_t)b * ZS_SEG_TAB + i] = L.codes[i];
+  const uint32_t payload = nend > sym0 ? nend - sym0 : 0u;
+  const uint32_t nl = max(1u, min(ZS_SEG_LANES, payload / smin));
+  const uint32_t S = max(1u, (payload + nl - 1u) / nl);
+  const uint32_t lmask = (1u << lbits) - 1u, dmask = (1u << dbits) - 1u, emask = D64 ? 31u : 15u;
+  const zcode* lt = L.codes;
+  const zcode* dt = L.codes + dofs;
+
+  // ---- lanes: lane j decodes from q = sym0 + j S
+  const bool on = lane < nl;
+  const uint32_t q = sym0 + lane * S;
+  for (uint32_t i = 0; i < ZS_SEG_W / 32; i++) L.bm[lane][i] = 0;
+  for (uint32_t i = 0; i < ZS_SEG_NCK; i++) L.ckp[lane][i] = ZS_SEG_NONE;
+  L.prog[lane] = on ? q : ZS_SEG_NONE;
+  L.conf[lane] = lane == 0;
+  L.absorbed[lane] = 0;
+  L.from[lane] = ~0ull;
+  L.kind[lane] = ZS_SG_K_NONE;
+  L.onchain[lane] = 0;
+  if (lane == 0) {
+    L.done = 0;
+    L.ok = 0;
+    L.bend = 0;
+  }
+  zs_sg_reader G;
+  zs_sg_init(G, src, n);
+  if (on) zs_sg_seek(G, q);
+  uint32_t pos = q, cum = 0, nck = 0, nxt = lane + 1, to = ZS_SEG_NONE, end = 0, last_len = 0;
+  uint32_t pe = lane == 0 ? (r == 0 ? 0u : f) : q;  // the end of the symbol before (events)
+  uint32_t nev = 0, ev_k[ZS_SEG_NEV], ev_sb[ZS_SEG_NEV], ev_c[ZS_SEG_NEV];
+  uint32_t neob = 0, eob_sb[ZS_SEG_NEOB], eob_end[ZS_SEG_NEOB];
+  uint32_t last_bad = ZS_SEG_NONE;
+#pragma unroll
+  for (uint32_t e = 0; e < ZS_SEG_NEV; e++) ev_k[e] = ev_sb[e] = ev_c[e] = 0;
+#pragma unroll
+  for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) eob_sb[e] = eob_end[e] = 0;
+  bool act = on;
+  uint32_t kind = ZS_SG_K_NONE;
+  // (a safety net: every iteration but a stalled one moves a lane on by a bit)
+  const uint32_t max_iter = 2u * (nbits + 64u - sym0) + 4096u;
+  for (uint32_t iter = 0;; iter++) {
+    if (!__syncthreads_or(act) || V.done) break;
+    if (iter > max_iter) {
+      act = false;  // (the block is then not OK)
+      kind = ZS_SG_K_STOP;
+      continue;
+    }
+    if (act && V.absorbed[lane]) {  // the lane before went past this one's window: not on the chain
+      act = false;
+      kind = ZS_SG_K_STOP;
+      V.prog[lane] = ZS_SEG_NONE;
+    }
+    if (act && !V.conf[lane]) {
+      const unsigned long long fr = V.from[lane];
+      if (fr != ~0ull && V.conf[(uint32_t)(fr >> 32)]) V.conf[lane] = 1;
+    }
+    const bool cf = act && V.conf[lane];
+    // a confirmed lane ends the block at its first end-of-block code at or past its start
+    if (cf && neob) {
+      const uint32_t st = lane == 0 ? sym0 : (uint32_t)V.from[lane];
+      bool hit = false;
+#pragma unroll
+      for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
+        if (!hit && e < neob && eob_sb[e] >= st) {
+          hit = true;
+          end = eob_end[e];
+        }
+      if (hit) {
+        act = false;
+        kind = ZS_SG_K_BEND;
+        V.prog[lane] = ZS_SEG_NONE;
+        V.done = 1;
+      } else if (neob > ZS_SEG_NEOB) {
+        act = false;  // the log overflowed: the block's end may be lost (the chain breaks here)
+        kind = ZS_SG_K_STOP;
+        V.prog[lane] = ZS_SEG_NONE;
+        V.done = 1;
+      }
+    }
+    // past the input (the garbage after a block's end): a confirmed lane has lost
+    // the chain; an unconfirmed one waits to be confirmed (its end of block is
+    // logged) or absorbed
+    bool stall = act && pos >= nbits + 64u;
+    if (stall && cf) {
+      act = false;
+      kind = ZS_SG_K_STOP;
+      V.prog[lane] = ZS_SEG_NONE;
+      V.done = 1;
+    }
+    if (act && !stall) {
+      const uint32_t off = pos - q;
+      if (off < ZS_SEG_W) {
+        V.bm[lane][off >> 5] |= 1u << (off & 31u);
+        if (off >= nck * ZS_SEG_CKB) {
+          V.ckp[lane][off / ZS_SEG_CKB] = pos;
+          V.ckc[lane][off / ZS_SEG_CKB] = cum;
+          nck = off / ZS_SEG_CKB + 1u;
+        }
+      }
+      V.prog[lane] = pos;
+      if (nxt < nl && pos >= sym0 + nxt * S) {
+        if (pos >= sym0 + nxt * S + ZS_SEG_W) {
+          // no symbol start in common within the next lane's window: only a
+          // confirmed lane takes the next range over (an unconfirmed one waits to
+          // be confirmed or absorbed)
+          if (!cf) {
+            stall = true;
+          } else {
+            do {
+              V.absorbed[nxt] = 1;
+              nxt++;
+            } while (nxt < nl && pos >= sym0 + nxt * S + ZS_SEG_W);
+          }
+        }
+        if (!stall && nxt < nl && pos >= sym0 + nxt * S) {
+          const uint32_t o2 = pos - (sym0 + nxt * S);
+          if (V.prog[nxt] < pos) {
+            stall = true;  // the next lane has not reached here yet
+          } else if ((V.bm[nxt][o2 >> 5] >> (o2 & 31u)) & 1u) {
+            atomicMin((unsigned long long*)&L.from[nxt], ((unsigned long long)lane << 32) | pos);
+            act = false;
+            kind = ZS_SG_K_SYNC;
+            to = nxt;
+            end = pos;
+            V.prog[lane] = ZS_SEG_NONE;
+          }
+        }
+      }
+    }
+    if (act && !stall) {
+      const uint32_t sb = pos;
+      const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
+      if (y.kind == ZS_SG_BAD) {
+        last_bad = sb;
+        pos = sb + 1u;
+        zs_sg_seek(G, pos);
+        pe = pos;
+      } else {
+        const uint32_t se = zs_sg_bitpos(G);
+        // sub-chunk crossing events: boundaries 262144 k (k >= 1) with pe <= b < se
+        uint32_t bd = (pe + 262143u) & ~262143u;
+        if (bd == 0) bd = 262144u;
+        while (bd < se) {
+#pragma unroll
+          for (uint32_t e = 0; e < ZS_SEG_NEV; e++)
+            if (e == nev) {
+              ev_k[e] = bd >> 18;
+              ev_sb[e] = sb;
+              ev_c[e] = cum;
+            }
+          nev++;
+          bd += 262144u;
+        }
+        if (y.kind == ZS_SG_EOB) {
+#pragma unroll
+          for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
+            if (e == neob) {
+              eob_sb[e] = sb;
+              eob_end[e] = se;
+            }
+          neob++;
+          last_len = 0;
+        } else {
+          cum += y.len;
+          last_len = y.len;
+        }
+        pe = se;
+        pos = se;
+      }
+    }
+  }
+  L.kind[lane] = kind;
+  L.to[lane] = to;
+  __syncthreads();
+  // ---- the chain: lane 0 -> the lane it synced into -> ... -> the end of block
+  if (lane == 0) {
+    uint32_t cur = 0, ok = 0, guard = 0;
+    while (guard++ < ZS_SEG_LANES) {
+      L.onchain[cur] = 1;
+      if (L.kind[cur] == ZS_SG_K_BEND) {
+        ok = 1;
+        break;
+      }
+      if (L.kind[cur] != ZS_SG_K_SYNC) break;
+      const uint32_t nx = L.to[cur];
+      if ((uint32_t)(L.from[nx] >> 32) != cur) break;
+      cur = nx;
+    }
+    L.ok = ok;
+  }
+  __syncthreads();
+  bool bad = false;
+  const bool chain = L.onchain[lane] && L.ok;
+  uint32_t start = ZS_SEG_NONE, cnt = 0;
+  if (chain) {
+    start = lane == 0 ? sym0 : (uint32_t)L.from[lane];
+    // the output count at the start: from the last checkpoint at or before it
+    uint32_t cp = q, cc = 0;
+    for (uint32_t c = 0; c < ZS_SEG_NCK; c++) {
+      const uint32_t p = L.ckp[lane][c];
+      if (p != ZS_SEG_NONE && p <= start) {
+        cp = p;
+        cc = L.ckc[lane][c];
+      }
+    }
+    zs_sg_seek(G, cp);
+    uint32_t p = cp;
+    while (p < start) {
+      const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
+      if (y.kind == ZS_SG_BAD) {
+        p = p + 1u;
+        zs_sg_seek(G, p);
+        continue;
+      }
+      if (y.kind != ZS_SG_EOB) cc += y.len;
+      p = zs_sg_bitpos(G);
+    }
+    bad |= p != start;
+    cnt = cum - cc;
+    // the piece's own events, consecutive sub-chunks
+    uint32_t k0 = 0, ne = 0;
+    uint32_t eo[ZS_SEG_NEV];
+#pragma unroll
+    for (uint32_t e = 0; e < ZS_SEG_NEV; e++) {
+      eo[e] = 0;
+      if (e < nev && ev_sb[e] >= start) {
+        if (ne == 0) k0 = ev_k[e];
+        bad |= ev_k[e] != k0 + ne;
+#pragma unroll
+        for (uint32_t g = 0; g < ZS_SEG_NEV; g++)
+          if (g == ne) eo[g] = ev_c[e] - cc;
+        ne++;
+      }
+    }
+    bad |= nev > ZS_SEG_NEV;
+    // an invalid code, or an end of block before the piece's end, in the true stream
+    bad |= last_bad != ZS_SEG_NONE && last_bad >= start;
+    if (kind == ZS_SG_K_SYNC) {
+#pragma unroll
+      for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) bad |= e < neob && eob_sb[e] >= start;
+    }
+    zs_seg_lane& P = lanes[(size_t)b * ZS_SEG_LANES + lane];
+    P.start = start;
+    P.end = end;
+    P.cnt = cnt;
+    P.last_len = last_len;
+    P.nev = ne;
+    P.ev_k0 = k0;
+#pragma unroll
+    for (uint32_t e = 0; e < ZS_SEG_NEV; e++) P.ev_o[e] = eo[e];
+    if (kind == ZS_SG_K_BEND) L.bend = end;
+  } else if (lane < ZS_SEG_LANES) {
+    lanes[(size_t)b * ZS_SEG_LANES + lane].start = ZS_SEG_NONE;
+  }
+  bad = __syncthreads_or(bad);
+  if (lane == 0) {
+    Bk.hdr = r == 0 ? hdr : f;
+    Bk.sym0 = sym0;
+    Bk.end = L.bend;
+    Bk.lbits = lbits;
+    Bk.dbits = dbits;
+    Bk.dofs = dofs;
+    Bk.nl = nl;
+    Bk.S = S;
+    Bk.flags = (L.ok && !bad ? ZS_SEG_B_OK : 0u) | (last ? ZS_SEG_B_FINAL : 0u);
+  }
+}
+
+// ------------------------------------------------------------------- plan
+// One wave per member: the blocks chained by their ends, the pieces placed,
+// the trailer and the capacity checked, and (REFW) the reference's call state
+// at each piece start -- tools/emu/emu_seg.py models exactly this walk.
+struct zs_sg_calls {
+  uint32_t B, wn, wh, cend;
+  __device__ void end_call(uint32_t at) {  // zs_refcalls_t::end_call
+    const uint32_t produced = at - B;
+    if (produced >= 32768u) {
+      wn = 0;
+      wh = 32768u;
+    } else if (produced) {
+      const uint32_t d = min(32768u - wn, produced), rest = produced - d;
+      if (rest) {
+        wn = rest;
+        wh = 32768u;
+      } else {
+        wn += d;
+        if (wn == 32768u) wn = 0;
+        wh = min(wh + d, 32768u);
+      }
+    }
+    B = at;
+  }
+  __device__ void fills(uint32_t o) {  // the buffer fills a symbol at output position o has triggered
+    while (o >= B + 65536u) end_call(B + 65536u);
+  }
+};
+
+__global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                    const uint32_t* __restrict__ in_len,
+                                                    const uint32_t* __restrict__ out_cap,
+                                                    const uint32_t* __restrict__ list, uint32_t n_list, int wbits,
+                                                    int refw, const uint32_t* __restrict__ cidx,
+                                                    zs_seg_blk* __restrict__ blk, zs_seg_lane* __restrict__ lanes,
+                                                    zs_seg_mem* __restrict__ mem, const uint32_t* __restrict__ pbase,
+                                                    uint32_t* __restrict__ plist) {
+  __shared__ uint32_t bidx[ZS_SPLIT_MAX], bhdr[ZS_SPLIT_MAX], bend[ZS_SPLIT_MAX], bfl[ZS_SPLIT_MAX];
+  __shared__ zs_seg_lane P[ZS_SEG_LANES];
+  __shared__ uint32_t s_bad, s_r, s_next, s_O, s_k, s_prev, s_plen, s_first;
+  __shared__ zs_sg_calls s_C;
+  const uint32_t m = blockIdx.x, lane = threadIdx.x;
+  if (m >= n_list) return;
+  zs_seg_mem& M = mem[m];
+  if (M.bad) return;
+  const uint32_t s = list[m];
+  {
+    const uint32_t bi = cidx[m * ZS_SPLIT_MAX + lane];
+    bidx[lane] = bi;
+    bhdr[lane] = bi != ZS_SEG_NONE ? blk[bi].hdr : ZS_SEG_NONE;
+    bend[lane] = bi != ZS_SEG_NONE ? blk[bi].end : 0u;
+    bfl[lane] = bi != ZS_SEG_NONE ? blk[bi].flags : 0u;
+  }
+  if (lane == 0) {
+    s_bad = 0;
+    s_r = 0;
+    s_O = 0;
+    s_k = 0;
+    s_prev = ZS_SEG_NONE;
+    s_plen = 0;
+    s_first = 1;
+    s_C.B = 0;
+    s_C.wn = 0;
+    s_C.wh = 0;
+    s_C.cend = 32768u;
+  }
+  __syncthreads();
+  const uint32_t pb = pbase[m], pmax = pbase[m + 1] - pb;
+  uint32_t guard = 0;
+  for (;;) {
+    const uint32_t r = s_r;
+    const uint32_t bi = bidx[r];
+    if (s_bad || bi == ZS_SEG_NONE || !(bfl[r] & ZS_SEG_B_OK) || guard++ > ZS_SPLIT_MAX) {
+      if (lane == 0) s_bad = 1;
+      break;
+    }
+    P[lane] = lanes[(size_t)bi * ZS_SEG_LANES + lane];
+    __syncthreads();
+    if (lane == 0) {
+      zs_sg_calls C = s_C;
+      uint32_t O = s_O, k = s_k, prev = s_prev, plen = s_plen;
+      bool first = s_first != 0, bad = false;
+      for (uint32_t l = 0; l < ZS_SEG_LANES && !bad; l++) {
+        zs_seg_lane& p = P[l];
+        if (p.start == ZS_SEG_NONE) continue;
+        bool merge = false;
+        if (!first && refw) {
+          if (l == 0) {
+            C.fills(O);  // the end-of-block code before it, at output O
+          } else {
+            C.fills(O - plen);  // the last symbol of the piece before
+            // a start within 144 bits before a sub-chunk end: the piece before decodes this one too
+            merge = p.start + 144u > 8u * C.cend;
+          }
+        }
+        if (merge) {
+          zs_seg_lane& q = P[prev];  // (the piece before is in this block: l > 0)
+          q.dend = p.end;
+          q.dcnt += p.cnt;
+          p.act = 0;
+        } else {
+          p.O = O;
+          p.off = ((O + 7u) & ~7u) + ZS_SEG_PAD * k;
+          p.dend = p.end;
+          p.dcnt = p.cnt;
+          p.B = C.B;
+          p.wn = C.wn;
+          p.wh = C.wh;
+          p.cend = C.cend;
+          p.act = 1u | (l == 0 ? 0u : 2u);
+          if (k >= pmax) bad = true;
+          else plist[pb + k] = bi * ZS_SEG_LANES + l;
+          k++;
+          prev = l;
+        }
+        if (refw) {
+          for (uint32_t e = 0; e < p.nev; e++) {
+            bad |= 32768u * (p.ev_k0 + e) + 32768u != C.cend;  // events come one sub-chunk at a time
+            const uint32_t o = O + p.ev_o[e];
+            C.fills(o);
+            C.end_call(o);
+            C.cend += 32768u;
+          }
+        }
+        O += p.cnt;
+        plen = p.last_len;
+        first = false;
+      }
+      s_C = C;
+      s_O = O;
+      s_k = k;
+      s_prev = ZS_SEG_NONE;
+      s_plen = plen;
+      s_first = first ? 1u : 0u;
+      if (bad) s_bad = 1;
+      // the next block starts where this one ended
+      uint32_t nx = ZS_SEG_NONE;
+      if (!(bfl[r] & ZS_SEG_B_FINAL))
+        for (uint32_t rr = r + 1; rr < ZS_SPLIT_MAX; rr++)
+          if (bhdr[rr] == bend[r]) {
+            nx = rr;
+            break;
+          }
+      s_next = nx;
+    }
+    __syncthreads();
+    // the pieces' plan back to HBM
+    if (P[lane].start != ZS_SEG_NONE) lanes[(size_t)bi * ZS_SEG_LANES + lane] = P[lane];
+    __syncthreads();
+    if (bfl[r] & ZS_SEG_B_FINAL) break;
+    if (lane == 0) {
+      if (s_next == ZS_SEG_NONE) s_bad = 1;
+      else s_r = s_next;
+    }
+    __syncthreads();
+    if (s_bad) break;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    bool bad = s_bad != 0;
+    const uint32_t total = s_O;
+    const uint32_t n = in_len[s];
+    const uint32_t e = bend[s_r];
+    uint32_t consumed = (e + 7u) >> 3, want = 0;
+    const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;
+    if (!bad && wrap) {  // the trailer (inflate.ts:1006-1036); the check value is verified after the checksum pass
+      const uint8_t* t = in + in_off[s] + consumed;
+      if (wrap & 2 && !(wrap & 1)) {
+        if (consumed + 8u > n) bad = true;
+        else {
+          want = (uint32_t)t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
+          const uint32_t isize = (uint32_t)t[4] | (uint32_t)t[5] << 8 | (uint32_t)t[6] << 16 | (uint32_t)t[7] << 24;
+          bad |= isize != total;
+          consumed += 8u;
+        }
+      } else {
+        if (consumed + 4u > n) bad = true;
+        else {
+          want = (uint32_t)t[0] << 24 | (uint32_t)t[1] << 16 | (uint32_t)t[2] << 8 | (uint32_t)t[3];
+          consumed += 4u;
+        }
+      }
+    }
+    if (!bad && consumed > n) bad = true;
+    if (total > out_cap[s]) bad = true;  // the exact path reports the capacity
+    M.bad = bad ? 1u : 0u;
+    M.total = total;
+    M.consumed = consumed;
+    M.want = want;
+    M.npieces = s_k;
+  }
+}
+
+// ----------------------------------------------------------------- decode
+// One lane's u16 output (bytes, or markers 255 + k: the value k positions
+// before the piece): a 64-value LDS ring, whole 16-byte units to HBM (the
+// piece's scratch is 16-byte aligned and padded, so no unit is shared).
+struct zs_sg_out {
+  uint16_t* dst;
+  uint16_t* ring;
+  uint32_t P, F;
+  __device__ __forceinline__ void put(uint32_t v) {
+    ring[P & 63u] = (uint16_t)v;
+    P++;
+  }
+  __device__ __forceinline__ void flush() {
+    while (F + 8u <= P) {
+      *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & 63u));
+      F += 8u;
+    }
+  }
+  __device__ __forceinline__ void room(uint32_t k) {  // room for k more values
+    if (P + k - F > 64u) flush();
+  }
+  // the value at piece position x < P: the ring holds the last 64, older ones are stored
+  __device__ __forceinline__ uint32_t get(uint32_t x) const { return x + 64u >= P ? ring[x & 63u] : dst[x]; }
+  __device__ __forceinline__ void finish() {
+    flush();
+    if (F < P) *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & 63u));
+  }
+};
+
+// n values from piece position x0 (negative: markers for the history before
+// the piece); false: a marker further back than a u16 says
+static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint32_t n) {
+  const int32_t d = (int32_t)W.P - x0;
+  if (x0 >= 0 && d >= 8) {
+    for (uint32_t i = 0; i < n; i += 8) {
+      W.room(8);
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) v[j] = W.get((uint32_t)x0 + i + j);
+      const uint32_t k = min(8u, n - i);
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++)
+        if (j < k) W.put(v[j]);
+    }
+    return true;
+  }
+  if (x0 >= 0) {  // period d < 8
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) v[j] = (int32_t)j < d ? W.get((uint32_t)x0 + j) : 0u;
+    uint32_t j = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      if ((i & 7u) == 0) W.room(8);
+      uint32_t x = v[0];
+#pragma unroll
+      for (uint32_t t = 1; t < 8; t++) x = t == j ? v[t] : x;
+      W.put(x);
+      j = j + 1 == (uint32_t)d ? 0u : j + 1;
+    }
+    return true;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    const int32_t x = x0 + (int32_t)i;
+    uint32_t v;
+    if (x < 0) {
+      const uint32_t back = (uint32_t)(-x);
+      if (back > ZS_SPLIT_MARK_MAX) return false;
+      v = 255u + back;
+    } else {
+      v = W.get((uint32_t)x);
+    }
+    if ((i & 7u) == 0) W.room(8);
+    W.put(v);
+  }
+  return true;
+}
+
+template <bool D64, bool REFW>
+__global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict__ in,
+                                                      const uint64_t* __restrict__ in_off,
+                                                      const uint32_t* __restrict__ in_len,
+                                                      const uint32_t* __restrict__ list,
+                                                      const uint32_t* __restrict__ counter,
+                                                      const zs_seg_blk* __restrict__ blk,
+                                                      const zs_seg_lane* __restrict__ lanes,
+                                                      const zcode* __restrict__ tcache, zs_seg_mem* __restrict__ mem,
+                                                      const uint64_t* __restrict__ sbase,
+                                                      uint16_t* __restrict__ scratch) {
+  __shared__ zcode codes[ZS_SEG_TAB];
+  __shared__ __attribute__((aligned(16))) uint16_t ring[ZS_SEG_LANES][64];
+  const uint32_t b = blockIdx.x, lane = threadIdx.x;
+  if (b >= *counter) return;
+  const zs_seg_blk& Bk = blk[b];
+  const uint32_t m = zs_u(Bk.m);
+  if (m == ZS_SEG_NONE || !(Bk.flags & ZS_SEG_B_OK) || mem[m].bad) return;
+  const uint32_t ntab = ZS_SEG_TAB;
+  for (uint32_t i = lane; i < ntab; i += 64) codes[i] = tcache[(size_t)b * ZS_SEG_TAB + i];
+  __syncthreads();
+  const zs_seg_lane& p = lanes[(size_t)b * ZS_SEG_LANES + lane];
+  if (lane >= zs_u(Bk.nl) || p.start == ZS_SEG_NONE || !(p.act & 1u)) return;
+  const uint32_t s = list[m];
+  const uint32_t lmask = (1u << Bk.lbits) - 1u, dmask = (1u << Bk.dbits) - 1u, emask = D64 ? 31u : 15u;
+  const zcode* lt = codes;
+  const zcode* dt = codes + Bk.dofs;
+  zs_sg_reader G;
+  zs_sg_init(G, in + in_off[s], in_len[s]);
+  zs_sg_seek(G, p.start);
+  zs_sg_out W;
+  W.dst = scratch + sbase[m] + p.off;
+  W.ring = ring[lane];
+  W.P = 0;
+  W.F = 0;
+  const uint32_t O = p.O, dend = p.dend;
+  zs_refcalls_t<uint32_t> C;
+  C.B = p.B;
+  C.wn = p.wn;
+  C.wh = p.wh;
+  C.cend = p.cend;
+  C.fast = (p.act >> 1) & 1u;
+  C.sfar = 8u * C.cend - 96u;
+  C.ofar = C.B + 65536u - 516u;
+  bool bad = false;
+  uint32_t sb = p.start;
+  while (sb < dend) {
+    if (W.P - W.F >= 32u) W.flush();
+    const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
+    const uint32_t o = O + W.P;
+    if (y.kind == ZS_SG_LIT) {
+      if (REFW) C.symbol(sb, o, 1u, y.l1, 0u, 0u, 0u, false);
+      W.room(1);
+      W.put(y.val);
+    } else if (y.kind == ZS_SG_COPY) {
+      if (y.val > o) {  // "invalid distance too far back": the exact path reports it
+        bad = true;
+        break;
+      }
+      uint32_t tail = 0;
+      if (REFW && C.symbol(sb, o, y.len, y.l1, y.e1, y.l2, y.e2, false)) tail = C.wrap(o, y.len, y.val);
+      if (!zs_sg_copy(W, (int32_t)W.P - (int32_t)y.val, y.len - tail)) {
+        bad = true;
+        break;
+      }
+      // the window-wrap copy: the call's first output bytes (from C.B on)
+      if (tail && !zs_sg_copy(W, (int32_t)C.B - (int32_t)O, tail)) {
+        bad = true;
+        break;
+      }
+    } else if (y.kind == ZS_SG_EOB) {
+      if (REFW) C.symbol(sb, o, 0u, y.l1, 0u, 0u, 0u, true);
+      bad = zs_sg_bitpos(G) != dend;  // only the block's last piece ends with its end of block
+      break;
+    } else {
+      bad = true;
+      break;
+    }
+    sb = zs_sg_bitpos(G);
+  }
+  bad |= sb > dend || W.P != p.dcnt;
+  if (!bad) W.finish();
+  if (bad) atomicOr(&mem[m].bad, 1u);
+}
+
+// ---------------------------------------------------------------- resolve
+// One workgroup per member: the pieces in order; a piece's markers name bytes
+// before its start, all final by then -- in the LDS ring of the last 64 KiB,
+// or (rarely: a marker carried far into a long piece) in the output already
+// stored.  Bytes leave as whole words.
+#define ZS_SG_RES_T 256u
+#define ZS_SG_RES_E 4u  // values per thread per round
+__global__ __launch_bounds__(256) void zs_k_seg_resolve(const uint32_t* __restrict__ list,
+                                                        const zs_seg_mem* __restrict__ mem,
+                                                        const zs_seg_lane* __restrict__ lanes,
+                                                        const uint32_t* __restrict__ pbase,
+                                                        const uint32_t* __restrict__ plist,
+                                                        const uint64_t* __restrict__ sbase,
+                                                        const uint16_t* __restrict__ scratch, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_off,
+                                                        zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out,
+                                                        uint32_t* __restrict__ n_ok) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t zs_rring[];  // 64 KiB of bytes
+  uint8_t* ring = reinterpret_cast<uint8_t*>(zs_rring);
+  const uint32_t m = blockIdx.x, t = threadIdx.x;
+  const uint32_t s = list[m];
+  const zs_seg_mem M = mem[m];
+  if (M.bad) {
+    if (t == 0) {
+      zs_lane_res r = {1u, 0u, 0u, 0u};
+      res[s] = r;
+      lens_out[s] = 0;
+    }
+    return;
+  }
+  uint32_t* dst = reinterpret_cast<uint32_t*>(out + out_off[s]);
+  const uint16_t* scr = scratch + sbase[m];
+  const uint32_t pb = pbase[m];
+  uint32_t wdone = 0;  // words stored
+  bool far = false;
+  for (uint32_t k = 0; k < M.npieces; k++) {
+    const zs_seg_lane& p = lanes[plist[pb + k]];
+    const uint32_t O = p.O, cnt = p.dcnt, off = p.off;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += ZS_SG_RES_T * ZS_SG_RES_E) {
+      uint32_t v[ZS_SG_RES_E];
+#pragma unroll
+      for (uint32_t e = 0; e < ZS_SG_RES_E; e++) {
+        const uint32_t i = i0 + e * ZS_SG_RES_T + t;
+        v[e] = 0;
+        if (i < cnt) {
+          const uint32_t x = scr[off + i];
+          if (x < 256u) {
+            v[e] = x;
+          } else {
+            const uint32_t tg = O - (x - 255u);
+            if (O + i - tg < 65536u - ZS_SG_RES_T * ZS_SG_RES_E) {
+              v[e] = ring[tg & 0xffffu];
+            } else if ((tg >> 2) < wdone) {
+              const uint32_t w = __hip_atomic_load(dst + (tg >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              v[e] = (w >> (8u * (tg & 3u))) & 0xffu;
+            } else {
+              far = true;  // a byte of the word not yet stored, out of the ring: the other paths decode it
+            }
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t e = 0; e < ZS_SG_RES_E; e++) {
+        const uint32_t i = i0 + e * ZS_SG_RES_T + t;
+        if (i < cnt) ring[(O + i) & 0xffffu] = (uint8_t)v[e];
+      }
+      __syncthreads();
+    }
+    // the words now complete
+    const uint32_t wend = (O + cnt) >> 2;
+    for (uint32_t w = wdone + t; w < wend; w += ZS_SG_RES_T) dst[w] = zs_rring[w & 0x3fffu];
+    wdone = wend;
+    __threadfence();
+    __syncthreads();
+  }
+  if (M.total & 3u) {
+    if (t == 0) dst[wdone] = zs_rring[wdone & 0x3fffu];  // the last word's bytes past the end lie inside the capacity
+  }
+  far = __syncthreads_or(far);
+  if (t == 0) {
+    if (!far) atomicAdd(n_ok, 1u);  // (statistics: zs_last_inflate_seg_count)
+    zs_lane_res r = {far ? 1u : 0u, far ? 0u : M.total, M.consumed, M.want};
+    res[s] = r;
+    lens_out[s] = M.total;
+  }
+}
+
+template __global__ void zs_k_seg_sync<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, int,
+                                              const uint64_t*, const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*,
+                                              uint32_t);
+template __global__ void zs_k_seg_sync<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, int,
+                                             const uint64_t*, const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*,
+                                             uint32_t);
+#define ZS_SEG_DEC_INST(D, W)                                                                                       \
+  template __global__ void zs_k_seg_decode<D, W>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, \
+                                                 const uint32_t*, const zs_seg_blk*, const zs_seg_lane*,           \
+                                                 const zcode*, zs_seg_mem*, const uint64_t*, uint16_t*);
+ZS_SEG_DEC_INST(false, false)
+ZS_SEG_DEC_INST(false, true)
+ZS_SEG_DEC_INST(true, false)

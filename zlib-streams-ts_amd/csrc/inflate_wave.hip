@@ -51,7 +51,8 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
                                                         const uint64_t* __restrict__ out_off,
                                                         const uint32_t* __restrict__ out_cap, int wbits,
                                                         const uint32_t* __restrict__ list, uint32_t n_list,
-                                                        zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out) {
+                                                        zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out,
+                                                        uint32_t skip_done) {
   extern __shared__ __attribute__((aligned(16))) uint8_t zs_wsm[];
   const bool d64 = wbits == -16;
   uint8_t* ring = zs_wsm;
@@ -60,6 +61,8 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
   if (blockIdx.x >= n_list) return;
   const uint32_t lane = threadIdx.x;
   const uint32_t s = zs_u(list[blockIdx.x]);
+  // skip_done: the members the segmented decode (inflate_seg.hip) finished already
+  if (skip_done && zs_u(res[s].bail) == 0) return;
   const uint8_t* src = in + in_off[s];
   zs_wave_reader R;
   R.n = zs_u(in_len[s]);
@@ -285,7 +288,7 @@ size_t zs_inflate_wave_lds_bytes(bool d64) { return zs_wave_ring_bytes(d64) + si
 
 template __global__ void zs_k_inflate_wave<false>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                                   const uint64_t*, const uint32_t*, int, const uint32_t*, uint32_t,
-                                                  zs_lane_res*, uint32_t*);
+                                                  zs_lane_res*, uint32_t*, uint32_t);
 template __global__ void zs_k_inflate_wave<true>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                                  const uint64_t*, const uint32_t*, int, const uint32_t*, uint32_t,
-                                                 zs_lane_res*, uint32_t*);
+                                                 zs_lane_res*, uint32_t*, uint32_t);

@@ -125,6 +125,8 @@ def lib():
     L.zs_last_batch_ms.argtypes = [_P]
     L.zs_last_inflate_lane_count.restype = ctypes.c_uint32
     L.zs_last_inflate_lane_count.argtypes = [_P]
+    L.zs_last_inflate_seg_count.restype = ctypes.c_uint32
+    L.zs_last_inflate_seg_count.argtypes = [_P]
     L.zs_last_phase_ms.restype = ctypes.c_double
     L.zs_last_phase_ms.argtypes = [_P, ctypes.c_char_p]
     L.zs_set_timing.argtypes = [_P, ctypes.c_int]
@@ -221,6 +223,10 @@ class Engine:
     def last_lane_count(self) -> int:
         """members of the last inflate batch decoded by the lane path"""
         return self._L.zs_last_inflate_lane_count(self._ctx)
+
+    def last_seg_count(self) -> int:
+        """members of the last inflate batch the segmented decode finished (inflate_seg.hip)"""
+        return self._L.zs_last_inflate_seg_count(self._ctx)
 
     def last_ms(self, phase: Optional[str] = None) -> float:
         if phase is None:
