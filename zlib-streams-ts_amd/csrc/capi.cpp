@@ -831,6 +831,17 @@ extern "C" void zs_corpus(int kind, uint32_t first, uint32_t n_streams, uint32_t
 // 2 symbols (u32 each; count = streams[s].nsym), 3 blocks (zs_block each),
 // 4 stream record (zs_stream).  Returns the number of bytes copied.
 extern "C" uint64_t zs_debug_fetch(zs_ctx* c, int what, uint32_t s, void* dst, uint64_t cap) {
+  if (c && what >= 16 && what <= 20) {
+    // the segmented decode's records of the last inflate batch: 16 counters (blocks, members
+    // finished), 17 blocks (zs_seg_blk), 18 lanes (zs_seg_lane), 19 members (zs_seg_mem), 20 found[]
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    const Buf* b = what == 16 ? &c->gcnt : what == 17 ? &c->gblk : what == 18 ? &c->glanes : what == 19 ? &c->gmem
+                                                                                                  : &c->gfound;
+    const uint64_t bytes = std::min<uint64_t>(cap, b->cap);
+    if (!b->p || !bytes || hipMemcpy(dst, b->p, bytes, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return bytes;
+  }
   if (!c || !c->streams.p) return 0;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);

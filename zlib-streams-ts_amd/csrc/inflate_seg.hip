@@ -358,12 +358,13 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
   uint32_t pos = q, cum = 0, nck = 0, nxt = lane + 1, to = ZS_SEG_NONE, end = 0, last_len = 0;
   uint32_t pe = lane == 0 ? (r == 0 ? 0u : f) : q;  // the end of the symbol before (events)
   uint32_t nev = 0, ev_k[ZS_SEG_NEV], ev_sb[ZS_SEG_NEV], ev_c[ZS_SEG_NEV];
-  uint32_t neob = 0, eob_sb[ZS_SEG_NEOB], eob_end[ZS_SEG_NEOB];
-  uint32_t last_bad = ZS_SEG_NONE;
+  uint32_t neob = 0, eob_sb[ZS_SEG_NEOB], eob_end[ZS_SEG_NEOB], eob_cum[ZS_SEG_NEOB];
+  uint32_t nbad = 0, bad_sb[ZS_SEG_NEOB];  // invalid codes met (garbage before the start / past the end, or an error)
+  uint32_t cum_end = 0;
 #pragma unroll
   for (uint32_t e = 0; e < ZS_SEG_NEV; e++) ev_k[e] = ev_sb[e] = ev_c[e] = 0;
 #pragma unroll
-  for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) eob_sb[e] = eob_end[e] = 0;
+  for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) eob_sb[e] = eob_end[e] = eob_cum[e] = bad_sb[e] = 0;
   bool act = on;
   uint32_t kind = ZS_SG_K_NONE;
   // (a safety net: every iteration but a stalled one moves a lane on by a bit)
@@ -380,7 +381,9 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
       kind = ZS_SG_K_STOP;
       V.prog[lane] = ZS_SEG_NONE;
     }
-    if (act && !V.conf[lane]) {
+    // confirmation travels down the chain one lane per iteration, through lanes
+    // that have stopped already too
+    if (on && !V.conf[lane]) {
       const unsigned long long fr = V.from[lane];
       if (fr != ~0ull && V.conf[(uint32_t)(fr >> 32)]) V.conf[lane] = 1;
     }
@@ -394,6 +397,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
         if (!hit && e < neob && eob_sb[e] >= st) {
           hit = true;
           end = eob_end[e];
+          cum_end = eob_cum[e];  // (the lane may have decoded on past it, waiting to be confirmed)
         }
       if (hit) {
         act = false;
@@ -452,6 +456,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
             kind = ZS_SG_K_SYNC;
             to = nxt;
             end = pos;
+            cum_end = cum;
             V.prog[lane] = ZS_SEG_NONE;
           }
         }
@@ -461,7 +466,10 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
       const uint32_t sb = pos;
       const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
       if (y.kind == ZS_SG_BAD) {
-        last_bad = sb;
+#pragma unroll
+        for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
+          if (e == nbad) bad_sb[e] = sb;
+        nbad++;
         pos = sb + 1u;
         zs_sg_seek(G, pos);
         pe = pos;
@@ -487,6 +495,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
             if (e == neob) {
               eob_sb[e] = sb;
               eob_end[e] = se;
+              eob_cum[e] = cum;
             }
           neob++;
           last_len = 0;
@@ -546,14 +555,15 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
       p = zs_sg_bitpos(G);
     }
     bad |= p != start;
-    cnt = cum - cc;
+    cnt = cum_end - cc;
+    if (kind == ZS_SG_K_BEND) last_len = 0;
     // the piece's own events, consecutive sub-chunks
     uint32_t k0 = 0, ne = 0;
     uint32_t eo[ZS_SEG_NEV];
 #pragma unroll
     for (uint32_t e = 0; e < ZS_SEG_NEV; e++) {
       eo[e] = 0;
-      if (e < nev && ev_sb[e] >= start) {
+      if (e < nev && ev_sb[e] >= start && ev_sb[e] < end) {
         if (ne == 0) k0 = ev_k[e];
         bad |= ev_k[e] != k0 + ne;
 #pragma unroll
@@ -562,9 +572,10 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
         ne++;
       }
     }
-    bad |= nev > ZS_SEG_NEV;
+    bad |= nev > ZS_SEG_NEV || nbad > ZS_SEG_NEOB || neob > ZS_SEG_NEOB;
     // an invalid code, or an end of block before the piece's end, in the true stream
-    bad |= last_bad != ZS_SEG_NONE && last_bad >= start;
+#pragma unroll
+    for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) bad |= e < nbad && bad_sb[e] >= start && bad_sb[e] < end;
     if (kind == ZS_SG_K_SYNC) {
 #pragma unroll
       for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) bad |= e < neob && eob_sb[e] >= start;
@@ -713,7 +724,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
         }
         if (refw) {
           for (uint32_t e = 0; e < p.nev; e++) {
-            bad |= 32768u * (p.ev_k0 + e) + 32768u != C.cend;  // events come one sub-chunk at a time
+            bad |= 32768u * (p.ev_k0 + e) != C.cend;  // events come one sub-chunk at a time (boundary k: cend = 32768 k)
             const uint32_t o = O + p.ev_o[e];
             C.fills(o);
             C.end_call(o);
