@@ -971,7 +971,7 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   HIPCHK(c->gtab.ensure(sizeof(zcode) * ZS_SEG_TAB * cap_blocks));
   HIPCHK(c->gmem.ensure(sizeof(zs_seg_mem) * ng));
   HIPCHK(c->gpbase.ensure(4ull * (ng + 1)));
-  HIPCHK(c->gplist.ensure(4ull * c->hgpbase[ng] + 16));
+  HIPCHK(c->gplist.ensure(16ull * c->hgpbase[ng] + 16));
   HIPCHK(c->gsbase.ensure(8ull * (ng + 1)));
   HIPCHK(c->gscr.ensure(2ull * c->hgsbase[ng] + 64));
   HIPCHK(c->gcnt.ensure(16));
@@ -991,7 +991,7 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   zcode* gt = c->gtab.as<zcode>();
   zs_seg_mem* gm = c->gmem.as<zs_seg_mem>();
   const uint32_t nb = (uint32_t)cap_blocks;
-  zs_k_split_find<<<ng * ZS_SPLIT_MAX, 1024, 0, sd>>>(d_in, d_ioff, d_ilen, gl, wbits, gf);
+  zs_k_split_find<<<ng * ZS_SPLIT_MAX, 256, 0, sd>>>(d_in, d_ioff, d_ilen, gl, wbits, gf);
   zs_k_seg_alloc<<<ng, 64, 0, sd>>>(gf, ng, c->gcidx.as<uint32_t>(), gb, cnt, nb, gm);
   if (int r = mark(c, sd, "seg_find")) return r;
   if (d64)
@@ -1001,7 +1001,7 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   if (int r = mark(c, sd, "seg_sync")) return r;
   zs_k_seg_plan<<<ng, 64, 0, sd>>>(d_in, d_ioff, d_ilen, d_ocap, gl, ng, wbits, refw ? 1 : 0,
                                    c->gcidx.as<uint32_t>(), gb, gln, gm, c->gpbase.as<uint32_t>(),
-                                   c->gplist.as<uint32_t>());
+                                   c->gplist.as<uint4>());
   if (int r = mark(c, sd, "seg_plan")) return r;
   const uint64_t* sb = c->gsbase.as<uint64_t>();
   uint16_t* scr = c->gscr.as<uint16_t>();
@@ -1013,8 +1013,8 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
     zs_k_seg_decode<false, false><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt, gb, gln, gt, gm, sb, scr);
   if (int r = mark(c, sd, "seg_decode")) return r;
   HIPCHK(hipFuncSetAttribute((const void*)zs_k_seg_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-  zs_k_seg_resolve<<<ng, 256, 65536, sd>>>(gl, gm, gln, c->gpbase.as<uint32_t>(), c->gplist.as<uint32_t>(), sb, scr,
-                                           d_out, d_ooff, lres, c->llen.as<uint32_t>(), cnt + 1);
+  zs_k_seg_resolve<<<ng, 512, 65536, sd>>>(gl, gm, c->gpbase.as<uint32_t>(), c->gplist.as<uint4>(), sb, scr, d_out,
+                                           d_ooff, lres, c->llen.as<uint32_t>(), cnt + 1);
   if (int r = mark(c, sd, "seg_resolve")) return r;
   // members the pieces could not finish: the wave kernel (skip_done), then the exact kernel
   const size_t wsm = zs_inflate_wave_lds_bytes(d64);
@@ -1165,7 +1165,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       const uint32_t* sl = c->slist.as<uint32_t>();
       uint64_t* sf = c->sfound.as<uint64_t>();
       zs_split_piece_res* sp = c->spres.as<zs_split_piece_res>();
-      zs_k_split_find<<<ns * ZS_SPLIT_MAX, 1024, 0, c->side>>>(d_in, d_ioff, d_ilen, sl, wbits, sf);
+      zs_k_split_find<<<ns * ZS_SPLIT_MAX, 256, 0, c->side>>>(d_in, d_ioff, d_ilen, sl, wbits, sf);
       if (int r = mark(c, c->side, "split_find")) return r;
       const size_t ssm = zs_split_lds_bytes(wbits == -16);
       HIPCHK(hipFuncSetAttribute((const void*)zs_k_split_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ssm));

@@ -643,7 +643,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
                                                     int refw, const uint32_t* __restrict__ cidx,
                                                     zs_seg_blk* __restrict__ blk, zs_seg_lane* __restrict__ lanes,
                                                     zs_seg_mem* __restrict__ mem, const uint32_t* __restrict__ pbase,
-                                                    uint32_t* __restrict__ plist) {
+                                                    uint4* __restrict__ ptab) {
   __shared__ uint32_t bidx[ZS_SPLIT_MAX], bhdr[ZS_SPLIT_MAX], bend[ZS_SPLIT_MAX], bfl[ZS_SPLIT_MAX];
   __shared__ zs_seg_lane P[ZS_SEG_LANES];
   __shared__ uint32_t s_bad, s_r, s_next, s_O, s_k, s_prev, s_plen, s_first;
@@ -707,6 +707,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
           q.dend = p.end;
           q.dcnt += p.cnt;
           p.act = 0;
+          if (k - 1 < pmax) ptab[pb + k - 1].y = q.dcnt;
         } else {
           p.O = O;
           p.off = ((O + 7u) & ~7u) + ZS_SEG_PAD * k;
@@ -718,7 +719,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
           p.cend = C.cend;
           p.act = 1u | (l == 0 ? 0u : 2u);
           if (k >= pmax) bad = true;
-          else plist[pb + k] = bi * ZS_SEG_LANES + l;
+          else ptab[pb + k] = make_uint4(O, p.cnt, p.off, 0u);
           k++;
           prev = l;
         }
@@ -963,23 +964,28 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
 }
 
 // ---------------------------------------------------------------- resolve
-// One workgroup per member: the pieces in order; a piece's markers name bytes
-// before its start, all final by then -- in the LDS ring of the last 64 KiB,
-// or (rarely: a marker carried far into a long piece) in the output already
-// stored.  Bytes leave as whole words.
-#define ZS_SG_RES_T 256u
-#define ZS_SG_RES_E 4u  // values per thread per round
-__global__ __launch_bounds__(256) void zs_k_seg_resolve(const uint32_t* __restrict__ list,
+// One workgroup per member: the pieces in order (the plan's table: output
+// position, values, scratch offset); a piece's markers name bytes before its
+// start, all final by then -- in the LDS ring of the last 64 KiB, or (rarely: a
+// marker carried far into a long piece) in the output already stored.  A round
+// covers up to 4,096 values of one piece; the next round's values are loaded
+// before this one's markers are looked up.  Bytes leave as whole words, 16 KiB
+// at a time.
+#define ZS_SG_RES_T 512u
+#define ZS_SG_RES_E 8u                                  // values per thread per round
+#define ZS_SG_RES_R (ZS_SG_RES_T * ZS_SG_RES_E)        // values per round
+#define ZS_SG_RES_PT 512u                               // piece-table entries staged in LDS
+__global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restrict__ list,
                                                         const zs_seg_mem* __restrict__ mem,
-                                                        const zs_seg_lane* __restrict__ lanes,
                                                         const uint32_t* __restrict__ pbase,
-                                                        const uint32_t* __restrict__ plist,
+                                                        const uint4* __restrict__ ptab,
                                                         const uint64_t* __restrict__ sbase,
                                                         const uint16_t* __restrict__ scratch, uint8_t* __restrict__ out,
                                                         const uint64_t* __restrict__ out_off,
                                                         zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out,
                                                         uint32_t* __restrict__ n_ok) {
   extern __shared__ __attribute__((aligned(16))) uint32_t zs_rring[];  // 64 KiB of bytes
+  __shared__ uint4 tab[ZS_SG_RES_PT];
   uint8_t* ring = reinterpret_cast<uint8_t*>(zs_rring);
   const uint32_t m = blockIdx.x, t = threadIdx.x;
   const uint32_t s = list[m];
@@ -994,49 +1000,76 @@ __global__ __launch_bounds__(256) void zs_k_seg_resolve(const uint32_t* __restri
   }
   uint32_t* dst = reinterpret_cast<uint32_t*>(out + out_off[s]);
   const uint16_t* scr = scratch + sbase[m];
-  const uint32_t pb = pbase[m];
+  const uint4* pt = ptab + pbase[m];
+  const uint32_t np = M.npieces;
   uint32_t wdone = 0;  // words stored
   bool far = false;
-  for (uint32_t k = 0; k < M.npieces; k++) {
-    const zs_seg_lane& p = lanes[plist[pb + k]];
-    const uint32_t O = p.O, cnt = p.dcnt, off = p.off;
-    for (uint32_t i0 = 0; i0 < cnt; i0 += ZS_SG_RES_T * ZS_SG_RES_E) {
-      uint32_t v[ZS_SG_RES_E];
+  uint32_t tb = 0;     // the staged table's first piece
+  for (uint32_t i = t; i < ZS_SG_RES_PT && i < np; i += ZS_SG_RES_T) tab[i] = pt[i];
+  __syncthreads();
+  // the current round (piece k from value i0) and its values
+  uint32_t k = 0, i0 = 0;
+  uint32_t cur[ZS_SG_RES_E], nxt[ZS_SG_RES_E];
+  auto load = [&](const uint4& e, uint32_t j0, uint32_t (&v)[ZS_SG_RES_E]) {
 #pragma unroll
-      for (uint32_t e = 0; e < ZS_SG_RES_E; e++) {
-        const uint32_t i = i0 + e * ZS_SG_RES_T + t;
-        v[e] = 0;
-        if (i < cnt) {
-          const uint32_t x = scr[off + i];
-          if (x < 256u) {
-            v[e] = x;
-          } else {
-            const uint32_t tg = O - (x - 255u);
-            if (O + i - tg < 65536u - ZS_SG_RES_T * ZS_SG_RES_E) {
-              v[e] = ring[tg & 0xffffu];
-            } else if ((tg >> 2) < wdone) {
-              const uint32_t w = __hip_atomic_load(dst + (tg >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              v[e] = (w >> (8u * (tg & 3u))) & 0xffu;
-            } else {
-              far = true;  // a byte of the word not yet stored, out of the ring: the other paths decode it
-            }
-          }
+    for (uint32_t q = 0; q < ZS_SG_RES_E; q++) {
+      const uint32_t i = j0 + q * ZS_SG_RES_T + t;
+      v[q] = i < e.y ? scr[e.z + i] : 0u;
+    }
+  };
+  if (np) load(tab[0], 0, cur);
+  while (k < np) {
+    const uint4 e = tab[k - tb];
+    uint32_t k2 = k, j2 = i0 + ZS_SG_RES_R;
+    if (j2 >= e.y) {
+      k2 = k + 1;
+      j2 = 0;
+    }
+    const bool restage = k2 < np && k2 - tb >= ZS_SG_RES_PT;
+    if (k2 < np && !restage) load(tab[k2 - tb], j2, nxt);
+    // this round's markers
+    const uint32_t O = e.x;
+#pragma unroll
+    for (uint32_t q = 0; q < ZS_SG_RES_E; q++) {
+      const uint32_t i = i0 + q * ZS_SG_RES_T + t;
+      const uint32_t x = cur[q];
+      if (i < e.y && x >= 256u) {
+        const uint32_t tg = O - (x - 255u);
+        if (O + i - tg < 65536u - ZS_SG_RES_R) {
+          cur[q] = ring[tg & 0xffffu];
+        } else if ((tg >> 2) < wdone) {
+          const uint32_t w = __hip_atomic_load(dst + (tg >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          cur[q] = (w >> (8u * (tg & 3u))) & 0xffu;
+        } else {
+          far = true;  // a byte of a word not stored yet, out of the ring: the other paths decode the member
         }
       }
-      __syncthreads();
+    }
+    __syncthreads();
 #pragma unroll
-      for (uint32_t e = 0; e < ZS_SG_RES_E; e++) {
-        const uint32_t i = i0 + e * ZS_SG_RES_T + t;
-        if (i < cnt) ring[(O + i) & 0xffffu] = (uint8_t)v[e];
-      }
+    for (uint32_t q = 0; q < ZS_SG_RES_E; q++) {
+      const uint32_t i = i0 + q * ZS_SG_RES_T + t;
+      if (i < e.y) ring[(O + i) & 0xffffu] = (uint8_t)cur[q];
+    }
+    __syncthreads();
+    // the complete words, 16 KiB at a time (and at the end)
+    const uint32_t wend = k2 >= np ? (O + e.y) >> 2 : (k2 == k ? (O + j2) >> 2 : (O + e.y) >> 2);
+    if (wend - wdone >= 4096u || k2 >= np) {
+      for (uint32_t w = wdone + t; w < wend; w += ZS_SG_RES_T) dst[w] = zs_rring[w & 0x3fffu];
+      wdone = wend;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // (far markers read them back)
       __syncthreads();
     }
-    // the words now complete
-    const uint32_t wend = (O + cnt) >> 2;
-    for (uint32_t w = wdone + t; w < wend; w += ZS_SG_RES_T) dst[w] = zs_rring[w & 0x3fffu];
-    wdone = wend;
-    __threadfence();
-    __syncthreads();
+    if (restage) {  // the next table entries (a member of more than ZS_SG_RES_PT pieces)
+      tb = k2;
+      for (uint32_t i = t; i < ZS_SG_RES_PT && tb + i < np; i += ZS_SG_RES_T) tab[i] = pt[tb + i];
+      __syncthreads();
+      load(tab[0], j2, nxt);
+    }
+    k = k2;
+    i0 = j2;
+#pragma unroll
+    for (uint32_t q = 0; q < ZS_SG_RES_E; q++) cur[q] = nxt[q];
   }
   if (M.total & 3u) {
     if (t == 0) dst[wdone] = zs_rring[wdone & 0x3fffu];  // the last word's bytes past the end lie inside the capacity
@@ -1046,7 +1079,7 @@ __global__ __launch_bounds__(256) void zs_k_seg_resolve(const uint32_t* __restri
     if (!far) atomicAdd(n_ok, 1u);  // (statistics: zs_last_inflate_seg_count)
     zs_lane_res r = {far ? 1u : 0u, far ? 0u : M.total, M.consumed, M.want};
     res[s] = r;
-    lens_out[s] = M.total;
+    lens_out[s] = far ? 0u : M.total;
   }
 }
 

@@ -7,9 +7,10 @@
 // member is cut at its block boundaries and the pieces decode in parallel:
 //
 //  1. zs_k_split_find: the member's bits are divided into ZS_SPLIT_MAX ranges;
-//     one workgroup per range tests every bit offset of its range (1024
-//     threads, no barriers: a lane stops past the best start so far) for the start of a dynamic-Huffman block header that zlib would
-//     accept (zs_split_header_ok: a complete code-length code, code lengths
+//     one workgroup per range tests every bit offset of its range (32 at a
+//     time per thread, candidates queued for the full check) for the start of a
+//     dynamic-Huffman block header that zlib would
+//     accept (zs_split_header_rest: a complete code-length code, code lengths
 //     that decode without overrunning, an end-of-block code, complete lit/len
 //     and distance codes -- stricter than inflate_table, which only costs a
 //     missed boundary), and keeps the first.
@@ -39,9 +40,6 @@
 #include "zs_inftab.h"
 #include "zs_wave.h"
 #include "zs_split.h"
-#ifndef ZS_SPLIT_EXP
-#define ZS_SPLIT_EXP 0  // timing experiments (0 in the product)
-#endif
 
 // ------------------------------------------------------------ header check
 // The candidate's bits: words of the member read aligned (w4: the aligned
@@ -59,37 +57,8 @@ struct zs_hdr_src {
   }
 };
 
-// Cheap first test of a candidate: BTYPE = 2, HLIT / HDIST in range and a
-// complete code-length code (Kraft sum of the 3-bit lengths), from four aligned
-// words -- almost every bit offset fails here.  a, b: stream bits 0..63, 64..
-static __device__ __forceinline__ bool zs_split_quick(const zs_hdr_src& S, uint64_t bit, bool d64, uint64_t& a,
-                                                      uint64_t& b) {
-  const uint64_t cb = (bit >> 3) + S.sh;
-  const uint32_t q = (uint32_t)(cb >> 2);
-  const uint32_t off = (uint32_t)((cb & 3u) * 8u + (bit & 7u));
-  const uint32_t w0 = S.word(q), w1 = S.word(q + 1u), w2 = S.word(q + 2u), w3 = S.word(q + 3u);
-  const uint64_t lo = ((uint64_t)w1 << 32) | w0, hi = ((uint64_t)w3 << 32) | w2;
-  a = off ? (lo >> off) | (hi << (64u - off)) : lo;
-  b = hi >> off;
-  if (((a >> 1) & 3u) != 2u) return false;
-  if (((a >> 3) & 31u) > 29u) return false;
-  if (!d64 && ((a >> 8) & 31u) > 29u) return false;
-  const uint32_t ncode = (uint32_t)((a >> 13) & 15u) + 4u;
-  uint32_t kraft = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < 19; i++) {
-    const uint32_t pos = 17u + 3u * i;
-    uint32_t v;
-    if (pos + 3u <= 64u) v = (uint32_t)(a >> pos) & 7u;
-    else if (pos >= 64u) v = (uint32_t)(b >> (pos - 64u)) & 7u;
-    else v = (uint32_t)((a >> pos) | (b << (64u - pos))) & 7u;
-    kraft += (i < ncode && v) ? (128u >> v) : 0u;
-  }
-  return kraft == 128u;  // CODES must be complete (inftrees.ts:128-139)
-}
-
 // The rest of a dynamic header that inflate (inflate.ts:662-836) accepts, for
-// a candidate that passed zs_split_quick: the code lengths decode (repeat 16
+// a candidate that passed the finder's quick tests: the code lengths decode (repeat 16
 // never first, no run past HLIT + HDIST), the end-of-block code has a length,
 // and -- stricter than inflate_table, which only costs a missed boundary --
 // the lit/len code is complete and the distance code complete or one 1-bit
@@ -207,32 +176,57 @@ static __device__ bool zs_split_header_rest(const zs_hdr_src& S, uint64_t bit, u
 }
 
 // ----------------------------------------------------------------- finder
-#if ZS_SPLIT_EXP & 4
-__device__ unsigned long long zs_split_stat[4];
-extern "C" int zs_split_stats(unsigned long long* out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_split_stat), sizeof(zs_split_stat));
+// The code-length code's Kraft sum from a candidate's bits (a: 0..63, b:
+// 64..127): CODES must be complete (inftrees.ts:128-139).
+static __device__ __forceinline__ bool zs_split_kraft(uint64_t a, uint64_t b) {
+  const uint32_t ncode = (uint32_t)((a >> 13) & 15u) + 4u;
+  uint32_t kraft = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 19; i++) {
+    const uint32_t pos = 17u + 3u * i;
+    uint32_t v;
+    if (pos + 3u <= 64u) v = (uint32_t)(a >> pos) & 7u;
+    else if (pos >= 64u) v = (uint32_t)(b >> (pos - 64u)) & 7u;
+    else v = (uint32_t)((a >> pos) | (b << (64u - pos))) & 7u;
+    kraft += (i < ncode && v) ? (128u >> v) : 0u;
+  }
+  return kraft == 128u;
 }
-#endif
+
 // One workgroup per (member, range): ranges r = 1 .. ZS_SPLIT_MAX-1 of
-// span = ceil(nbits / ZS_SPLIT_MAX) bits (range 0 is the member's start);
+// span = max(16384, nbits / ZS_SPLIT_MAX) bits (range 0 is the member's start);
 // found[m * ZS_SPLIT_MAX + r] = the first header start in the range, or ~0.
-__global__ __launch_bounds__(1024) void zs_k_split_find(const uint8_t* __restrict__ in,
-                                                      const uint64_t* __restrict__ in_off,
-                                                      const uint32_t* __restrict__ in_len,
-                                                      const uint32_t* __restrict__ list, int wbits,
-                                                      uint64_t* __restrict__ found) {
+// A thread tests the 32 bit offsets of one member word at a time: BTYPE = 2
+// and HLIT / HDIST in range for all 32 at once on shifted words (about one
+// offset in five passes), the code-length code's Kraft sum for those, and the
+// survivors (~1 %) queue in LDS; the full header check (zs_split_header_rest)
+// then runs one candidate per thread, so a wave's lanes share the long checks
+// instead of waiting on one.  Chunks of 8,192 offsets in order: the first chunk
+// with an accepted candidate holds the range's first.
+#define ZS_FIND_T 256u
+#define ZS_FIND_Q 1024u
+__global__ __launch_bounds__(256) void zs_k_split_find(const uint8_t* __restrict__ in,
+                                                     const uint64_t* __restrict__ in_off,
+                                                     const uint32_t* __restrict__ in_len,
+                                                     const uint32_t* __restrict__ list, int wbits,
+                                                     uint64_t* __restrict__ found) {
   __shared__ unsigned long long best;
-  const uint32_t m = blockIdx.x / ZS_SPLIT_MAX, r = blockIdx.x % ZS_SPLIT_MAX;
+  __shared__ uint32_t nq;
+  __shared__ uint32_t qoff[ZS_FIND_Q];  // queued candidates, bits past the range's start
+  const uint32_t m = blockIdx.x / ZS_SPLIT_MAX, r = blockIdx.x % ZS_SPLIT_MAX, t = threadIdx.x;
   const uint32_t s = list[m];
   const uint32_t n = in_len[s];
   const uint8_t* src = in + in_off[s];
   const uint64_t nbits = 8ull * n;
   const uint64_t span = zs_split_span(n);
   const uint64_t lo = span * r, hi = min(nbits, lo + span);
-  if (threadIdx.x == 0) best = ~0ull;
+  if (t == 0) {
+    best = ~0ull;
+    nq = 0;
+  }
   __syncthreads();
-  if (r == 0) {
-    if (threadIdx.x == 0) found[blockIdx.x] = 0;
+  if (r == 0 || lo >= hi) {
+    if (t == 0) found[blockIdx.x] = r == 0 ? 0ull : ~0ull;
     return;
   }
   const bool d64 = wbits == -16;
@@ -240,32 +234,62 @@ __global__ __launch_bounds__(1024) void zs_k_split_find(const uint8_t* __restric
   S.sh = (uint32_t)((uintptr_t)src & 3u);
   S.w4 = reinterpret_cast<const uint32_t*>(src - S.sh);
   S.last = (S.sh + n - 1u) >> 2;
-  // No barrier per round: a wave whose lane runs the (rare, long) full check
-  // holds up only itself, and a lane stops once past the best start found so
-  // far -- every offset below the final minimum is still tested.
-  volatile unsigned long long* vb = &best;
-  for (uint64_t b = lo + threadIdx.x; b < hi && b < *vb; b += blockDim.x) {
-    uint64_t wa, wb;
-#if ZS_SPLIT_EXP & 1  // timing experiments: the quick test alone (nothing accepted)
-    if (zs_split_quick(S, b, d64, wa, wb) && b == ~0ull)
-#elif ZS_SPLIT_EXP & 2  // the loop alone
-    if (b == ~0ull)
-#elif ZS_SPLIT_EXP & 4  // counters: full checks, their clock cycles
-    bool qk = zs_split_quick(S, b, d64, wa, wb), ok = false;
-    if (qk) {
-      const unsigned long long t0 = clock64();
-      ok = zs_split_header_rest(S, b, nbits, wa, wb);
-      atomicAdd(&zs_split_stat[0], 1ull);
-      atomicAdd(&zs_split_stat[1], clock64() - t0);
+  const uint64_t w_lo = lo >> 5, w_hi = (hi + 31u) >> 5;
+  for (uint64_t wc = w_lo; wc < w_hi; wc += ZS_FIND_T) {
+    const uint64_t w = wc + t;
+    if (w < w_hi) {
+      // member words w .. w+4 (member bit 32 w on), from the aligned words
+      uint32_t mw[5];
+      {
+        uint32_t aw[6];
+#pragma unroll
+        for (uint32_t k = 0; k < 6; k++) aw[k] = S.word((uint32_t)w + k);
+#pragma unroll
+        for (uint32_t k = 0; k < 5; k++) mw[k] = __builtin_amdgcn_alignbyte(aw[k + 1], aw[k], S.sh);
+      }
+      const uint64_t x0 = ((uint64_t)mw[1] << 32) | mw[0], x1 = ((uint64_t)mw[3] << 32) | mw[2], x2 = mw[4];
+#define ZS_SB(k) ((uint32_t)(x0 >> (k)))  // bit o + k of the candidate at offset o, for o = 0..31
+      uint32_t c = ~ZS_SB(1) & ZS_SB(2) & ~(ZS_SB(4) & ZS_SB(5) & ZS_SB(6) & ZS_SB(7));
+      if (!d64) c &= ~(ZS_SB(9) & ZS_SB(10) & ZS_SB(11) & ZS_SB(12));
+#undef ZS_SB
+      const uint64_t b0 = 32ull * w;
+      if (b0 < lo) c &= ~0u << (uint32_t)(lo - b0);
+      if (b0 + 32u > hi) c &= (1u << (uint32_t)(hi - b0)) - 1u;
+      while (c) {
+        const uint32_t o = (uint32_t)__builtin_ctz(c);
+        c &= c - 1u;
+        const uint64_t a = o ? (x0 >> o) | (x1 << (64u - o)) : x0;
+        const uint64_t bb = o ? (x1 >> o) | (x2 << (64u - o)) : x1;
+        if (zs_split_kraft(a, bb)) {
+          const uint32_t qi = atomicAdd(&nq, 1u);
+          if (qi < ZS_FIND_Q) qoff[qi] = (uint32_t)(b0 + o - lo);
+          else if (zs_split_header_rest(S, b0 + o, nbits, a, bb)) atomicMin(&best, (unsigned long long)(b0 + o));
+        }
+      }
     }
-    if (ok)
-#else
-    if (zs_split_quick(S, b, d64, wa, wb) && zs_split_header_rest(S, b, nbits, wa, wb))
-#endif
-      atomicMin(&best, (unsigned long long)b);
+    __syncthreads();
+    const uint32_t cnt = min(nq, ZS_FIND_Q);
+    for (uint32_t i = t; i < cnt; i += ZS_FIND_T) {
+      const uint64_t bit = lo + qoff[i];
+      if (bit >= best) continue;
+      uint64_t a, bb;
+      {
+        const uint64_t cb = (bit >> 3) + S.sh;
+        const uint32_t q = (uint32_t)(cb >> 2);
+        const uint32_t off = (uint32_t)((cb & 3u) * 8u + (bit & 7u));
+        const uint64_t l0 = ((uint64_t)S.word(q + 1u) << 32) | S.word(q),
+                       h0 = ((uint64_t)S.word(q + 3u) << 32) | S.word(q + 2u);
+        a = off ? (l0 >> off) | (h0 << (64u - off)) : l0;
+        bb = h0 >> off;
+      }
+      if (zs_split_header_rest(S, bit, nbits, a, bb)) atomicMin(&best, (unsigned long long)bit);
+    }
+    __syncthreads();
+    if (best != ~0ull) break;
+    if (t == 0) nq = 0;
+    __syncthreads();
   }
-  __syncthreads();
-  if (threadIdx.x == 0) found[blockIdx.x] = best;
+  if (t == 0) found[blockIdx.x] = best;
 }
 
 // the member's found starts in order (piece order; piece 0 starts at bit 0)

@@ -64,12 +64,11 @@ __global__ void zs_k_seg_sync(const uint8_t* in, const uint64_t* in_off, const u
 __global__ void zs_k_seg_plan(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                               const uint32_t* out_cap, const uint32_t* list, uint32_t n_list, int wbits, int refw,
                               const uint32_t* cidx, zs_seg_blk* blk, zs_seg_lane* lanes, zs_seg_mem* mem,
-                              const uint32_t* pbase, uint32_t* plist);
+                              const uint32_t* pbase, uint4* ptab);
 template <bool D64, bool REFW>
 __global__ void zs_k_seg_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* list,
                                 const uint32_t* counter, const zs_seg_blk* blk, const zs_seg_lane* lanes,
                                 const zcode* tcache, zs_seg_mem* mem, const uint64_t* sbase, uint16_t* scratch);
-__global__ void zs_k_seg_resolve(const uint32_t* list, const zs_seg_mem* mem, const zs_seg_lane* lanes,
-                                 const uint32_t* pbase, const uint32_t* plist, const uint64_t* sbase,
-                                 const uint16_t* scratch, uint8_t* out, const uint64_t* out_off, zs_lane_res* res,
-                                 uint32_t* lens_out, uint32_t* n_ok);
+__global__ void zs_k_seg_resolve(const uint32_t* list, const zs_seg_mem* mem, const uint32_t* pbase,
+                                 const uint4* ptab, const uint64_t* sbase, const uint16_t* scratch, uint8_t* out,
+                                 const uint64_t* out_off, zs_lane_res* res, uint32_t* lens_out, uint32_t* n_ok);
