@@ -155,6 +155,10 @@ void zs_free(void *p);
  * One batch at a time per pool. */
 typedef struct zs_pool zs_pool;
 int zs_pool_create(uint64_t device_mask, zs_pool **out);
+/* The same from a list of devices, in shard order; a device may appear more
+ * than once (each entry gets its own context: the pool's sharding rehearsed on
+ * one GPU).  ZS_STREAM_ERROR for a device that does not exist. */
+int zs_pool_create_list(const int *devices, int n_devices, zs_pool **out);
 void zs_pool_destroy(zs_pool *pool);
 int zs_pool_size(const zs_pool *pool);
 int zs_pool_device(const zs_pool *pool, int k);

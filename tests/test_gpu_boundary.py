@@ -128,6 +128,42 @@ def test_pool_on_one_device_equals_engine(engine):
     pool.close()
 
 
+def test_pool_on_every_visible_device_equals_engine(engine):
+    """zs_pool over every visible device (mask 0): the batch is sharded across
+    them (8 on the driver's node, 1 here) and must return what one engine does."""
+    import torch
+    import zsamd
+
+    pool = zsamd.Pool()
+    assert pool.devices == list(range(torch.cuda.device_count()))
+    xs = [corpus.text(corpus.stream_seed(i), 65536) for i in range(48)] + [corpus.mixed(5, 200000)]
+    a = pool.compress_batch_detailed(xs, "gzip", 6)
+    assert a == engine.compress_batch_detailed(xs, "gzip", 6)
+    assert pool.decompress_batch([o for _, o, _ in a], "gzip") == xs
+    pool.close()
+
+
+def test_pool_sharding_rehearsed_with_two_contexts_on_one_device(engine):
+    """The pool's sharding (contiguous shard_range ranges, one host thread per
+    context, each writing its shard straight into the caller's arrays) with two
+    contexts on device 0 -- the multi-device code path without a second GPU."""
+    import zsamd
+
+    pool = zsamd.Pool([0, 0], repeat=True)
+    assert pool.devices == [0, 0]
+    xs = [corpus.text(corpus.stream_seed(i), 65536) for i in range(37)] + [b"", corpus.mixed(9, 262144)]
+    for fmt in ("deflate-raw", "deflate"):
+        a = pool.compress_batch_detailed(xs, fmt, 6)
+        assert a == engine.compress_batch_detailed(xs, fmt, 6)
+        comps = [o for _, o, _ in a]
+        assert pool.decompress_batch(comps, fmt) == engine.decompress_batch(comps, fmt) == xs
+        caps = [len(x) + 8 for x in xs]
+        assert pool.decompress_batch_detailed(comps, fmt, caps) == engine.decompress_batch_detailed(comps, fmt, caps)
+    pool.close()
+    with pytest.raises(ValueError):
+        zsamd.Pool([0, 999], repeat=True)
+
+
 @pytest.mark.slow
 def test_c3_all_65536_members_decode(engine):
     """BASELINE.json configs[2] at its full size: the 4,096 unique M-corpus

@@ -1,0 +1,141 @@
+"""GPU parity of the segmented decode (inflate_seg.hip): a member's blocks cut
+into lane-sized pieces that synchronise, markers for the history before a
+piece, the reference's inflate() call state per piece (window-wrap copy of
+inffast.ts:127-147).  Every member it finishes must equal the oracle with the
+reference's defect (reference_bugs, oracle/inflate.c) -- i.e. what
+DecompressionStream (streams.ts:253-262) returns for one write() -- and every
+member it does not finish must take the other paths to the same outcome."""
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+import corpus
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class _opts:
+    DEFAULTS = {"inflate_seg": 1, "seg_bits": 4096, "seg_small_batch": 16384, "seg_small_min": 4096,
+                "inflate_fast": 1, "inflate_ref_wrap": 1, "inflate_wave_min": 32768}
+
+    def __init__(self, engine, **kw):
+        self.e, self.kw = engine, kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.e.set_option(k, v)
+
+    def __exit__(self, *a):
+        for k in self.kw:
+            self.e.set_option(k, self.DEFAULTS[k])
+
+
+def _members(rng, fmt, kinds, levels, sizes, count):
+    out = []
+    for _ in range(count):
+        n = rng.choice(sizes)
+        s = corpus.make({"kind": rng.choice(kinds), "n": n, "seed": corpus.stream_seed(rng.randrange(4096))})
+        out.append((s, oracle.compress(s, rng.choice(levels), fmt)[1]))
+    return out
+
+
+@pytest.mark.parametrize("fmt", ["deflate-raw", "deflate", "gzip"])
+def test_segmented_decode_equals_the_reference(engine, fmt):
+    """T- and M-corpus members of 20 KB .. 500 KB at levels 1 / 6 / 9: every one
+    finished by the segmented decode, bytes / consumed / check value equal to the
+    oracle's decode with the reference's window-wrap copy."""
+    rng = random.Random({"deflate-raw": 1, "deflate": 2, "gzip": 3}[fmt])
+    ms = _members(rng, fmt, ["text", "mixed"], [1, 6, 9], [20000, 65536, 150000, 262144, 500000], 24)
+    comps = [c for _, c in ms]
+    caps = [len(s) + 16 for s, _ in ms]
+    got = engine.decompress_batch_detailed(comps, fmt, caps)
+    assert engine.last_seg_count() == len(ms)
+    for i, ((s, c), g) in enumerate(zip(ms, got)):
+        st, out, cons, ph, msg = oracle.decompress(c, fmt, cap=len(s) + 16, reference_bugs=True)
+        assert g[0] == st == 1 and g[3] == out and g[4] == cons == len(c), i
+        if fmt != "deflate-raw":
+            assert (g[5] & 0xffffffff) == (oracle.crc32(out) if fmt == "gzip" else oracle.adler32(out)), i
+
+
+@pytest.mark.parametrize("bits", [8192, 65536])
+def test_piece_size_does_not_change_bytes(engine, bits):
+    """seg_bits (input bits per piece) only changes how a member is cut: the
+    bytes of M-corpus members at L6 (window-wrap copies in most) are the same."""
+    rng = random.Random(bits)
+    ms = _members(rng, "deflate-raw", ["mixed"], [6, 9], [262144, 500000], 8)
+    comps = [c for _, c in ms]
+    caps = [len(s) for s, _ in ms]
+    with _opts(engine, seg_bits=bits):
+        got = engine.decompress_batch_raw(comps, "deflate-raw", caps)
+        nseg = engine.last_seg_count()
+    want = [oracle.decompress(c, "deflate-raw", cap=len(s), reference_bugs=True) for s, c in ms]
+    assert nseg == len(ms)
+    assert [g[3] for g in got] == [w[1] for w in want]
+
+
+def test_segmented_decode_without_the_window_wrap_copy(engine):
+    """inflate_ref_wrap = 0: zlib semantics (no call bookkeeping); the members
+    decode to their sources."""
+    rng = random.Random(77)
+    ms = _members(rng, "deflate-raw", ["mixed", "text"], [6, 9], [200000, 500000], 8)
+    with _opts(engine, inflate_ref_wrap=0):
+        got = engine.decompress_batch_raw([c for _, c in ms], "deflate-raw", [len(s) for s, _ in ms])
+        nseg = engine.last_seg_count()
+    assert nseg == len(ms)
+    assert [g[3] for g in got] == [s for s, _ in ms]
+
+
+def test_deflate64_fixtures_through_the_segmented_decode(engine):
+    """The reference's test/data deflate64 fixtures (decoded sizes / digests
+    pinned by inflate_small.json), each as a "large" member of a small batch."""
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "inflate_small.json")))
+    fx = [(open(os.path.join(ROOT, "tests", "golden", "d64", c["name"][4:]), "rb").read(), c["out_len"],
+           c["out_sha256"]) for c in g["cases"] if c["name"].startswith("d64_") and c.get("ok")]
+    with _opts(engine, seg_small_min=256):
+        got = engine.decompress_batch_raw([d for d, _, _ in fx], "deflate64-raw", [n for _, n, _ in fx])
+        nseg = engine.last_seg_count()
+    for (d, n, h), r in zip(fx, got):
+        assert r[0] == 1 and len(r[3]) == n and hashlib.sha256(r[3]).hexdigest() == h and r[4] == len(d)
+    assert nseg >= len(fx) // 2
+
+
+def test_damaged_members_take_the_other_paths(engine):
+    """Bit flips and truncations: whatever the pieces see, each member's outcome
+    (status, phase, message, bytes, consumed) equals the exact kernel's."""
+    rng = random.Random(31)
+    members = []
+    for k, (s, c) in enumerate(_members(rng, "deflate-raw", ["text", "mixed"], [1, 6], [70000, 262144], 16)):
+        b = bytearray(c)
+        if k % 3 == 0:
+            for _ in range(rng.choice([1, 4])):
+                b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+        elif k % 3 == 1:
+            b = b[:rng.randrange(len(b) // 3, len(b))]
+        members.append(bytes(b))
+    caps = [300000] * len(members)
+    got = engine.decompress_batch_raw(members, "deflate-raw", caps)
+    with _opts(engine, inflate_fast=0):
+        want = engine.decompress_batch_raw(members, "deflate-raw", caps)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, i
+
+
+def test_segmented_and_lane_paths_agree_on_a_mixed_batch(engine):
+    """One batch with tiny members (lanes) and large ones (segmented), in gzip:
+    the same outcome as with the segmented decode off."""
+    rng = random.Random(5)
+    ms = _members(rng, "gzip", ["text", "mixed"], [6], [300, 3000, 9000, 65536, 262144], 40)
+    comps = [c for _, c in ms]
+    caps = [len(s) + 8 for s, _ in ms]
+    got = engine.decompress_batch_detailed(comps, "gzip", caps)
+    assert engine.last_seg_count() == sum(1 for c in comps if len(c) > 4096)
+    with _opts(engine, inflate_seg=0):
+        want = engine.decompress_batch_detailed(comps, "gzip", caps)
+    assert got == want
+    assert [g[3] for g in got] == [s for s, _ in ms]

@@ -190,6 +190,41 @@ extern "C" int zs_pool_create(uint64_t device_mask, zs_pool** out) {
   return ZS_OK;
 }
 
+extern "C" int zs_pool_create_list(const int* devices, int n, zs_pool** out) {
+  if (!out || !devices || n <= 0) {
+    zs_set_last_error("invalid arguments");
+    return ZS_STREAM_ERROR;
+  }
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    zs_set_last_error("no HIP device");
+    return ZS_STREAM_ERROR;
+  }
+  zs_pool* p = new zs_pool();
+  for (int k = 0; k < n; k++) {
+    if (devices[k] < 0 || devices[k] >= ndev) {
+      delete p;
+      zs_set_last_error("device list names a device that does not exist");
+      return ZS_STREAM_ERROR;
+    }
+    p->devices.push_back(devices[k]);
+  }
+  for (int d : p->devices) {
+    zs_ctx* c = nullptr;
+    const int r = zs_ctx_create(d, &c);
+    if (r != ZS_OK) {
+      const std::string e = zs_last_error();
+      zs_pool_destroy(p);
+      zs_set_last_error(e);
+      return r;
+    }
+    p->ctx.push_back(c);
+  }
+  *out = p;
+  return ZS_OK;
+}
+
 extern "C" void zs_pool_destroy(zs_pool* p) {
   if (!p) return;
   for (zs_ctx* c : p->ctx) zs_ctx_destroy(c);

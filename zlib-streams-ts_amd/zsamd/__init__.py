@@ -104,6 +104,7 @@ def lib():
     L.zs_inflate_batch_auto.argtypes = [_P] + _inf_host + [ctypes.POINTER(_P), _U64P] + _inf_res
     L.zs_free.argtypes = [_P]
     L.zs_pool_create.argtypes = [ctypes.c_uint64, ctypes.POINTER(_P)]
+    L.zs_pool_create_list.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]
     L.zs_pool_destroy.argtypes = [_P]
     L.zs_pool_size.argtypes = [_P]
     L.zs_pool_device.argtypes = [_P, ctypes.c_int]
@@ -426,18 +427,25 @@ class Pool:
     context per device; each batch is split into contiguous stream ranges, one
     per device, run in parallel -- results identical to one device's."""
 
-    def __init__(self, devices: Optional[Sequence[int]] = None):
+    def __init__(self, devices: Optional[Sequence[int]] = None, repeat: bool = False):
+        """devices: device indices (None / empty: every visible device).  repeat=True
+        takes the list as given, in shard order, a device possibly more than once
+        (zs_pool_create_list: the sharding rehearsed on one GPU)."""
         L = lib()
-        mask = 0
-        for d in devices or []:
-            if not 0 <= int(d) < 64:  # the C mask is 64 bits (ctypes would truncate it to "every device")
-                raise ValueError("device index %r outside 0..63" % (d,))
-            mask |= 1 << int(d)
         p = _P()
-        r = L.zs_pool_create(mask, ctypes.byref(p))
+        if repeat:
+            ds = [int(d) for d in devices or []]
+            r = L.zs_pool_create_list((ctypes.c_int * max(1, len(ds)))(*ds), len(ds), ctypes.byref(p))
+        else:
+            mask = 0
+            for d in devices or []:
+                if not 0 <= int(d) < 64:  # the C mask is 64 bits (ctypes would truncate it to "every device")
+                    raise ValueError("device index %r outside 0..63" % (d,))
+                mask |= 1 << int(d)
+            r = L.zs_pool_create(mask, ctypes.byref(p))
         if r != 0:
             err = L.zs_last_error().decode()
-            if r == Z_STREAM_ERROR and "device mask" in err:
+            if r == Z_STREAM_ERROR and ("device mask" in err or "device list" in err or "invalid arg" in err):
                 raise ValueError(err)
             raise ZsUnavailable("zs_pool_create failed: %s" % err)
         self._L, self._pool = L, p
