@@ -117,8 +117,10 @@ struct zs_ctx {
   bool seg_used = false;            // the last inflate batch ran it
   std::vector<uint64_t> hgsbase;
   // host staging for the host-buffer entry points
-  Buf d_in, d_out, d_res, d_pack;
-  HostBuf h_in, h_out;
+  Buf d_in, d_out, d_res, d_pack, d_offs;
+  HostBuf h_in, h_out, h_res, h_offs;
+  hipStream_t h2d = nullptr, d2h = nullptr;  // the host entries' copies, beside the kernels (host_batch)
+  std::vector<hipEvent_t> hev;               // their events, reused
   std::vector<uint8_t> hmeta;
   size_t last_n = 0;
   // timing
@@ -223,6 +225,8 @@ int zs_ctx_create(int device, zs_ctx** out) {
     return fail(ZS_MEM_ERROR, "%s", hipGetErrorString(e));
   }
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) {
     zs_ctx_destroy(c);
@@ -270,8 +274,15 @@ void zs_ctx_destroy(zs_ctx* c) {
                  &c->spres, &c->sscr, &c->smem, &c->sval, &c->glist, &c->gfound, &c->gcidx, &c->gblk,
                  &c->glanes, &c->gtab, &c->gmem, &c->gpbase, &c->gplist, &c->gsbase, &c->gscr, &c->gcnt})
     if (b->p) (void)hipFree(b->p);
-  for (HostBuf* b : {&c->h_in, &c->h_out})
+  for (HostBuf* b : {&c->h_in, &c->h_out, &c->h_res, &c->h_offs})
     if (b->p) (void)hipHostFree(b->p);
+  if (c->d_offs.p) (void)hipFree(c->d_offs.p);
+  for (hipEvent_t e : c->hev) (void)hipEventDestroy(e);
+  for (hipStream_t q : {c->h2d, c->d2h})
+    if (q) {
+      (void)hipStreamSynchronize(q);
+      (void)hipStreamDestroy(q);
+    }
   for (auto& m : c->marks) (void)hipEventDestroy(m.ev);
   if (c->lane_ev) (void)hipEventSynchronize(c->lane_ev);
   if (c->lane_count_host) (void)hipHostFree(c->lane_count_host);
@@ -593,11 +604,11 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
 }
 
 // ---------------------------------------------------------- host buffers
-// The host-buffer entry points move data in ONE DMA each way: the caller's
-// streams are packed (in parallel) into a pinned staging buffer and copied to
-// HBM in one hipMemcpyAsync; after the batch the outputs are compacted on the
-// device (4-aligned, in stream order) and come back in one copy of exactly
-// the produced bytes, which the host then scatters to the caller's offsets.
+// The host-buffer entry points: the caller's streams are packed (in parallel)
+// into a pinned staging buffer and copied to HBM; after the batch the outputs
+// are compacted on the device (4-aligned, in stream order) and come back in one
+// copy of exactly the produced bytes, which the host then scatters to the
+// caller's offsets -- chunk by chunk, overlapped with the kernels (host_batch).
 static void par_copy(uint32_t n, uint8_t* dst, const uint64_t* dst_off, const uint8_t* src, const uint64_t* src_off,
                      const uint32_t* len, uint64_t total) {
   const int T = total >= (32u << 20) ? 8 : (total >= (4u << 20) ? 4 : 1);
@@ -634,29 +645,111 @@ __global__ void zs_k_compact(const uint8_t* __restrict__ src, const uint64_t* __
   for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) b[i] = a[i];
 }
 
-// Compacts the produced outputs (len[] already on the host) and copies them
-// into the caller's buffer at out_off[].
-static int fetch_out(zs_ctx* c, uint32_t n, const uint64_t* soff, const uint32_t* d_len, const uint32_t* len,
-                     const uint32_t* cap, uint8_t* out, const uint64_t* out_off) {
-  std::vector<uint64_t> offs(2ull * n), poff(n);
-  uint64_t P = 0;
+// The host-buffer entries, pipelined: the batch runs as a few chunks of
+// streams ([1/8, 3/8, 3/8, 1/8] of them for batches of 32 MB or more), so that
+// packing chunk k+1 into the pinned staging and its H2D copy (stream h2d) run
+// while chunk k's kernels do (the context's stream), and chunk k-1's output
+// compaction, D2H copy (stream d2h) and scatter into the caller's buffers run
+// while chunk k+1's do.  `launch(a, b, doff, ooff, ocap, d_res)` enqueues the
+// device batch of streams [a, b) on c->stream; d_res holds nres u32 arrays of n
+// entries (array r at d_res + r n), res_host the caller's nres arrays, of which
+// res_host[len_idx] is the output length.  Outputs land at out + out_off[i].
+template <class Launch>
+static int host_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                      const std::vector<uint32_t>& ocap, uint32_t nres, uint32_t* const* res_host, uint32_t len_idx,
+                      uint8_t* out, const uint64_t* out_off, Launch launch) {
+  std::vector<uint64_t> doff(n), ooff(n);
+  uint64_t tin = 0, tout = 0;
   for (uint32_t i = 0; i < n; i++) {
-    if (len[i] > cap[i]) return fail(ZS_MEM_ERROR, "stream %s reported more output than its capacity", std::to_string(i).c_str());
-    offs[i] = soff[i];
-    offs[n + i] = poff[i] = P;
-    P += ((uint64_t)len[i] + 3) & ~3ull;
+    doff[i] = tin;
+    tin += in_len[i];
+    ooff[i] = tout;
+    tout += ocap[i];
   }
-  if (!P) return ZS_OK;
-  HIPCHK(c->d_pack.ensure(P + 16 + 16ull * n));
-  uint64_t* d_offs = (uint64_t*)(c->d_pack.as<uint8_t>() + ((P + 15) & ~15ull));
-  HIPCHK(hipMemcpyAsync(d_offs, offs.data(), 16ull * n, hipMemcpyHostToDevice, c->stream));
-  zs_k_compact<<<n, 256, 0, c->stream>>>(c->d_out.as<uint8_t>(), d_offs, d_len, c->d_pack.as<uint8_t>(), n);
-  HIPCHK(hipGetLastError());
-  HIPCHK(c->h_out.ensure(P + 16));
-  HIPCHK(hipMemcpyAsync(c->h_out.p, c->d_pack.p, P, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  par_copy(n, out, out_off, c->h_out.as<uint8_t>(), poff.data(), len, P);
-  return ZS_OK;
+  HIPCHK(c->d_in.ensure(tin + 16));
+  HIPCHK(c->h_in.ensure(tin + 16));
+  HIPCHK(c->d_out.ensure(tout + 16));
+  HIPCHK(c->d_pack.ensure(tout + 16));
+  HIPCHK(c->h_out.ensure(tout + 16));
+  HIPCHK(c->d_res.ensure(4ull * nres * n + 16));
+  HIPCHK(c->h_res.ensure(4ull * nres * n + 16));
+  HIPCHK(c->d_offs.ensure(16ull * n + 16));
+  HIPCHK(c->h_offs.ensure(16ull * n + 16));
+  std::vector<uint32_t> bnd{0};
+  if (n >= 64 && tin >= (32ull << 20))
+    for (uint32_t f : {1u, 4u, 7u}) bnd.push_back((uint32_t)((uint64_t)n * f / 8));
+  bnd.push_back(n);
+  const uint32_t K = (uint32_t)bnd.size() - 1;
+  while (c->hev.size() < 3 * K) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->hev.push_back(e);
+  }
+  hipEvent_t* ev_in = c->hev.data();
+  hipEvent_t* ev_k = ev_in + K;
+  hipEvent_t* ev_out = ev_k + K;
+  uint8_t* hin = c->h_in.as<uint8_t>();
+  uint32_t* dres = c->d_res.as<uint32_t>();
+  uint32_t* hres = c->h_res.as<uint32_t>();
+  uint64_t* hoffs = c->h_offs.as<uint64_t>();
+  std::vector<uint64_t> poff(n);
+  // chunk k's results are in: the caller's arrays, then its compaction and D2H (stream d2h)
+  auto after_kernels = [&](uint32_t k) -> int {
+    const uint32_t a = bnd[k], b = bnd[k + 1], m = b - a;
+    HIPCHK(hipEventSynchronize(ev_k[k]));
+    for (uint32_t r = 0; r < nres; r++)
+      if (res_host[r]) memcpy(res_host[r] + a, hres + (size_t)r * n + a, 4ull * m);
+    const uint32_t* len = res_host[len_idx];
+    uint64_t P = ooff[a];
+    for (uint32_t i = a; i < b; i++) {
+      if (len[i] > ocap[i])
+        return fail(ZS_MEM_ERROR, "stream %s reported more output than its capacity", std::to_string(i).c_str());
+      hoffs[2 * a + (i - a)] = ooff[i];
+      hoffs[2 * a + m + (i - a)] = poff[i] = P;
+      P += ((uint64_t)len[i] + 3) & ~3ull;
+    }
+    if (P > ooff[a]) {
+      uint64_t* doffs = c->d_offs.as<uint64_t>() + 2 * a;
+      HIPCHK(hipMemcpyAsync(doffs, hoffs + 2 * a, 16ull * m, hipMemcpyHostToDevice, c->d2h));
+      zs_k_compact<<<m, 256, 0, c->d2h>>>(c->d_out.as<uint8_t>(), doffs, dres + (size_t)len_idx * n + a,
+                                          c->d_pack.as<uint8_t>(), m);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(c->h_out.as<uint8_t>() + ooff[a], c->d_pack.as<uint8_t>() + ooff[a], P - ooff[a],
+                            hipMemcpyDeviceToHost, c->d2h));
+    }
+    HIPCHK(hipEventRecord(ev_out[k], c->d2h));
+    return ZS_OK;
+  };
+  // chunk k's bytes are in pinned memory: into the caller's buffers
+  auto after_copy = [&](uint32_t k) -> int {
+    const uint32_t a = bnd[k], b = bnd[k + 1];
+    HIPCHK(hipEventSynchronize(ev_out[k]));
+    uint64_t bytes = 0;
+    for (uint32_t i = a; i < b; i++) bytes += res_host[len_idx][i];
+    par_copy(b - a, out, out_off + a, c->h_out.as<uint8_t>(), poff.data() + a, res_host[len_idx] + a, bytes);
+    return ZS_OK;
+  };
+  for (uint32_t k = 0; k < K; k++) {
+    const uint32_t a = bnd[k], b = bnd[k + 1], m = b - a;
+    const uint64_t bytes = (b < n ? doff[b] : tin) - doff[a];
+    par_copy(m, hin, doff.data() + a, in, in_off + a, in_len + a, bytes);
+    if (bytes) HIPCHK(hipMemcpyAsync(c->d_in.as<uint8_t>() + doff[a], hin + doff[a], bytes, hipMemcpyHostToDevice, c->h2d));
+    HIPCHK(hipEventRecord(ev_in[k], c->h2d));
+    HIPCHK(hipStreamWaitEvent(c->stream, ev_in[k], 0));
+    std::vector<uint32_t*> dr(nres);
+    for (uint32_t r = 0; r < nres; r++) dr[r] = dres + (size_t)r * n + a;
+    int rc = launch(a, b, doff.data() + a, ooff.data() + a, ocap.data() + a, dr.data());
+    if (rc != ZS_OK) return rc;
+    for (uint32_t r = 0; r < nres; r++)
+      HIPCHK(hipMemcpyAsync(hres + (size_t)r * n + a, dr[r], 4ull * m, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipEventRecord(ev_k[k], c->stream));
+    if (k >= 1 && (rc = after_kernels(k - 1)) != ZS_OK) return rc;
+    if (k >= 2 && (rc = after_copy(k - 2)) != ZS_OK) return rc;
+  }
+  int rc = after_kernels(K - 1);
+  if (rc == ZS_OK && K >= 2) rc = after_copy(K - 2);
+  if (rc == ZS_OK) rc = after_copy(K - 1);
+  return rc;
 }
 
 extern "C" int zs_deflate_batch(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* in, const uint64_t* in_off,
@@ -671,30 +764,17 @@ extern "C" int zs_deflate_batch_ex(zs_ctx* c, int level, int wbits, uint32_t n, 
                                    uint32_t* out_len, uint32_t* check) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   HIPCHK(hipSetDevice(c->device));
-  std::vector<uint64_t> doff, ooff(n);
-  uint64_t total = 0, ototal = 0;
-  int r = stage_in(c, n, in, in_off, in_len, doff, total);
-  if (r != ZS_OK) return r;
+  if (n == 0) return ZS_OK;
   std::vector<uint32_t> ocap(n);
-  for (uint32_t i = 0; i < n; i++) {
-    ooff[i] = ototal;
-    ocap[i] = out_cap[i] & ~3u;
-    ototal += ocap[i];
-  }
-  HIPCHK(c->d_out.ensure(ototal + 16));
-  HIPCHK(c->d_res.ensure(12ull * n + 16));
-  int32_t* d_status = c->d_res.as<int32_t>();
-  uint32_t* d_len = (uint32_t*)(d_status + n);
-  uint32_t* d_chk = d_len + n;
-  r = zs_deflate_batch_device_ex(c, level, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len,
-                                 c->d_out.as<uint8_t>(), ooff.data(), ocap.data(), d_status, d_len,
-                                 check ? d_chk : nullptr, c->stream);
-  if (r != ZS_OK) return r;
-  HIPCHK(hipMemcpyAsync(status, d_status, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(out_len, d_len, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  if (check) HIPCHK(hipMemcpyAsync(check, d_chk, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return fetch_out(c, n, ooff.data(), d_len, out_len, ocap.data(), out, out_off);  // out_len is 0 for failed streams
+  for (uint32_t i = 0; i < n; i++) ocap[i] = out_cap[i] & ~3u;
+  uint32_t* res[3] = {(uint32_t*)status, out_len, check};
+  return host_batch(c, n, in, in_off, in_len, ocap, 3, res, 1, out, out_off,
+                    [&](uint32_t a, uint32_t b, const uint64_t* doff, const uint64_t* ooff, const uint32_t* cap,
+                        uint32_t** dr) {
+                      return zs_deflate_batch_device_ex(c, level, wbits, b - a, c->d_in.as<uint8_t>(), doff, in_len + a,
+                                                        c->d_out.as<uint8_t>(), ooff, cap, (int32_t*)dr[0], dr[1],
+                                                        check ? dr[2] : nullptr, c->stream);
+                    });  // out_len is 0 for failed streams
 }
 
 static int checksum_batch(zs_ctx* c, int kind, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
@@ -1308,30 +1388,17 @@ extern "C" int zs_inflate_batch_ex(zs_ctx* c, int wbits, uint32_t n, const uint8
                                    uint32_t* out_len, uint32_t* consumed, uint32_t* check) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   HIPCHK(hipSetDevice(c->device));
-  std::vector<uint64_t> doff, ooff(n);
-  uint64_t total = 0, ototal = 0;
-  int r = stage_in(c, n, in, in_off, in_len, doff, total);
-  if (r != ZS_OK) return r;
-  std::vector<uint32_t> ocap(n);
-  for (uint32_t i = 0; i < n; i++) { ooff[i] = ototal; ocap[i] = out_cap[i]; ototal += ((uint64_t)out_cap[i] + 3) & ~3ull; }
-  HIPCHK(c->d_out.ensure(ototal + 16));
-  HIPCHK(c->d_res.ensure(24ull * n + 16));
-  int32_t* d_status = c->d_res.as<int32_t>();
-  int32_t* d_phase = d_status + n;
-  int32_t* d_msg = d_phase + n;
-  uint32_t* d_len = (uint32_t*)(d_msg + n);
-  uint32_t* d_cons = d_len + n;
-  uint32_t* d_chk = d_cons + n;
-  r = zs_inflate_batch_device_ex(c, wbits, n, c->d_in.as<uint8_t>(), doff.data(), in_len, c->d_out.as<uint8_t>(),
-                                 ooff.data(), ocap.data(), d_status, d_phase, d_msg, d_len, d_cons,
-                                 check ? d_chk : nullptr, c->stream);
-  if (r != ZS_OK) return r;
-  if (check) HIPCHK(hipMemcpyAsync(check, d_chk, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(status, d_status, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(phase, d_phase, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(msg, d_msg, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(out_len, d_len, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(consumed, d_cons, 4ull * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return fetch_out(c, n, ooff.data(), d_len, out_len, ocap.data(), out, out_off);
+  if (n == 0) return ZS_OK;
+  // device regions: the caller's capacity rounded up to whole words (the decoders store dwords)
+  std::vector<uint32_t> ocap(n), creq(out_cap, out_cap + n);
+  for (uint32_t i = 0; i < n; i++) ocap[i] = (uint32_t)std::min<uint64_t>(0xfffffffcull, ((uint64_t)out_cap[i] + 3) & ~3ull);
+  uint32_t* res[6] = {(uint32_t*)status, (uint32_t*)phase, (uint32_t*)msg, out_len, consumed, check};
+  return host_batch(c, n, in, in_off, in_len, ocap, 6, res, 3, out, out_off,
+                    [&](uint32_t a, uint32_t b, const uint64_t* doff, const uint64_t* ooff, const uint32_t*,
+                        uint32_t** dr) {
+                      return zs_inflate_batch_device_ex(c, wbits, b - a, c->d_in.as<uint8_t>(), doff, in_len + a,
+                                                        c->d_out.as<uint8_t>(), ooff, creq.data() + a,
+                                                        (int32_t*)dr[0], (int32_t*)dr[1], (int32_t*)dr[2], dr[3], dr[4],
+                                                        check ? dr[5] : nullptr, c->stream);
+                    });
 }

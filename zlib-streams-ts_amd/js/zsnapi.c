@@ -2,10 +2,13 @@
  * zsnapi.c -- the thin N-API addon between the JavaScript host side
  * (streams-api.mjs) and libzsgpu.so (include/zs_gpu.h).  Plain C against
  * node_api.h (N-API v8): it borrows the callers' Uint8Array backing stores for
- * the duration of one call (napi_get_typedarray_info), packs them into one
- * host batch, runs zs_deflate_batch / zs_inflate_batch on the GPU and returns
- * fresh Uint8Arrays -- nothing is retained after the call (SURVEY.md 8(b)
- * "Ownership").  The batch calls return Promises: the GPU work runs on a libuv
+ * the duration of one call (napi_get_typedarray_info; the arrays are held by a
+ * reference until the batch settles, SURVEY.md 8(b) "Ownership"), hands their
+ * addresses straight to zs_deflate_batch / zs_inflate_batch (the library packs
+ * them into its pinned staging on the worker thread: no copy on the JS thread),
+ * and returns the outputs as views of ONE external ArrayBuffer that the batch's
+ * output buffer becomes (freed when the views are collected: no copy back
+ * either).  The batch calls return Promises: the GPU work runs on a libuv
  * worker thread (napi_async_work), so the event loop keeps running.  A batch
  * runs on a device set (SURVEY.md 8(b) "device mask"): a zs_pool per distinct
  * set, created lazily on the JS thread, splits it into contiguous stream
@@ -185,9 +188,10 @@ static int32_t arg_i32(napi_env env, napi_value v, int32_t dflt) {
   return x;
 }
 
-/* One batch in flight: inputs packed on the JS thread (the borrowed
- * Uint8Arrays are not touched after the call returns), the GPU work on a libuv
- * worker thread (napi_async_work), results built back on the JS thread. */
+/* One batch in flight: the borrowed inputs (kept alive by `keep` until the
+ * batch settles; the caller must not modify them meanwhile, as with the
+ * reference's write()), the GPU work on a libuv worker thread (napi_async_work),
+ * results built back on the JS thread. */
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
@@ -199,7 +203,10 @@ typedef struct {
   uint64_t *in_off, *out_off;
   uint32_t *in_len, *cap, *olen, *cons, *check;
   int32_t *status, *phase, *msg;
-  uint8_t *blob, *out;
+  const uint8_t *base; /* inputs: base + in_off[i] (the callers' own buffers) */
+  uint8_t *out;
+  int out_given;       /* out now belongs to the results' external ArrayBuffer */
+  napi_ref keep;       /* a JS array holding the input Uint8Arrays */
   int rc;
   char err[512];
 } job;
@@ -207,9 +214,11 @@ typedef struct {
 static void job_free(job *j) {
   if (!j) return;
   free(j->in_off); free(j->out_off); free(j->in_len); free(j->cap); free(j->olen); free(j->cons); free(j->check);
-  free(j->status); free(j->phase); free(j->msg); free(j->blob);
-  if (j->unbounded) zs_free(j->out);
-  else free(j->out);
+  free(j->status); free(j->phase); free(j->msg);
+  if (!j->out_given) {
+    if (j->unbounded) zs_free(j->out);
+    else free(j->out);
+  }
   free(j);
 }
 
@@ -241,15 +250,21 @@ static void job_execute(napi_env env, void *data) {
   (void)env;
   if (j->n == 0) j->rc = ZS_OK;
   else if (j->inflate && j->unbounded)
-    j->rc = zs_pool_inflate_batch_auto(j->pool, j->wbits, j->n, j->blob, j->in_off, j->in_len, &j->out, j->out_off,
+    j->rc = zs_pool_inflate_batch_auto(j->pool, j->wbits, j->n, j->base, j->in_off, j->in_len, &j->out, j->out_off,
                                        j->status, j->phase, j->msg, j->olen, j->cons, j->check);
   else if (j->inflate)
-    j->rc = zs_pool_inflate_batch(j->pool, j->wbits, j->n, j->blob, j->in_off, j->in_len, j->out, j->out_off, j->cap,
+    j->rc = zs_pool_inflate_batch(j->pool, j->wbits, j->n, j->base, j->in_off, j->in_len, j->out, j->out_off, j->cap,
                                   j->status, j->phase, j->msg, j->olen, j->cons, j->check);
   else
-    j->rc = zs_pool_deflate_batch(j->pool, j->level, j->wbits, j->n, j->blob, j->in_off, j->in_len, j->out,
+    j->rc = zs_pool_deflate_batch(j->pool, j->level, j->wbits, j->n, j->base, j->in_off, j->in_len, j->out,
                                   j->out_off, j->cap, j->status, j->olen, j->check);
   if (j->rc != ZS_OK) snprintf(j->err, sizeof j->err, "%s", zs_last_error());  /* the error is per thread */
+}
+
+static void free_out(napi_env env, void *data, void *hint) {
+  (void)env;
+  if (hint) zs_free(data);
+  else free(data);
 }
 
 static napi_value build_result(napi_env env, job *j) {
@@ -257,8 +272,24 @@ static napi_value build_result(napi_env env, job *j) {
   if (napi_create_array_with_length(env, j->n, &outs) != napi_ok || napi_create_object(env, &obj) != napi_ok) return NULL;
   napi_value msgs = NULL;
   if (j->inflate && napi_create_array_with_length(env, j->n, &msgs) != napi_ok) return NULL;
+  /* the outputs: views of the batch's output buffer, which becomes an external
+   * ArrayBuffer (copies only where the runtime refuses external buffers) */
+  napi_value ab = NULL;
+  uint64_t span = 0;
+  for (uint32_t i = 0; i < j->n; i++)
+    if (j->status[i] == ZS_STREAM_END && j->out_off[i] + j->olen[i] > span) span = j->out_off[i] + j->olen[i];
+  if (j->out && span &&
+      napi_create_external_arraybuffer(env, j->out, (size_t)span, free_out, j->unbounded ? (void *)1 : NULL, &ab) ==
+          napi_ok)
+    j->out_given = 1;
   for (uint32_t i = 0; i < j->n; i++) {
-    napi_value u = make_u8(env, j->out ? j->out + j->out_off[i] : NULL, j->status[i] == ZS_STREAM_END ? j->olen[i] : 0);
+    const size_t len = j->status[i] == ZS_STREAM_END ? j->olen[i] : 0;
+    napi_value u = NULL;
+    if (ab && len) {
+      if (napi_create_typedarray(env, napi_uint8_array, len, ab, (size_t)j->out_off[i], &u) != napi_ok) u = NULL;
+    } else {
+      u = make_u8(env, j->out ? j->out + j->out_off[i] : NULL, len);
+    }
     if (!u || napi_set_element(env, outs, i, u) != napi_ok) return NULL;
     if (j->inflate) {
       napi_value s;
@@ -297,7 +328,28 @@ static void job_complete(napi_env env, napi_status st, void *data) {
     napi_reject_deferred(env, j->deferred, e);
   }
   napi_delete_async_work(env, j->work);
+  if (j->keep) napi_delete_reference(env, j->keep);
   job_free(j);
+}
+
+/* the inputs by address (base = the lowest), the Uint8Arrays kept alive in a
+ * fresh array until the batch settles */
+static int borrow_inputs(napi_env env, job *j, napi_value arr, const view *v) {
+  uintptr_t lo = 0;
+  for (uint32_t i = 0; i < j->n; i++)
+    if (v[i].n && (!lo || (uintptr_t)v[i].p < lo)) lo = (uintptr_t)v[i].p;
+  j->base = (const uint8_t *)lo;
+  for (uint32_t i = 0; i < j->n; i++) {
+    j->in_off[i] = v[i].n ? (uint64_t)((uintptr_t)v[i].p - lo) : 0;
+    j->in_len[i] = (uint32_t)v[i].n;
+  }
+  napi_value hold;
+  if (napi_create_array_with_length(env, j->n, &hold) != napi_ok) return -1;
+  for (uint32_t i = 0; i < j->n; i++) {
+    napi_value e;
+    if (napi_get_element(env, arr, i, &e) != napi_ok || napi_set_element(env, hold, i, e) != napi_ok) return -1;
+  }
+  return napi_create_reference(env, hold, 1, &j->keep) == napi_ok ? 0 : -1;
 }
 
 static napi_value queue_job(napi_env env, job *j, const char *name) {
@@ -306,6 +358,7 @@ static napi_value queue_job(napi_env env, job *j, const char *name) {
       napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name) != napi_ok ||
       napi_create_async_work(env, NULL, res_name, job_execute, job_complete, j, &j->work) != napi_ok ||
       napi_queue_async_work(env, j->work) != napi_ok) {
+    if (j->keep) napi_delete_reference(env, j->keep);
     job_free(j);
     return throw_code(env, ZS_MEM_ERROR, "could not queue the batch");
   }
@@ -334,24 +387,19 @@ static napi_value CompressBatch(napi_env env, napi_callback_info info) {
   j->pool = pool;
   j->wbits = arg_i32(env, argv[1], -15);
   j->level = arg_i32(env, argv[2], -1);
-  uint64_t tin = 0, tout = 0;
+  uint64_t tout = 0;
   for (uint32_t i = 0; i < n; i++) {
-    j->in_off[i] = tin;
-    j->in_len[i] = (uint32_t)v[i].n;
-    tin += v[i].n;
     j->out_off[i] = tout;
     j->cap[i] = (uint32_t)((zs_deflate_bound(v[i].n, j->wbits) + 3) & ~3ull);
     tout += j->cap[i];
   }
-  j->blob = (uint8_t *)malloc(tin ? tin : 1);
-  j->out = (uint8_t *)malloc(tout ? tout : 1);
-  if (!j->blob || !j->out) {
+  j->out = (uint8_t *)malloc(tout ? tout : 1);  /* (uninitialised: only the outputs are written) */
+  if (!j->out || borrow_inputs(env, j, argv[0], v) != 0) {
     free(v);
+    if (j->keep) napi_delete_reference(env, j->keep);
     job_free(j);
     return throw_code(env, ZS_MEM_ERROR, "out of host memory");
   }
-  for (uint32_t i = 0; i < n; i++)
-    if (v[i].n) memcpy(j->blob + j->in_off[i], v[i].p, v[i].n);
   free(v);
   return queue_job(env, j, "zs.compressBatch");
 }
@@ -386,7 +434,7 @@ static napi_value DecompressBatch(napi_env env, napi_callback_info info) {
   bool caps_arr = false;
   if (!j->unbounded) napi_is_array(env, argv[2], &caps_arr);
   const uint32_t cap_all = caps_arr || j->unbounded ? 0 : arg_cap(env, argv[2], 1 << 16);
-  uint64_t tin = 0, tout = 0;
+  uint64_t tout = 0;
   for (uint32_t i = 0; i < n; i++) {
     uint32_t c = cap_all;
     if (caps_arr) {
@@ -394,22 +442,17 @@ static napi_value DecompressBatch(napi_env env, napi_callback_info info) {
       napi_get_element(env, argv[2], i, &e);
       c = arg_cap(env, e, 1 << 16);
     }
-    j->in_off[i] = tin;
-    j->in_len[i] = (uint32_t)v[i].n;
-    tin += v[i].n;
     j->out_off[i] = tout;
     j->cap[i] = (uint32_t)(((uint64_t)c + 3u) & 0xfffffffcull);
     tout += j->cap[i];
   }
-  j->blob = (uint8_t *)malloc(tin ? tin : 1);
   j->out = j->unbounded ? NULL : (uint8_t *)malloc(tout ? tout : 1);  /* unbounded: the library allocates it */
-  if (!j->blob || (!j->unbounded && !j->out)) {
+  if ((!j->unbounded && !j->out) || borrow_inputs(env, j, argv[0], v) != 0) {
     free(v);
+    if (j->keep) napi_delete_reference(env, j->keep);
     job_free(j);
     return throw_code(env, ZS_MEM_ERROR, "out of host memory");
   }
-  for (uint32_t i = 0; i < n; i++)
-    if (v[i].n) memcpy(j->blob + j->in_off[i], v[i].p, v[i].n);
   free(v);
   return queue_job(env, j, "zs.decompressBatch");
 }

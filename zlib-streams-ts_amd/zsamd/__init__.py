@@ -300,6 +300,14 @@ class Engine:
                                      in_off, in_len, _P(h_out), out_off, out_cap, status, out_len)
         self._check(r, "zs_deflate_batch")
 
+    def decompress_host(self, fmt: str, n: int, h_in: int, in_off, in_len, h_out: int, out_off, out_cap, status,
+                        phase, msg, out_len, consumed):
+        """zs_inflate_batch on caller-owned host memory (pointers as ints, layout /
+        result arrays as ctypes arrays): the end-to-end host->host decode."""
+        r = self._L.zs_inflate_batch(self._ctx, decompress_wbits(fmt), n, ctypes.cast(h_in, ctypes.c_char_p), in_off,
+                                     in_len, _P(h_out), out_off, out_cap, status, phase, msg, out_len, consumed)
+        self._check(r, "zs_inflate_batch")
+
     def checksum_device(self, kind: str, n: int, d_in: int, in_off, in_len, d_check: int, hip_stream: int = 0,
                         seeds=None):
         """crc32 / adler32 of n device-resident streams (seeds: ctypes u32 array or None)"""
