@@ -48,19 +48,26 @@ def _members(rng, fmt, kinds, levels, sizes, count):
 @pytest.mark.parametrize("fmt", ["deflate-raw", "deflate", "gzip"])
 def test_segmented_decode_equals_the_reference(engine, fmt):
     """T- and M-corpus members of 20 KB .. 500 KB at levels 1 / 6 / 9: every one
-    finished by the segmented decode, bytes / consumed / check value equal to the
-    oracle's decode with the reference's window-wrap copy."""
+    finished by the segmented decode, and the outcome equal to the oracle's decode
+    with the reference's window-wrap copy -- for zlib / gzip that includes the
+    reference's own "incorrect data check" when the copy changes bytes that the
+    trailer's checksum covers (the reference reports its defect that way)."""
     rng = random.Random({"deflate-raw": 1, "deflate": 2, "gzip": 3}[fmt])
     ms = _members(rng, fmt, ["text", "mixed"], [1, 6, 9], [20000, 65536, 150000, 262144, 500000], 24)
     comps = [c for _, c in ms]
     caps = [len(s) + 16 for s, _ in ms]
     got = engine.decompress_batch_detailed(comps, fmt, caps)
     assert engine.last_seg_count() == len(ms)
+    ok = 0
     for i, ((s, c), g) in enumerate(zip(ms, got)):
         st, out, cons, ph, msg = oracle.decompress(c, fmt, cap=len(s) + 16, reference_bugs=True)
-        assert g[0] == st == 1 and g[3] == out and g[4] == cons == len(c), i
-        if fmt != "deflate-raw":
-            assert (g[5] & 0xffffffff) == (oracle.crc32(out) if fmt == "gzip" else oracle.adler32(out)), i
+        assert (g[0], g[1]) == (st, ph), i
+        if st == 1:
+            ok += 1
+            assert g[3] == out and g[4] == cons == len(c), i
+            if fmt != "deflate-raw":
+                assert (g[5] & 0xffffffff) == (oracle.crc32(out) if fmt == "gzip" else oracle.adler32(out)), i
+    assert ok >= len(ms) // 2
 
 
 @pytest.mark.parametrize("bits", [8192, 65536])
@@ -138,4 +145,6 @@ def test_segmented_and_lane_paths_agree_on_a_mixed_batch(engine):
     with _opts(engine, inflate_seg=0):
         want = engine.decompress_batch_detailed(comps, "gzip", caps)
     assert got == want
-    assert [g[3] for g in got] == [s for s, _ in ms]
+    for (s, c), g in zip(ms, got):  # (the window-wrap copy can fail a gzip member's CRC, as in the reference)
+        st, out, cons, ph, msg = oracle.decompress(c, "gzip", cap=len(s) + 8, reference_bugs=True)
+        assert (g[0], g[1]) == (st, ph) and (st != 1 or g[3] == out)

@@ -32,7 +32,7 @@ class _opts:
     """Engine options for the duration of a block (restored to the defaults after)."""
 
     DEFAULTS = {"inflate_split": 1, "inflate_wave_min": 32768, "inflate_ref_wrap": 1, "inflate_fast": 1,
-                "lane_large_min": 2304}
+                "lane_large_min": 2304, "inflate_seg": 1}
 
     def __init__(self, engine, **kw):
         self.e, self.kw = engine, kw
@@ -47,6 +47,7 @@ class _opts:
 
 
 def _decode(engine, members, fmt, caps, **kw):
+    kw.setdefault("inflate_seg", 0)  # (the segmented decode has its own tests: test_gpu_seg.py)
     with _opts(engine, **kw):
         res = engine.decompress_batch_raw(members, fmt, out_caps=caps)
         return res, engine.last_lane_count()

@@ -121,6 +121,7 @@ struct zs_ctx {
   HostBuf h_in, h_out, h_res, h_offs;
   hipStream_t h2d = nullptr, d2h = nullptr;  // the host entries' copies, beside the kernels (host_batch)
   std::vector<hipEvent_t> hev;               // their events, reused
+  bool keep_counts = false;                  // a later chunk of one host batch: the lane / seg counts go on
   std::vector<uint8_t> hmeta;
   size_t last_n = 0;
   // timing
@@ -738,7 +739,9 @@ static int host_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* 
     HIPCHK(hipStreamWaitEvent(c->stream, ev_in[k], 0));
     std::vector<uint32_t*> dr(nres);
     for (uint32_t r = 0; r < nres; r++) dr[r] = dres + (size_t)r * n + a;
+    c->keep_counts = k > 0;
     int rc = launch(a, b, doff.data() + a, ooff.data() + a, ocap.data() + a, dr.data());
+    c->keep_counts = false;
     if (rc != ZS_OK) return rc;
     for (uint32_t r = 0; r < nres; r++)
       HIPCHK(hipMemcpyAsync(hres + (size_t)r * n + a, dr[r], 4ull * m, hipMemcpyDeviceToHost, c->stream));
@@ -1058,7 +1061,8 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   HIPCHK(hipMemcpyAsync(c->glist.p, c->hglist.data(), 4ull * ng, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(c->gpbase.p, c->hgpbase.data(), 4ull * (ng + 1), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(c->gsbase.p, c->hgsbase.data(), 8ull * (ng + 1), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemsetAsync(c->gcnt.p, 0, 8, st));  // the block counter, the members finished
+  // the block counter, and (unless a later chunk of one host batch) the members finished
+  HIPCHK(hipMemsetAsync(c->gcnt.p, 0, c->keep_counts ? 4 : 8, st));
   HIPCHK(hipEventRecord(c->fork, st));
   HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
   hipStream_t sd = c->side;
@@ -1133,7 +1137,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
-  c->seg_used = false;
+  if (!c->keep_counts) c->seg_used = false;
   // every decoder stores whole dwords: up to 3 bytes past a member's end, inside its
   // capacity rounded up to a multiple of 4 -- which the next 4-aligned offset cannot overlap
   for (uint32_t i = 0; i < n; i++)
@@ -1225,7 +1229,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       }
       if (!c->hwlist.empty() || !c->hslist.empty() || !c->hglist.empty()) wave_min = big_min;
     }
-    c->seg_used = !c->hglist.empty();
+    c->seg_used |= !c->hglist.empty();
     if (!c->hglist.empty()) {
       const int r = seg_launch(c, st, wbits, n, d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, in_len, out_cap, lres);
       if (r != ZS_OK) return r;
@@ -1359,7 +1363,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
                                     c->istate.as<zs_inflate_result>(), lres, c->inflate_ref_wrap ? ZS_INF_REF_WRAP : 0);
   MARK("inflate");
   HIPCHK(c->lstat.ensure(16));
-  HIPCHK(hipMemsetAsync(c->lstat.p, 0, 4, st));
+  if (!c->keep_counts) HIPCHK(hipMemsetAsync(c->lstat.p, 0, 4, st));
   zs_k_inflate_finish<<<(n + 255) / 256, 256, 0, st>>>(c->istate.as<zs_inflate_result>(), lres, d_status, d_phase,
                                                        d_msg, d_out_len, d_consumed, (int)n, c->lstat.as<uint32_t>());
   if (!c->lane_count_host) {

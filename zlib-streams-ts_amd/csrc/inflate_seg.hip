@@ -358,8 +358,12 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
   uint32_t pos = q, cum = 0, nck = 0, nxt = lane + 1, to = ZS_SEG_NONE, end = 0, last_len = 0;
   uint32_t pe = lane == 0 ? (r == 0 ? 0u : f) : q;  // the end of the symbol before (events)
   uint32_t nev = 0, ev_k[ZS_SEG_NEV], ev_sb[ZS_SEG_NEV], ev_c[ZS_SEG_NEV];
+  // End-of-block codes and invalid codes met: those in the lane's window (where
+  // its garbage before the sync point is) in rings of the last ZS_SEG_NEOB, and
+  // the first one past the window (always in the true stream, or past the end).
   uint32_t neob = 0, eob_sb[ZS_SEG_NEOB], eob_end[ZS_SEG_NEOB], eob_cum[ZS_SEG_NEOB];
-  uint32_t nbad = 0, bad_sb[ZS_SEG_NEOB];  // invalid codes met (garbage before the start / past the end, or an error)
+  uint32_t xeob_sb = ZS_SEG_NONE, xeob_end = 0, xeob_cum = 0;
+  uint32_t nbad = 0, bad_sb[ZS_SEG_NEOB], xbad = ZS_SEG_NONE;
   uint32_t cum_end = 0;
 #pragma unroll
   for (uint32_t e = 0; e < ZS_SEG_NEV; e++) ev_k[e] = ev_sb[e] = ev_c[e] = 0;
@@ -388,25 +392,26 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
       if (fr != ~0ull && V.conf[(uint32_t)(fr >> 32)]) V.conf[lane] = 1;
     }
     const bool cf = act && V.conf[lane];
-    // a confirmed lane ends the block at its first end-of-block code at or past its start
-    if (cf && neob) {
+    // a confirmed lane ends the block at its first end-of-block code at or past
+    // its start (it may have decoded on past it, waiting to be confirmed)
+    if (cf && (neob || xeob_sb != ZS_SEG_NONE)) {
       const uint32_t st = lane == 0 ? sym0 : (uint32_t)V.from[lane];
-      bool hit = false;
+      uint32_t hs = ZS_SEG_NONE;
 #pragma unroll
       for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
-        if (!hit && e < neob && eob_sb[e] >= st) {
-          hit = true;
+        if (e < neob && eob_sb[e] >= st && eob_sb[e] < hs) {
+          hs = eob_sb[e];
           end = eob_end[e];
-          cum_end = eob_cum[e];  // (the lane may have decoded on past it, waiting to be confirmed)
+          cum_end = eob_cum[e];
         }
-      if (hit) {
+      if (hs == ZS_SEG_NONE && xeob_sb != ZS_SEG_NONE) {
+        hs = xeob_sb;
+        end = xeob_end;
+        cum_end = xeob_cum;
+      }
+      if (hs != ZS_SEG_NONE) {
         act = false;
         kind = ZS_SG_K_BEND;
-        V.prog[lane] = ZS_SEG_NONE;
-        V.done = 1;
-      } else if (neob > ZS_SEG_NEOB) {
-        act = false;  // the log overflowed: the block's end may be lost (the chain breaks here)
-        kind = ZS_SG_K_STOP;
         V.prog[lane] = ZS_SEG_NONE;
         V.done = 1;
       }
@@ -466,10 +471,14 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
       const uint32_t sb = pos;
       const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
       if (y.kind == ZS_SG_BAD) {
+        if (sb - q < ZS_SEG_W) {
 #pragma unroll
-        for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
-          if (e == nbad) bad_sb[e] = sb;
-        nbad++;
+          for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
+            if (e == (nbad & (ZS_SEG_NEOB - 1u))) bad_sb[e] = sb;
+          nbad++;
+        } else if (xbad == ZS_SEG_NONE) {
+          xbad = sb;
+        }
         pos = sb + 1u;
         zs_sg_seek(G, pos);
         pe = pos;
@@ -490,14 +499,20 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
           bd += 262144u;
         }
         if (y.kind == ZS_SG_EOB) {
+          if (sb - q < ZS_SEG_W) {
 #pragma unroll
-          for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
-            if (e == neob) {
-              eob_sb[e] = sb;
-              eob_end[e] = se;
-              eob_cum[e] = cum;
-            }
-          neob++;
+            for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
+              if (e == (neob & (ZS_SEG_NEOB - 1u))) {
+                eob_sb[e] = sb;
+                eob_end[e] = se;
+                eob_cum[e] = cum;
+              }
+            neob = min(neob + 1u, 2u * ZS_SEG_NEOB);  // (a ring: the last ZS_SEG_NEOB)
+          } else if (xeob_sb == ZS_SEG_NONE) {
+            xeob_sb = sb;
+            xeob_end = se;
+            xeob_cum = cum;
+          }
           last_len = 0;
         } else {
           cum += y.len;
@@ -572,13 +587,16 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
         ne++;
       }
     }
-    bad |= nev > ZS_SEG_NEV || nbad > ZS_SEG_NEOB || neob > ZS_SEG_NEOB;
+    bad |= nev > ZS_SEG_NEV;
     // an invalid code, or an end of block before the piece's end, in the true stream
+    // (the rings hold the last ones of the window: any in the true stream is among them)
 #pragma unroll
     for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) bad |= e < nbad && bad_sb[e] >= start && bad_sb[e] < end;
+    bad |= xbad < end;
     if (kind == ZS_SG_K_SYNC) {
 #pragma unroll
       for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) bad |= e < neob && eob_sb[e] >= start;
+      bad |= xeob_sb < end;
     }
     zs_seg_lane& P = lanes[(size_t)b * ZS_SEG_LANES + lane];
     P.start = start;

@@ -49,7 +49,11 @@
 struct zs_hdr_src {
   const uint32_t* w4;
   uint32_t sh, last;
-  __device__ __forceinline__ uint32_t word(uint32_t q) const { return w4[min(q, last)]; }
+  const uint32_t* lw;  // a window of the aligned words staged in LDS: [lq0, lq0 + ln)
+  uint32_t lq0, ln;
+  __device__ __forceinline__ uint32_t word(uint32_t q) const {
+    return q - lq0 < ln ? lw[q - lq0] : w4[min(q, last)];
+  }
   __device__ __forceinline__ uint32_t load4(uint64_t at) const {  // bytes [at, at + 4)
     const uint64_t cb = at + sh;
     const uint32_t q = (uint32_t)(cb >> 2);
@@ -205,6 +209,15 @@ static __device__ __forceinline__ bool zs_split_kraft(uint64_t a, uint64_t b) {
 // with an accepted candidate holds the range's first.
 #define ZS_FIND_T 256u
 #define ZS_FIND_Q 1024u
+#ifndef ZS_FIND_EXP
+#define ZS_FIND_EXP 0  // timing experiments (0 in the product): 1 no full checks, 2 no Kraft test, 4 staging only, 8 counters
+#endif
+#if ZS_FIND_EXP & 8
+__device__ unsigned long long zs_find_stat[4];  // chunks, queued, checked, clock cycles in the checks
+extern "C" int zs_find_stats(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_find_stat), sizeof(zs_find_stat));
+}
+#endif
 __global__ __launch_bounds__(256) void zs_k_split_find(const uint8_t* __restrict__ in,
                                                      const uint64_t* __restrict__ in_off,
                                                      const uint32_t* __restrict__ in_len,
@@ -212,7 +225,8 @@ __global__ __launch_bounds__(256) void zs_k_split_find(const uint8_t* __restrict
                                                      uint64_t* __restrict__ found) {
   __shared__ unsigned long long best;
   __shared__ uint32_t nq;
-  __shared__ uint32_t qoff[ZS_FIND_Q];  // queued candidates, bits past the range's start
+  __shared__ uint32_t qoff[ZS_FIND_Q];       // queued candidates, bits past the range's start
+  __shared__ uint32_t stage[2 * ZS_FIND_T];  // the chunk's aligned words and as many after (the headers' bits)
   const uint32_t m = blockIdx.x / ZS_SPLIT_MAX, r = blockIdx.x % ZS_SPLIT_MAX, t = threadIdx.x;
   const uint32_t s = list[m];
   const uint32_t n = in_len[s];
@@ -234,10 +248,19 @@ __global__ __launch_bounds__(256) void zs_k_split_find(const uint8_t* __restrict
   S.sh = (uint32_t)((uintptr_t)src & 3u);
   S.w4 = reinterpret_cast<const uint32_t*>(src - S.sh);
   S.last = (S.sh + n - 1u) >> 2;
+  S.lw = stage;
+  S.ln = 0;
+  S.lq0 = 0;
   const uint64_t w_lo = lo >> 5, w_hi = (hi + 31u) >> 5;
   for (uint64_t wc = w_lo; wc < w_hi; wc += ZS_FIND_T) {
+    // stage the chunk's words (and 1 KiB after): the quick tests and most header checks read LDS
+    S.ln = 0;
+    for (uint32_t i = t; i < 2 * ZS_FIND_T; i += ZS_FIND_T) stage[i] = S.word((uint32_t)wc + i);
+    __syncthreads();
+    S.lq0 = (uint32_t)wc;
+    S.ln = 2 * ZS_FIND_T;
     const uint64_t w = wc + t;
-    if (w < w_hi) {
+    if (!(ZS_FIND_EXP & 4) && w < w_hi) {
       // member words w .. w+4 (member bit 32 w on), from the aligned words
       uint32_t mw[5];
       {
@@ -260,7 +283,7 @@ __global__ __launch_bounds__(256) void zs_k_split_find(const uint8_t* __restrict
         c &= c - 1u;
         const uint64_t a = o ? (x0 >> o) | (x1 << (64u - o)) : x0;
         const uint64_t bb = o ? (x1 >> o) | (x2 << (64u - o)) : x1;
-        if (zs_split_kraft(a, bb)) {
+        if (!(ZS_FIND_EXP & 2) && zs_split_kraft(a, bb)) {
           const uint32_t qi = atomicAdd(&nq, 1u);
           if (qi < ZS_FIND_Q) qoff[qi] = (uint32_t)(b0 + o - lo);
           else if (zs_split_header_rest(S, b0 + o, nbits, a, bb)) atomicMin(&best, (unsigned long long)(b0 + o));
@@ -268,10 +291,20 @@ __global__ __launch_bounds__(256) void zs_k_split_find(const uint8_t* __restrict
       }
     }
     __syncthreads();
-    const uint32_t cnt = min(nq, ZS_FIND_Q);
+    const uint32_t cnt = (ZS_FIND_EXP & 1) ? 0u : min(nq, ZS_FIND_Q);
+#if ZS_FIND_EXP & 8
+    if (t == 0) {
+      atomicAdd(&zs_find_stat[0], 1ull);
+      atomicAdd(&zs_find_stat[1], (unsigned long long)cnt);
+    }
+    const unsigned long long tc0 = clock64();
+#endif
     for (uint32_t i = t; i < cnt; i += ZS_FIND_T) {
       const uint64_t bit = lo + qoff[i];
       if (bit >= best) continue;
+#if ZS_FIND_EXP & 8
+      atomicAdd(&zs_find_stat[2], 1ull);
+#endif
       uint64_t a, bb;
       {
         const uint64_t cb = (bit >> 3) + S.sh;
@@ -284,10 +317,13 @@ __global__ __launch_bounds__(256) void zs_k_split_find(const uint8_t* __restrict
       }
       if (zs_split_header_rest(S, bit, nbits, a, bb)) atomicMin(&best, (unsigned long long)bit);
     }
+#if ZS_FIND_EXP & 8
+    if ((t & 63) == 0) atomicAdd(&zs_find_stat[3], clock64() - tc0);
+#endif
     __syncthreads();
     if (best != ~0ull) break;
     if (t == 0) nq = 0;
-    __syncthreads();
+    __syncthreads();  // (also: the stage is rewritten next)
   }
   if (t == 0) found[blockIdx.x] = best;
 }
