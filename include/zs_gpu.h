@@ -74,11 +74,12 @@ void zs_ctx_destroy(zs_ctx *ctx);
 const char *zs_last_error(void);
 const char *zs_version(void);
 
-/* Re-checks the hardware property the chain builder relies on: same-address
+/* Re-checks the hardware property the fast chain builders use: same-address
  * LDS atomics of one wave instruction apply in lane order (gfx950).  Writes the
- * number of violations (0 expected).  zs_ctx_create runs it and fails with
- * ZS_STREAM_ERROR when it does not hold.  No reference counterpart (engine
- * self-check). */
+ * number of violations (0 expected).  zs_ctx_create runs it; when it does not
+ * hold, the context uses the ballot-ranked builders instead (option lane_order
+ * = 0, which can also be set by hand; the output bytes are the same).  No
+ * reference counterpart (engine self-check). */
 int zs_selftest(zs_ctx *ctx, uint64_t *violations);
 
 /* deflateBound for a fresh stream with memLevel 8 (deflate.ts:615-674). */

@@ -226,8 +226,42 @@ def test_c4_256k_streams_match_reference_goldens(engine, name, level):
 
 @pytest.mark.gpu
 def test_lds_atomic_lane_order_selftest(engine):
-    """The chain builder's hardware assumption (selftest.hip) holds on this part."""
+    """The fast chain builders' hardware assumption (selftest.hip) holds on this part."""
     assert engine.selftest() == 0
+
+
+@pytest.mark.parametrize("level", [1, 2, 3, 4, 6, 9])
+def test_ballot_ranked_builders_equal_lane_ordered_ones(engine, level):
+    """lane_order = 0: zs_k_bucket / zs_k_prev / zs_k_fast rank equal hashes by
+    ballots (zs_wave_match) instead of relying on same-address LDS atomics of one
+    instruction applying in lane order -- the form a device failing the self-test
+    runs.  Same bytes as the default on C2 streams (65536 B: bucket + sweep), C4
+    256 KiB streams (prev + match at L4-9, zs_k_fast at L1-3), all-zero streams
+    (one hash per group), random and ragged streams; the C2 goldens at L6."""
+    import zsamd
+
+    specs = [("zeros", 65536), ("zeros", 200000), ("rand", 65536), ("rand", 70001), ("mixed", 131072 + 17),
+             ("text", 1), ("text", 3), ("text", 64), ("text", 65537), ("ramp", 70000)]
+    inputs = [corpus.make({"kind": k, "n": n, "seed": 9700 + i}) for i, (k, n) in enumerate(specs)]
+    inputs += [bytes(b) for b in (zsamd.corpus("text", 0, 1, 262144), zsamd.corpus("text", 1, 1, 262144))]
+    c2 = bytes(zsamd.corpus("text", 0, 64, 65536))
+    inputs += [c2[i * 65536:(i + 1) * 65536] for i in range(64)]
+    outs = []
+    try:
+        for order in (1, 0):
+            engine.set_option("lane_order", order)
+            outs.append(engine.compress_batch_raw(inputs, "deflate-raw", level))
+    finally:
+        engine.set_option("lane_order", 1)
+    bad = [i for i in range(len(inputs)) if outs[0][i] != outs[1][i]]
+    assert not bad, bad[:10]
+    if level == 6:
+        recs = golden_io.batch("t64_l6_raw")
+        k0 = len(inputs) - 64
+        assert all((len(outs[1][k0 + i][1]), hashlib.sha256(outs[1][k0 + i][1]).digest()[:16]) == recs[i]
+                   for i in range(64))
+    for d, (st, out) in zip(inputs[:len(specs)], outs[1]):
+        assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1], len(d)
 
 
 def test_level0_stored_layout_matches_reference_goldens(engine):

@@ -97,6 +97,11 @@ struct zs_ctx {
   int cur_pw = 1;            // waves per stream of the current deflate batch's parse (zs_k_parse / _2w / _4w)
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
+  // the chain builders (zs_k_bucket, zs_k_prev, zs_k_fast) let same-address LDS atomics of
+  // one instruction apply in lane order (1) or rank equal hashes by ballots (0); 0 when the
+  // self-test finds the order violated on this device
+  bool lane_order = true;
+  bool lane_order_ok = true;  // the self-test's verdict
   uint32_t inflate_wave_min = 32768;  // members with more input bytes decode one per wave (inflate_wave.hip); 0: never
   uint32_t lane_large_min = 2304;     // this many large members or more: one LANE each (zs_k_inflate_lane<.., true>); 256 KiB members: wave kernel 26.9 / 68.5 / 128 ms at 1024 / 2048 / 4096, lanes 68.6 / 78.3 / 77.7
   hipStream_t side = nullptr;         // second stream: the wave-per-member kernel runs beside the lane kernel
@@ -233,15 +238,16 @@ int zs_ctx_create(int device, zs_ctx** out) {
     zs_ctx_destroy(c);
     return fail(ZS_MEM_ERROR, "%s", "cannot create the side stream");
   }
-  // the chain builder relies on lane-ordered LDS atomics: check before any use
+  // the chain builders use lane-ordered LDS atomics where the device applies them so:
+  // check before any use; a device that violates it gets the ballot-ranked form
   uint64_t bad = 0;
   const int st = zs_selftest(c, &bad);
-  if (st != ZS_OK || bad != 0) {
-    const std::string why = st != ZS_OK ? std::string(zs_last_error())
-                                        : std::to_string(bad) + " lane-order violations of same-address LDS atomics";
+  if (st != ZS_OK) {
+    const std::string why = zs_last_error();
     zs_ctx_destroy(c);
     return fail(ZS_STREAM_ERROR, "self-test failed: %s", why.c_str());
   }
+  c->lane_order = c->lane_order_ok = bad == 0;
   *out = c;
   return ZS_OK;
 }
@@ -306,6 +312,11 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "fast_group")) c->fast_group = value != 0;
+  else if (!strcmp(name, "lane_order")) {
+    if (value && !c->lane_order_ok)
+      return fail(ZS_STREAM_ERROR, "lane_order: this device does not apply LDS atomics in lane order");
+    c->lane_order = value != 0;
+  }
   else if (!strcmp(name, "inflate_split")) c->inflate_split = value != 0;
   else if (!strcmp(name, "inflate_seg")) c->inflate_seg = value != 0;
   else if (!strcmp(name, "seg_bits")) {
@@ -463,9 +474,11 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
     if (c->match_sweep) {
       // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
       // longer ones: chain links + per-tile chain walk (deflate_match.hip)
-      zs_k_bucket<<<n, 256, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
+      (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<n, 256, 0, st>>>(
+          d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
       if (max_len > 65537u)
-        zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), 65537u);
+        (c->lane_order ? zs_k_prev<true> : zs_k_prev<false>)<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos,
+                                                                               c->prevd.as<uint16_t>(), 65537u);
       MARK("bucket");
       zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
                                      cfg.chain, cfg.nice);
@@ -477,7 +490,8 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
       }
     } else {
       // cross-check (option match_sweep = 0): the chain-walk kernels for every stream
-      zs_k_prev<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), 0u);
+      (c->lane_order ? zs_k_prev<true> : zs_k_prev<false>)<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos,
+                                                                             c->prevd.as<uint16_t>(), 0u);
       MARK("prev");
       if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
                                                    c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
@@ -491,7 +505,9 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
   } else {
     const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
     // levels 1..3: the group-speculative replay (default) or the step-by-step one (fast_group = 0)
-    auto fast = !c->fast_group ? zs_k_fast_serial : cfg.nice <= 8 ? zs_k_fast<2> : cfg.nice <= 16 ? zs_k_fast<4> : zs_k_fast<8>;
+    auto fast = !c->fast_group ? zs_k_fast_serial
+                : c->lane_order   ? (cfg.nice <= 8 ? zs_k_fast<2, true> : cfg.nice <= 16 ? zs_k_fast<4, true> : zs_k_fast<8, true>)
+                                  : (cfg.nice <= 8 ? zs_k_fast<2, false> : cfg.nice <= 16 ? zs_k_fast<4, false> : zs_k_fast<8, false>);
     HIPCHK(hipFuncSetAttribute((const void*)fast, hipFuncAttributeMaxDynamicSharedMemorySize, fast_smem));
     fast<<<n, 64, fast_smem, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, syms, d_bk, d_st,
                                         cfg.chain, cfg.lazy, cfg.nice);

@@ -256,7 +256,12 @@ static __device__ __forceinline__ uint32_t zs_fg_mskor(uint32_t addr, uint32_t m
   return old;
 }
 
-template <int NW>  // words compared per walk candidate: nice / 4 (2 / 4 / 8 at levels 1 / 2 / 3)
+// NW: words compared per walk candidate: nice / 4 (2 / 4 / 8 at levels 1 / 2 / 3).
+// ORD = false (option lane_order = 0, or a device that fails the self-test): the
+// links the lane-ordered exchanges hand out come from zs_wave_match instead --
+// the highest lower lane of the same hash, else head[h] -- and the last lane of
+// each hash stores head[h] with a plain half-word store.
+template <int NW, bool ORD>
 __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                 const uint32_t* __restrict__ in_len,
                                                 const uint64_t* __restrict__ pos_base,
@@ -368,10 +373,16 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
     const uint32_t h = (((hw & 0xffu) << 10) ^ (((hw >> 8) & 0xffu) << 5) ^ ((hw >> 16) & 0xffu)) & ZS_HASH_MASK;
     const uint32_t ha = zs_fg_addr(&L.head[h >> 1]), sh = 16u * (h & 1u);
     const uint32_t hm = ok ? 0xffffu << sh : 0u;
-    const uint32_t sp = (zs_fg_mskor(ha, hm, ok ? (rg0 + lane) << sh : 0u) >> sh) & 0xffffu;
-    const bool spin = sp != 0u && sp >= rg0;  // the link is an earlier lane of the group
-    // the first lane of each hash restores the original head, which every lane then reads
-    (void)zs_fg_mskor(ha, ok && !spin ? hm : 0u, ok && !spin ? sp << sh : 0u);
+    uint32_t sp;
+    if (ORD) {
+      sp = (zs_fg_mskor(ha, hm, ok ? (rg0 + lane) << sh : 0u) >> sh) & 0xffffu;
+      const bool spin = sp != 0u && sp >= rg0;  // the link is an earlier lane of the group
+      // the first lane of each hash restores the original head, which every lane then reads
+      (void)zs_fg_mskor(ha, ok && !spin ? hm : 0u, ok && !spin ? sp << sh : 0u);
+    } else {
+      const int pl = zs_lane_below(zs_wave_match(h, ok), lane);
+      sp = !ok ? 0u : pl >= 0 ? rg0 + (uint32_t)pl : (L.head[h >> 1] >> sh) & 0xffffu;
+    }
     const uint32_t orig = ok ? (L.head[h >> 1] >> sh) & 0xffffu : 0u;
 
     FG_T(1);
@@ -582,7 +593,19 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
     FG_T(3);
     // ---- 4. the truly inserted positions enter head[] / prev[] in lane order
     const bool ins = (tm >> lane) & 1ull;
-    const uint32_t tp = (zs_fg_mskor(ha, ins ? hm : 0u, ins ? (rg0 + lane) << sh : 0u) >> sh) & 0xffffu;
+    uint32_t tp;
+    if (ORD) {
+      tp = (zs_fg_mskor(ha, ins ? hm : 0u, ins ? (rg0 + lane) << sh : 0u) >> sh) & 0xffffu;
+    } else {
+      const uint64_t im = zs_wave_match(h, ins);
+      const int pl = zs_lane_below(im, lane);
+      tp = pl >= 0 ? rg0 + (uint32_t)pl : (L.head[h >> 1] >> sh) & 0xffffu;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      if (ins && (im >> lane) == 1ull) reinterpret_cast<uint16_t*>(L.head)[h] = (uint16_t)(rg0 + lane);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
     if (ins) L.prev[(rg0 + lane) & 0x7fffu] = (uint16_t)tp;
     FG_T(4);
   }
@@ -598,9 +621,15 @@ __global__ __launch_bounds__(64) void zs_k_fast(const uint8_t* __restrict__ in, 
   }
 }
 
-template __global__ void zs_k_fast<2>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+template __global__ void zs_k_fast<2, true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
                                       uint32_t*, zs_block*, zs_stream*, int, int, int);
-template __global__ void zs_k_fast<4>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+template __global__ void zs_k_fast<4, true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
                                       uint32_t*, zs_block*, zs_stream*, int, int, int);
-template __global__ void zs_k_fast<8>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+template __global__ void zs_k_fast<8, true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+                                      uint32_t*, zs_block*, zs_stream*, int, int, int);
+template __global__ void zs_k_fast<2, false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+                                      uint32_t*, zs_block*, zs_stream*, int, int, int);
+template __global__ void zs_k_fast<4, false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
+                                      uint32_t*, zs_block*, zs_stream*, int, int, int);
+template __global__ void zs_k_fast<8, false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, const uint32_t*,
                                       uint32_t*, zs_block*, zs_stream*, int, int, int);

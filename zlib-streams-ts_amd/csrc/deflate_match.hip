@@ -32,7 +32,11 @@
 // by zs_selftest), so the value each lane gets back is exactly the previous
 // position with the same hash -- the reference's prev[] link.  head[] holds
 // q + 1 (absolute, 32-bit), so no slide (deflate.ts:125-141) is needed.
+// ORD = false (option lane_order = 0, or a device that fails the self-test):
+// each lane's link is the highest lower lane of the group with the same hash
+// (zs_wave_match) or head[h], and the group's last lane of each hash stores it.
 #define ZS_PREV_STAGE 4096u
+template <bool ORD>
 __global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                 const uint32_t* __restrict__ in_len,
                                                 const uint64_t* __restrict__ pos_base, uint16_t* __restrict__ prevd,
@@ -76,10 +80,24 @@ __global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, 
         h[j] = (((w & 0xffu) << 10) ^ (((w >> 8) & 0xffu) << 5) ^ ((w >> 16) & 0xffu)) & ZS_HASH_MASK;
       }
       // in order: group j's exchanges land after group j-1's (LDS executes a wave's ops in order)
+      if (ORD) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t p = g0 + 64 * j + lane;
-        e[j] = valid[j] ? atomicExch(&head[h[j]], p + 1) : 0u;
+        for (int j = 0; j < 4; j++) {
+          const uint32_t p = g0 + 64 * j + lane;
+          e[j] = valid[j] ? atomicExch(&head[h[j]], p + 1) : 0u;
+        }
+      } else {
+        for (int j = 0; j < 4; j++) {
+          const uint32_t p = g0 + 64 * j + lane;
+          const uint64_t mm = zs_wave_match(h[j], valid[j]);
+          const int pl = zs_lane_below(mm, lane);
+          e[j] = !valid[j] ? 0u : pl >= 0 ? g0 + 64 * j + (uint32_t)pl + 1u : head[h[j]];
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
+          if (valid[j] && (mm >> lane) == 1ull) head[h[j]] = p + 1;  // the last lane of its hash
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
+        }
       }
 #pragma unroll
       for (int j = 0; j < 4; j++) {
@@ -93,6 +111,10 @@ __global__ __launch_bounds__(64) void zs_k_prev(const uint8_t* __restrict__ in, 
   }
 }
 
+template __global__ void zs_k_prev<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, uint16_t*,
+                                         uint32_t);
+template __global__ void zs_k_prev<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, uint16_t*,
+                                          uint32_t);
 
 // --------------------------------------------------------------- zs_k_match
 #define ZS_TILE 8192u

@@ -93,6 +93,7 @@ extern "C" int zs_bucket_stats(unsigned long long* out) {
 #define ZS_BK_INFLIGHT 8  // pass 2: wave instructions (x 64 positions) per wait
 #define ZS_BK_CHUNK 2048u  // pass 2: positions per chunk (input bytes staged in LDS, slots queued)
 
+template <bool ORD>  // false: claims ranked by zs_wave_match instead of the LDS atomics' lane order
 __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __restrict__ in,
                                                             const uint64_t* __restrict__ in_off,
                                                             const uint32_t* __restrict__ in_len,
@@ -222,16 +223,33 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
       const uint32_t c1 = min(m, c0 + ZS_BK_CHUNK);
       uint16_t* const qc = q[c & 1u];
       for (uint32_t g0 = c0; g0 < c1; g0 += 64 * ZS_BK_INFLIGHT) {
-        uint32_t a[ZS_BK_INFLIGHT], v[ZS_BK_INFLIGHT], sh[ZS_BK_INFLIGHT], e[ZS_BK_INFLIGHT];
+        uint32_t a[ZS_BK_INFLIGHT], v[ZS_BK_INFLIGHT], sh[ZS_BK_INFLIGHT], e[ZS_BK_INFLIGHT], hh[ZS_BK_INFLIGHT];
 #pragma unroll
         for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
           const uint32_t p = g0 + 64 * j + lane;
           const uint32_t o = p - c0;
           const uint32_t h = sw_hash(__builtin_amdgcn_alignbyte(stg[(o >> 2) + 1], stg[o >> 2], o & 3u));
+          hh[j] = h;
           sh[j] = 16u * (h & 1u);
           a[j] = sw_lds_addr(&cnt[h >> 1]);
           v[j] = p < c1 ? 1u << sh[j] : 0u;  // a lane past the chunk adds nothing
         }
+        if (!ORD) {
+          // order-independent: one add per distinct hash (its lowest lane), ranks by ballot
+#pragma unroll
+          for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
+            const uint32_t p = g0 + 64 * j + lane;
+            const uint32_t h = hh[j];
+            const uint64_t mm = zs_wave_match(h, p < c1);
+            const uint32_t rank = (uint32_t)__builtin_popcountll(mm & ((1ull << lane) - 1ull));
+            const uint32_t lead = mm ? (uint32_t)__builtin_ctzll(mm) : lane;
+            uint32_t old = 0;
+            if (p < c1 && lead == lane)
+              old = atomicAdd(&cnt[h >> 1], (uint32_t)__builtin_popcountll(mm) << sh[j]);
+            old = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead * 4u), (int)old);
+            e[j] = old + (rank << sh[j]);
+          }
+        } else {
         // in order: instruction j's adds land after instruction j-1's (LDS executes a wave's ops in order)
         asm volatile(
             "ds_add_rtn_u32 %0, %8, %16\n\t"
@@ -247,6 +265,7 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
             : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(v[0]),
               "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7])
             : "memory");
+        }
 #pragma unroll
         for (int j = 0; j < ZS_BK_INFLIGHT; j++) {
           const uint32_t p = g0 + 64 * j + lane;
@@ -262,6 +281,10 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
   }
   BK_MARK(2);
 }
+template __global__ void zs_k_bucket<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, uint16_t*,
+                                           uint2*);
+template __global__ void zs_k_bucket<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, uint16_t*,
+                                            uint2*);
 
 // --------------------------------------------------------------- zs_k_sweep
 static __device__ __forceinline__ uint32_t sw_word(const uint32_t* win, uint32_t off) {

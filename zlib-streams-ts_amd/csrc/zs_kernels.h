@@ -30,11 +30,14 @@ struct zs_stream {
   uint32_t pad;
 };
 
+// ORD: same-address LDS atomics of one instruction apply in lane order (zs_selftest); false: the ballot form
+template <bool ORD>
 __global__ void zs_k_prev(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           uint16_t* prevd, uint32_t min_len);
 __global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint16_t* prevd, uint2* mres, int chain, int nice, uint32_t min_len);
 // levels 4..9, streams of at most 65,537 bytes (deflate_sweep.hip)
+template <bool ORD>
 __global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                             uint16_t* members, uint2* mres);
 __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
@@ -54,7 +57,7 @@ ZS_PARSE_DECL(zs_k_parse_4w)  // four waves per stream, ZS_PARSE4W_SEG-position 
 #define ZS_PARSE2W_SEG_WORDS 2060u
 #define ZS_PARSE4W_SEG 256u
 #define ZS_PARSE4W_SEG_WORDS 1292u
-template <int NW>
+template <int NW, bool ORD>
 __global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,
                           int lazy, int nice);
