@@ -601,7 +601,7 @@ def main_inflate(args):
     D.barrier()
     elapsed = D.max(time.perf_counter() - t0)
     for ph in ("inflate_lane", "inflate_long", "inflate_wave", "inflate_large", "split_find", "split_decode", "split_resolve",
-               "seg_find", "seg_sync", "seg_plan", "seg_decode", "seg_resolve", "seg_fallback",
+               "seg_find", "seg_walk", "seg_plan", "seg_decode", "seg_resolve", "seg_fallback",
                "inflate_join", "inflate_check", "inflate", "finish"):
         v = eng.last_ms(ph)  # summed over the timed steps
         if v >= 0:

@@ -30,6 +30,7 @@ static inline uint32_t zs_host_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
 #define __builtin_amdgcn_alignbyte(hi, lo, s) zs_host_alignbyte(hi, lo, s)
 // one lane: a ballot is the lane's own bit, LDS atomics are plain read-modify-writes
 #define __builtin_amdgcn_ballot_w64(c) ((c) ? 1ull : 0ull)
+#define __builtin_amdgcn_readlane(v, l) (v)  // (one lane)
 static inline uint32_t atomicAdd(uint32_t* p, uint32_t v) {
   const uint32_t o = *p;
   *p = o + v;

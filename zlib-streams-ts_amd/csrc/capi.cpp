@@ -105,7 +105,8 @@ struct zs_ctx {
   uint32_t inflate_wave_min = 32768;  // members with more input bytes decode one per wave (inflate_wave.hip); 0: never
   uint32_t lane_large_min = 2304;     // this many large members or more: one LANE each (zs_k_inflate_lane<.., true>); 256 KiB members: wave kernel 26.9 / 68.5 / 128 ms at 1024 / 2048 / 4096, lanes 68.6 / 78.3 / 77.7
   hipStream_t side = nullptr;         // second stream: the wave-per-member kernel runs beside the lane kernel
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipStream_t side2 = nullptr;        // third: the split decode, beside the segmented decode
+  hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
   Buf wlist;
   std::vector<uint32_t> hwlist;
   // split decode of large members (inflate_split.hip): deflate64, or raw deflate without the window-wrap copy
@@ -114,11 +115,11 @@ struct zs_ctx {
   std::vector<uint32_t> hslist;
   // segmented decode (inflate_seg.hip): a member's blocks cut into lane-sized pieces that synchronise
   bool inflate_seg = true;
-  uint32_t seg_bits = 4096;         // bits of input per piece at least (> 2 ZS_SEG_W)
+  uint32_t seg_bits = 2048;         // input bits per lane of an entry's first block (later ones: from the block before)
   uint32_t seg_small_batch = 16384; // batches of at most this many members ...
   uint32_t seg_small_min = 4096;    // ... send members with more input bytes than this to it too
-  Buf glist, gfound, gcidx, gblk, glanes, gtab, gmem, gpbase, gplist, gsbase, gscr, gcnt;
-  std::vector<uint32_t> hglist, hgpbase;
+  Buf glist, gfound, gbig, gbigs, gspb, gspl, gflist, gent, gblk, glanes, gtab, gmem, gpbase, gplist, gsbase, gscr, gcnt;
+  std::vector<uint32_t> hglist, hgpbase, hgspb, hgbig, hgbig_s;
   bool seg_used = false;            // the last inflate batch ran it
   std::vector<uint64_t> hgsbase;
   // host staging for the host-buffer entry points
@@ -231,6 +232,8 @@ int zs_ctx_create(int device, zs_ctx** out) {
     return fail(ZS_MEM_ERROR, "%s", hipGetErrorString(e));
   }
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join2, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
@@ -278,7 +281,7 @@ void zs_ctx_destroy(zs_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   for (Buf* b : {&c->lstat, &c->ltabs, &c->lres, &c->llen, &c->pscr, &c->meta, &c->prevd, &c->mres, &c->syms, &c->blocks, &c->streams, &c->codes, &c->hdr, &c->check,
                  &c->istate, &c->d_in, &c->d_out, &c->d_res, &c->d_pack, &c->wlist, &c->slist, &c->sfound,
-                 &c->spres, &c->sscr, &c->smem, &c->sval, &c->glist, &c->gfound, &c->gcidx, &c->gblk,
+                 &c->spres, &c->sscr, &c->smem, &c->sval, &c->glist, &c->gfound, &c->gbig, &c->gbigs, &c->gspb, &c->gspl, &c->gflist, &c->gent, &c->gblk,
                  &c->glanes, &c->gtab, &c->gmem, &c->gpbase, &c->gplist, &c->gsbase, &c->gscr, &c->gcnt})
     if (b->p) (void)hipFree(b->p);
   for (HostBuf* b : {&c->h_in, &c->h_out, &c->h_res, &c->h_offs})
@@ -297,6 +300,9 @@ void zs_ctx_destroy(zs_ctx* c) {
   if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->fork) (void)hipEventDestroy(c->fork);
   if (c->join) (void)hipEventDestroy(c->join);
+  if (c->side2) (void)hipStreamSynchronize(c->side2);
+  if (c->join2) (void)hipEventDestroy(c->join2);
+  if (c->side2) (void)hipStreamDestroy(c->side2);
   if (c->side) (void)hipStreamDestroy(c->side);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -320,7 +326,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "inflate_split")) c->inflate_split = value != 0;
   else if (!strcmp(name, "inflate_seg")) c->inflate_seg = value != 0;
   else if (!strcmp(name, "seg_bits")) {
-    if (value < (int)(2 * ZS_SEG_W) || value > (1 << 24)) return fail(ZS_STREAM_ERROR, "seg_bits must be 4096 .. 2^24");
+    if (value < (int)ZS_SEG_W || value > (int)ZS_SEG_SMAX) return fail(ZS_STREAM_ERROR, "seg_bits must be 1024 .. 8192");
     c->seg_bits = (uint32_t)value;
   } else if (!strcmp(name, "seg_small_batch")) {
     if (value < 0) return fail(ZS_STREAM_ERROR, "seg_small_batch must be >= 0");
@@ -930,13 +936,14 @@ extern "C" void zs_corpus(int kind, uint32_t first, uint32_t n_streams, uint32_t
 // 2 symbols (u32 each; count = streams[s].nsym), 3 blocks (zs_block each),
 // 4 stream record (zs_stream).  Returns the number of bytes copied.
 extern "C" uint64_t zs_debug_fetch(zs_ctx* c, int what, uint32_t s, void* dst, uint64_t cap) {
-  if (c && what >= 16 && what <= 20) {
-    // the segmented decode's records of the last inflate batch: 16 counters (blocks, members
-    // finished), 17 blocks (zs_seg_blk), 18 lanes (zs_seg_lane), 19 members (zs_seg_mem), 20 found[]
+  if (c && what >= 16 && what <= 21) {
+    // the segmented decode's records of the last inflate batch: 16 counters (-, members
+    // finished), 17 spans (zs_seg_blk), 18 lanes (zs_seg_lane), 19 members (zs_seg_mem), 20 found[]
+    // (big members), 21 entries (zs_seg_ent)
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     const Buf* b = what == 16 ? &c->gcnt : what == 17 ? &c->gblk : what == 18 ? &c->glanes : what == 19 ? &c->gmem
-                                                                                                  : &c->gfound;
+                   : what == 21 ? &c->gent : &c->gfound;
     const uint64_t bytes = std::min<uint64_t>(cap, b->cap);
     if (!b->p || !bytes || hipMemcpy(dst, b->p, bytes, hipMemcpyDeviceToHost) != hipSuccess) return 0;
     return bytes;
@@ -1049,36 +1056,60 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   const uint32_t ng = (uint32_t)c->hglist.size();
   const bool d64 = wbits == -16;
   const bool refw = c->inflate_ref_wrap && !d64;
-  // per member: the finder's candidates (at most one per range of >= 16,384 bits), the
-  // pieces' bound and their u16 scratch (each piece 16-byte aligned and padded)
+  // per member: span slots (one per ZS_SEG_BLOCK_BITS input bits for the blocks, twice the
+  // spans of the narrowest lanes, 8 more), the pieces' bound and their u16
+  // scratch (each piece 16-byte aligned and padded); members over ZS_SEG_BIG_BITS
+  // input bits also walk from the finder's block starts
   c->hgpbase.assign(ng + 1, 0);
   c->hgsbase.assign(ng + 1, 0);
-  uint64_t cap_blocks = 0;
+  c->hgspb.assign(ng + 1, 0);
+  c->hgbig.clear();
   for (uint32_t k = 0; k < ng; k++) {
     const uint32_t i = c->hglist[k];
     const uint64_t nbits = 8ull * in_len[i];
-    cap_blocks += std::min<uint64_t>(ZS_SPLIT_MAX, (nbits + zs_split_span(in_len[i]) - 1) / zs_split_span(in_len[i]));
-    const uint32_t pmax = (uint32_t)(nbits / c->seg_bits + ZS_SPLIT_MAX + 1);
+    const uint64_t spans = nbits / ZS_SEG_BLOCK_BITS + 2 * nbits / (64ull * ZS_SEG_W) + 8;
+    const uint32_t pmax = (uint32_t)std::min<uint64_t>(spans * ZS_SEG_LANES, nbits / ZS_SEG_W + spans + 1);
+    c->hgspb[k + 1] = c->hgspb[k] + (uint32_t)spans;
     c->hgpbase[k + 1] = c->hgpbase[k] + pmax;
     c->hgsbase[k + 1] = c->hgsbase[k] + ((((uint64_t)out_cap[i] + 7) & ~7ull) + ZS_SEG_PAD * (uint64_t)pmax + 16);
+    if (nbits > ZS_SEG_BIG_BITS) c->hgbig.push_back(k);
   }
+  const uint32_t nb = c->hgspb[ng], nbig = (uint32_t)c->hgbig.size();
   HIPCHK(c->glist.ensure(4ull * ng));
-  HIPCHK(c->gfound.ensure(8ull * ZS_SPLIT_MAX * ng));
-  HIPCHK(c->gcidx.ensure(4ull * ZS_SPLIT_MAX * ng));
-  HIPCHK(c->gblk.ensure(sizeof(zs_seg_blk) * cap_blocks));
-  HIPCHK(c->glanes.ensure(sizeof(zs_seg_lane) * ZS_SEG_LANES * cap_blocks));
-  HIPCHK(c->gtab.ensure(sizeof(zcode) * ZS_SEG_TAB * cap_blocks));
+  HIPCHK(c->gspb.ensure(4ull * (ng + 1)));
+  HIPCHK(c->gbig.ensure(4ull * nbig + 4));
+  HIPCHK(c->gfound.ensure(8ull * ZS_SPLIT_MAX * nbig + 8));
+  HIPCHK(c->gblk.ensure(sizeof(zs_seg_blk) * nb));
+  HIPCHK(c->glanes.ensure(sizeof(zs_seg_lane) * ZS_SEG_LANES * nb));
+  HIPCHK(c->gtab.ensure(sizeof(zcode) * ZS_SEG_TAB * nb));
+  HIPCHK(c->gent.ensure(sizeof(zs_seg_ent) * ZS_SPLIT_MAX * ng));
   HIPCHK(c->gmem.ensure(sizeof(zs_seg_mem) * ng));
   HIPCHK(c->gpbase.ensure(4ull * (ng + 1)));
   HIPCHK(c->gplist.ensure(16ull * c->hgpbase[ng] + 16));
   HIPCHK(c->gsbase.ensure(8ull * (ng + 1)));
   HIPCHK(c->gscr.ensure(2ull * c->hgsbase[ng] + 64));
   HIPCHK(c->gcnt.ensure(16));
+  // the big members' stream indices for the finder, then their list indices for the walk
+  c->hgbig_s.resize(nbig);
+  for (uint32_t k = 0; k < nbig; k++) c->hgbig_s[k] = c->hglist[c->hgbig[k]];
   HIPCHK(hipMemcpyAsync(c->glist.p, c->hglist.data(), 4ull * ng, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->gspb.p, c->hgspb.data(), 4ull * (ng + 1), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(c->gpbase.p, c->hgpbase.data(), 4ull * (ng + 1), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(c->gsbase.p, c->hgsbase.data(), 8ull * (ng + 1), hipMemcpyHostToDevice, st));
-  // the block counter, and (unless a later chunk of one host batch) the members finished
-  HIPCHK(hipMemsetAsync(c->gcnt.p, 0, c->keep_counts ? 4 : 8, st));
+  if (nbig) {
+    HIPCHK(c->gbigs.ensure(4ull * nbig));
+    HIPCHK(hipMemcpyAsync(c->gbigs.p, c->hgbig_s.data(), 4ull * nbig, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->gbig.p, c->hgbig.data(), 4ull * nbig, hipMemcpyHostToDevice, st));
+  }
+  // fresh records: members (span counters), entries (start 0 = none), spans (member NONE)
+  HIPCHK(hipMemsetAsync(c->gmem.p, 0, sizeof(zs_seg_mem) * ng, st));
+  HIPCHK(hipMemsetAsync(c->gent.p, 0, sizeof(zs_seg_ent) * ZS_SPLIT_MAX * ng, st));
+  HIPCHK(hipMemsetAsync(c->gblk.p, 0xff, sizeof(zs_seg_blk) * nb, st));
+  // the spans taken (the decode's work list), and (unless a later chunk of one host batch) the members finished
+  HIPCHK(c->gspl.ensure(4ull * nb + 4));
+  HIPCHK(c->gflist.ensure(4ull * ng));
+  HIPCHK(hipMemsetAsync(c->gcnt.as<uint32_t>() + 2, 0, 8, st));  // spans taken, members left over
+  if (!c->keep_counts) HIPCHK(hipMemsetAsync(c->gcnt.p, 0, 8, st));
   HIPCHK(hipEventRecord(c->fork, st));
   HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
   hipStream_t sd = c->side;
@@ -1089,43 +1120,54 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   zs_seg_blk* gb = c->gblk.as<zs_seg_blk>();
   zs_seg_lane* gln = c->glanes.as<zs_seg_lane>();
   zcode* gt = c->gtab.as<zcode>();
+  zs_seg_ent* ge = c->gent.as<zs_seg_ent>();
   zs_seg_mem* gm = c->gmem.as<zs_seg_mem>();
-  const uint32_t nb = (uint32_t)cap_blocks;
-  zs_k_split_find<<<ng * ZS_SPLIT_MAX, 256, 0, sd>>>(d_in, d_ioff, d_ilen, gl, wbits, gf);
-  zs_k_seg_alloc<<<ng, 64, 0, sd>>>(gf, ng, c->gcidx.as<uint32_t>(), gb, cnt, nb, gm);
-  if (int r = mark(c, sd, "seg_find")) return r;
+  const uint32_t* gspb = c->gspb.as<uint32_t>();
+  if (nbig) {
+    zs_k_split_find<<<nbig * ZS_SPLIT_MAX, 256, 0, sd>>>(d_in, d_ioff, d_ilen, c->gbigs.as<uint32_t>(), wbits, gf);
+    if (int r = mark(c, sd, "seg_find")) return r;
+  }
+  const uint32_t nwalk = ng + nbig * (ZS_SPLIT_MAX - 1u);
   if (d64)
-    zs_k_seg_sync<true><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, wbits, gf, cnt, gb, gln, gt, c->seg_bits);
+    zs_k_seg_walk<true><<<nwalk, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, ng, c->gbig.as<uint32_t>(), nbig, wbits, gf,
+                                              gspb, gb, gln, gt, ge, gm, cnt + 2, c->gspl.as<uint32_t>(), c->seg_bits);
   else
-    zs_k_seg_sync<false><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, wbits, gf, cnt, gb, gln, gt, c->seg_bits);
-  if (int r = mark(c, sd, "seg_sync")) return r;
-  zs_k_seg_plan<<<ng, 64, 0, sd>>>(d_in, d_ioff, d_ilen, d_ocap, gl, ng, wbits, refw ? 1 : 0,
-                                   c->gcidx.as<uint32_t>(), gb, gln, gm, c->gpbase.as<uint32_t>(),
-                                   c->gplist.as<uint4>());
+    zs_k_seg_walk<false><<<nwalk, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, ng, c->gbig.as<uint32_t>(), nbig, wbits, gf,
+                                               gspb, gb, gln, gt, ge, gm, cnt + 2, c->gspl.as<uint32_t>(), c->seg_bits);
+  if (int r = mark(c, sd, "seg_walk")) return r;
+  zs_k_seg_plan<<<ng, 64, 0, sd>>>(d_in, d_ioff, d_ilen, d_ocap, gl, ng, wbits, refw ? 1 : 0, gb, gln, ge, gm,
+                                   c->gpbase.as<uint32_t>(), c->gplist.as<uint4>());
   if (int r = mark(c, sd, "seg_plan")) return r;
   const uint64_t* sb = c->gsbase.as<uint64_t>();
   uint16_t* scr = c->gscr.as<uint16_t>();
+  // one wave per span taken, grid-stride over the work list
+  const uint32_t gdec = std::min<uint32_t>(nb, 8192u);
+  const uint32_t* spl = c->gspl.as<uint32_t>();
   if (d64)
-    zs_k_seg_decode<true, false><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt, gb, gln, gt, gm, sb, scr);
+    zs_k_seg_decode<true, false><<<gdec, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt + 2, spl, gb, gln, gt, gm, sb, scr);
   else if (refw)
-    zs_k_seg_decode<false, true><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt, gb, gln, gt, gm, sb, scr);
+    zs_k_seg_decode<false, true><<<gdec, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt + 2, spl, gb, gln, gt, gm, sb, scr);
   else
-    zs_k_seg_decode<false, false><<<nb, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt, gb, gln, gt, gm, sb, scr);
+    zs_k_seg_decode<false, false><<<gdec, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt + 2, spl, gb, gln, gt, gm, sb, scr);
   if (int r = mark(c, sd, "seg_decode")) return r;
   HIPCHK(hipFuncSetAttribute((const void*)zs_k_seg_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
   zs_k_seg_resolve<<<ng, 512, 65536, sd>>>(gl, gm, c->gpbase.as<uint32_t>(), c->gplist.as<uint4>(), sb, scr, d_out,
-                                           d_ooff, lres, c->llen.as<uint32_t>(), cnt + 1);
+                                           d_ooff, lres, c->llen.as<uint32_t>(), cnt + 1, cnt + 3,
+                                           c->gflist.as<uint32_t>());
   if (int r = mark(c, sd, "seg_resolve")) return r;
   // members the pieces could not finish: the wave kernel (skip_done), then the exact kernel
   const size_t wsm = zs_inflate_wave_lds_bytes(d64);
   const void* wk = refw ? (const void*)zs_k_inflate_wave<true> : (const void*)zs_k_inflate_wave<false>;
   HIPCHK(hipFuncSetAttribute(wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wsm));
+  // (the members the resolve listed: usually none, so a small grid walks the list)
+  const uint32_t gfb = std::min<uint32_t>(ng, 256u);
+  const uint32_t* fl = c->gflist.as<uint32_t>();
   if (refw)
-    zs_k_inflate_wave<true><<<ng, 64, wsm, sd>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, gl, ng, lres,
-                                                 c->llen.as<uint32_t>(), 1u);
+    zs_k_inflate_wave<true><<<gfb, 64, wsm, sd>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, fl, ng, lres,
+                                                  c->llen.as<uint32_t>(), cnt + 3);
   else
-    zs_k_inflate_wave<false><<<ng, 64, wsm, sd>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, gl, ng, lres,
-                                                  c->llen.as<uint32_t>(), 1u);
+    zs_k_inflate_wave<false><<<gfb, 64, wsm, sd>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits, fl, ng, lres,
+                                                   c->llen.as<uint32_t>(), cnt + 3);
   HIPCHK(hipGetLastError());
   if (int r = mark(c, sd, "seg_fallback")) return r;
   (void)n;
@@ -1228,7 +1270,9 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       constexpr uint32_t kPieceCapMax = 4u << 20;  // values per piece
       for (uint32_t i = 0; i < n; i++) {
         if (in_len[i] <= big_min) continue;
-        if (c->inflate_seg && in_len[i] < (1u << 29)) {  // (bit positions in 32 bits)
+        // (the segmented decode keeps bit positions in 32 bits; members with long
+        // blocks of long copies -- deflate64 -- decode faster split, with a wave per block)
+        if (c->inflate_seg && in_len[i] < (1u << 29) && !(splittable && wbits == -16 && 8ull * in_len[i] > ZS_SEG_SPLIT_BITS)) {
           c->hglist.push_back(i);
           continue;
         }
@@ -1250,9 +1294,9 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       const int r = seg_launch(c, st, wbits, n, d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, in_len, out_cap, lres);
       if (r != ZS_OK) return r;
       // (the join below waits for the side stream's last kernel)
-      if (c->hslist.empty() && c->hwlist.empty()) HIPCHK(hipEventRecord(c->join, c->side));
+      if (c->hwlist.empty()) HIPCHK(hipEventRecord(c->join, c->side));
     }
-    if (!c->hslist.empty()) {
+    if (!c->hslist.empty()) {  // on the third stream, beside the segmented decode
       const uint32_t ns = (uint32_t)c->hslist.size();
       HIPCHK(c->slist.ensure(4ull * ns));
       HIPCHK(c->sfound.ensure(8ull * ZS_SPLIT_MAX * ns));
@@ -1260,32 +1304,32 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       HIPCHK(c->sscr.ensure(2ull * ZS_SPLIT_MAX * piece_cap * ns));
       HIPCHK(hipMemcpyAsync(c->slist.p, c->hslist.data(), 4ull * ns, hipMemcpyHostToDevice, st));
       HIPCHK(hipEventRecord(c->fork, st));
-      HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
-      if (int r = mark(c, c->side, "start")) return r;
+      HIPCHK(hipStreamWaitEvent(c->side2, c->fork, 0));
+      if (int r = mark(c, c->side2, "start")) return r;
       const uint32_t* sl = c->slist.as<uint32_t>();
       uint64_t* sf = c->sfound.as<uint64_t>();
       zs_split_piece_res* sp = c->spres.as<zs_split_piece_res>();
-      zs_k_split_find<<<ns * ZS_SPLIT_MAX, 256, 0, c->side>>>(d_in, d_ioff, d_ilen, sl, wbits, sf);
-      if (int r = mark(c, c->side, "split_find")) return r;
+      zs_k_split_find<<<ns * ZS_SPLIT_MAX, 256, 0, c->side2>>>(d_in, d_ioff, d_ilen, sl, wbits, sf);
+      if (int r = mark(c, c->side2, "split_find")) return r;
       const size_t ssm = zs_split_lds_bytes(wbits == -16);
       HIPCHK(hipFuncSetAttribute((const void*)zs_k_split_decode, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ssm));
-      zs_k_split_decode<<<ns * ZS_SPLIT_MAX, 64, ssm, c->side>>>(d_in, d_ioff, d_ilen, sl, wbits, sf, sp,
+      zs_k_split_decode<<<ns * ZS_SPLIT_MAX, 64, ssm, c->side2>>>(d_in, d_ioff, d_ilen, sl, wbits, sf, sp,
                                                                   c->sscr.as<uint16_t>(), piece_cap);
-      if (int r = mark(c, c->side, "split_decode")) return r;
+      if (int r = mark(c, c->side2, "split_decode")) return r;
       HIPCHK(c->smem.ensure(sizeof(zs_split_member) * ns));
       HIPCHK(c->sval.ensure(4ull * val_stride * ns + 16));
       zs_split_member* sm = c->smem.as<zs_split_member>();
       uint32_t* sv = c->sval.as<uint32_t>();
-      zs_k_split_chain<<<(ns + 63) / 64, 64, 0, c->side>>>(d_ilen, d_ocap, sl, ns, sp, sm);
-      zs_k_split_place<<<ns * ZS_SPLIT_MAX, 256, 0, c->side>>>(sp, sm, c->sscr.as<uint16_t>(), piece_cap, sv, val_stride);
+      zs_k_split_chain<<<(ns + 63) / 64, 64, 0, c->side2>>>(d_ilen, d_ocap, sl, ns, sp, sm);
+      zs_k_split_place<<<ns * ZS_SPLIT_MAX, 256, 0, c->side2>>>(sp, sm, c->sscr.as<uint16_t>(), piece_cap, sv, val_stride);
       // the jump and write grids cover the largest member (grid-stride beyond)
       const uint32_t gx = (uint32_t)std::min<uint64_t>(1024, (val_stride + 1023) / 1024);
-      for (int k = 0; k < 6; k++) zs_k_split_jump<<<dim3(gx, ns), 256, 0, c->side>>>(sm, sv, val_stride);
-      zs_k_split_write<<<dim3(gx, ns), 256, 0, c->side>>>(sl, sm, sv, val_stride, d_out, d_ooff);
-      zs_k_split_final<<<(ns + 63) / 64, 64, 0, c->side>>>(sl, ns, sm, lres, c->llen.as<uint32_t>());
+      for (int k = 0; k < 6; k++) zs_k_split_jump<<<dim3(gx, ns), 256, 0, c->side2>>>(sm, sv, val_stride);
+      zs_k_split_write<<<dim3(gx, ns), 256, 0, c->side2>>>(sl, sm, sv, val_stride, d_out, d_ooff);
+      zs_k_split_final<<<(ns + 63) / 64, 64, 0, c->side2>>>(sl, ns, sm, lres, c->llen.as<uint32_t>());
       HIPCHK(hipGetLastError());
-      if (int r = mark(c, c->side, "split_resolve")) return r;
-      if (c->hwlist.empty()) HIPCHK(hipEventRecord(c->join, c->side));
+      if (int r = mark(c, c->side2, "split_resolve")) return r;
+      HIPCHK(hipEventRecord(c->join2, c->side2));
     }
     if (!c->hwlist.empty()) {
       const uint32_t nw = (uint32_t)c->hwlist.size();
@@ -1323,10 +1367,12 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
               c->llen.as<uint32_t>(), ZS_INF_REF_WRAP, 0u, c->wlist.as<uint32_t>());
       } else if (refw)
         zs_k_inflate_wave<true><<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
-                                                          c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>(), 0u);
+                                                          c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>(),
+                                                          nullptr);
       else
         zs_k_inflate_wave<false><<<nw, 64, wsm, c->side>>>(d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, wbits,
-                                                           c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>(), 0u);
+                                                           c->wlist.as<uint32_t>(), nw, lres, c->llen.as<uint32_t>(),
+                                                          nullptr);
       HIPCHK(hipGetLastError());
       if (int r = mark(c, c->side, lanes ? "inflate_large" : "inflate_wave")) return r;
       HIPCHK(hipEventRecord(c->join, c->side));
@@ -1365,8 +1411,9 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       MARK("inflate_long");
     }
     if (wave_min) {
-      HIPCHK(hipStreamWaitEvent(st, c->join, 0));
-      MARK("inflate_join");  // the caller's stream waiting for the wave kernel beyond the lane kernel
+      if (!c->hglist.empty() || !c->hwlist.empty()) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
+      if (!c->hslist.empty()) HIPCHK(hipStreamWaitEvent(st, c->join2, 0));
+      MARK("inflate_join");  // the caller's stream waiting for the side streams beyond the lane kernel
     }
     if (wbits > 0) {  // trailer checks over the decoded bytes: adler32 (zlib) / crc32 (gzip)
       uint32_t* chk = c->llen.as<uint32_t>() + n;

@@ -4,7 +4,6 @@
 // shards of the 8-GPU configs (512 x 256 KiB, 1,024 x 64 KiB).
 //
 // A member's decode is one serial chain of Huffman lookups; three facts cut it:
-//  * block starts can be found by testing every bit offset (zs_k_split_find);
 //  * inside a block, Huffman decoding started at an arbitrary bit falls into
 //    step with the true symbol stream after a few symbols (median 100 bits,
 //    max ~1,750 over 7,800 trials on the benchmark corpora): a lane decoding
@@ -12,7 +11,9 @@
 //    start that lane also visited -- from there both are the true stream;
 //  * a copy reaching back before a piece's start can be written as a MARKER
 //    (u16 255 + k: "the value k positions before the piece"), propagated by
-//    later copies like a byte, and resolved once the earlier pieces are known.
+//    later copies like a byte, and resolved once the earlier pieces are known;
+//  * for members too long for one walk, block starts can be found by testing
+//    every bit offset (zs_k_split_find), and walks started there.
 // The reference's window-wrap copy (inffast.ts:127-147, reproduced by default)
 // depends on its inflate() call boundaries (32 KiB input sub-chunks, 64 KiB
 // output buffers, streams.ts:78-93): they move only at "events" -- the first
@@ -23,17 +24,21 @@
 // bookkeeping (zs_refcalls) from its start.
 //
 // Kernels, each over the whole batch:
-//  zs_k_split_find  candidate block starts (inflate_split.hip), one per bit range
-//  zs_k_seg_alloc   compact indices for the candidates
-//  zs_k_seg_sync    one wave per candidate block: the header and tables, then
-//                   lane j decodes from bit sym0 + j S, recording the symbol
-//                   starts of its first ZS_SEG_W bits; it stops at the first
-//                   of its positions (past the next lane's start) that the next
-//                   lane recorded.  Output counts, crossing events, the block's end.
-//  zs_k_seg_plan    one wave per member: blocks chained by their ends, pieces
-//                   placed (prefix sum), trailer and capacity checked, call state
-//                   per piece (REFW)
-//  zs_k_seg_decode  one wave per block: each lane decodes its piece into u16
+//  zs_k_split_find  (members over ZS_SEG_BIG_BITS only) candidate block starts,
+//                   one per bit range (inflate_split.hip)
+//  zs_k_seg_walk    one wave per entry (a member's start; a big member's found
+//                   block starts): block after block, header and tables, then
+//                   spans of 64 lanes, lane j decoding from bit sym0 + j S and
+//                   recording the symbol starts of its first ZS_SEG_W bits; it
+//                   stops at the first of its positions (past the next lane's
+//                   start) that the next lane recorded.  Output counts,
+//                   crossing events, the span's end (end of block, or the next
+//                   span's start); the walk stops at the final block or at a
+//                   later entry's start.
+//  zs_k_seg_plan    one wave per member: entries chained by their ends, the
+//                   pieces placed (prefix sum), trailer and capacity checked,
+//                   call state per piece (REFW)
+//  zs_k_seg_decode  one wave per span: each lane decodes its piece into u16
 //                   values (bytes or markers) with the window-wrap copy replayed
 //  zs_k_seg_resolve one workgroup per member: pieces in order, markers looked up
 //                   in the bytes already final (a 64 KiB LDS ring), bytes written
@@ -48,36 +53,6 @@
 #include "zs_wave.h"
 #include "zs_refcalls.h"
 #include "zs_seg.h"
-
-// ------------------------------------------------------------------ alloc
-// One wave per member, lane r = the finder's range r: the member's candidates
-// get consecutive block indices from a global counter (the order of members is
-// free); a member whose blocks do not fit is marked bad.
-__global__ __launch_bounds__(64) void zs_k_seg_alloc(const uint64_t* __restrict__ found, uint32_t n_list,
-                                                     uint32_t* __restrict__ cidx, zs_seg_blk* __restrict__ blk,
-                                                     uint32_t* __restrict__ counter, uint32_t cap_blocks,
-                                                     zs_seg_mem* __restrict__ mem) {
-  const uint32_t m = blockIdx.x, r = threadIdx.x;
-  if (m >= n_list) return;
-  const bool cand = found[m * ZS_SPLIT_MAX + r] != ~0ull;
-  const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
-  const uint32_t cnt = (uint32_t)__builtin_popcountll(bal);
-  uint32_t base = 0;
-  if (r == 0) base = atomicAdd(counter, cnt);
-  base = (uint32_t)__shfl(base, 0);
-  const uint32_t idx = base + (uint32_t)__builtin_popcountll(bal & ((1ull << r) - 1ull));
-  const bool fits = base + cnt <= cap_blocks;
-  cidx[m * ZS_SPLIT_MAX + r] = cand && fits ? idx : ZS_SEG_NONE;
-  if (cand && idx < cap_blocks) {
-    blk[idx].m = fits ? m : ZS_SEG_NONE;
-    blk[idx].r = r;
-    blk[idx].flags = 0;
-  }
-  if (r == 0) {
-    zs_seg_mem z = {fits ? 0u : 1u, 0u, 0u, 0u, 0u, {0u, 0u, 0u}};
-    mem[m] = z;
-  }
-}
 
 // ------------------------------------------------------------- lane reader
 // One lane's bit reader (the lane kernel's scheme: clamped aligned words, one
@@ -244,334 +219,289 @@ static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* l
   return true;
 }
 
-// ------------------------------------------------------------------- sync
-struct zs_sg_sync_lds {
+// ------------------------------------------------------------------- walk
+// One wave per ENTRY: entry 0 of every member is its first bit; a member with
+// more than ZS_SEG_BIG_BITS input bits also has the block starts the finder
+// found (zs_k_split_find, one per bit range) as entries 1 ..  An entry's wave
+// walks the blocks from its start in order -- header and tables, then the
+// block's symbols in SPANS of 64 lanes, lane j decoding from sym0 + j S -- until
+// a block ends at a later entry's start (the plan links them there) or the final
+// block ends.  Within a span, lane j records the symbol starts of the first
+// ZS_SEG_W bits of its range and stops at the first of its positions, past the
+// next lane's start, that the next lane recorded: from there both decode the
+// true stream (the lane before is confirmed, so is it).  The span ends at the
+// end-of-block code of a confirmed lane, or -- its last lane confirmed past the
+// span's nominal end -- at a symbol start, where the next span continues.
+struct zs_sg_walk_lds {
   uint32_t inw[ZS_WIN_IN];
   zcode codes[ZS_SEG_TAB];
   uint16_t lens[320];
   uint16_t work[288];
-  uint32_t bm[ZS_SEG_LANES][ZS_SEG_W / 32];  // each lane's visited symbol starts in its window
-  uint32_t ckp[ZS_SEG_LANES][ZS_SEG_NCK];    // checkpoints: a visited position per 128-bit bucket ...
-  uint32_t ckc[ZS_SEG_LANES][ZS_SEG_NCK];    // ... and the lane's output count there
-  uint32_t prog[ZS_SEG_LANES];   // a lane's current position (ZS_SEG_NONE once stopped)
-  uint32_t conf[ZS_SEG_LANES];   // on the true chain (lane 0, or synced into by a confirmed lane)
-  uint32_t absorbed[ZS_SEG_LANES];
-  uint32_t kind[ZS_SEG_LANES], to[ZS_SEG_LANES], onchain[ZS_SEG_LANES];
-  unsigned long long from[ZS_SEG_LANES];  // (lane << 32 | bit) of the lane that synced into it (the lowest lane wins)
-  uint32_t done, ok, bend;
+  uint32_t own[ZS_SEG_LANES][ZS_SEG_W / 32];   // each lane's symbol starts in [q, q + W)
+  uint32_t tail[ZS_SEG_LANES][ZS_SEG_W / 32];  // ... and in [q + S, q + S + W): the next lane's window
+  uint32_t okp[ZS_SEG_LANES][ZS_SEG_NCK], okc[ZS_SEG_LANES][ZS_SEG_NCK];  // checkpoints (position, count) in each
+  uint32_t tkp[ZS_SEG_LANES][ZS_SEG_NCK], tkc[ZS_SEG_LANES][ZS_SEG_NCK];
+  uint32_t sync[ZS_SEG_LANES];  // lane j's start on the true stream: the first start it shares with lane j - 1
+  uint32_t send;
 };
-#define ZS_SG_K_NONE 0u
-#define ZS_SG_K_SYNC 1u
-#define ZS_SG_K_BEND 2u
-#define ZS_SG_K_STOP 3u
 
-// one wave per candidate block
+// One span of a block whose tables are in L.codes: lanes j < nl decode from
+// q_j = sym0 + j S; pe0 is the end of the symbol before sym0 (sub-chunk events).
+//  1. every lane decodes on its own -- no barrier, no exchange -- from q_j to
+//     the first symbol start at or past q_{j+1} + W (the last lane: past the
+//     span's nominal end, or to the input's end when the span reaches it),
+//     recording its symbol starts in [q_j, q_j + W) and in [q_{j+1}, q_{j+1} + W),
+//     with checkpoints of its output count, its end-of-block / invalid codes
+//     and its sub-chunk crossings;
+//  2. lane j's true start is the first symbol start lane j - 1 recorded in
+//     [q_j, q_j + W) that lane j recorded too (lane 0 starts on the true stream,
+//     so by induction each lane from its start does);
+//  3. the chain is lanes 0 .. J - 1 (J: the first lane without a shared start);
+//     the first of them whose piece holds an end-of-block code ends the block
+//     there (BEND); else the span ends at the last chain lane's stop, a true
+//     symbol start where the next span continues (CONT) -- past the nominal end,
+//     or, the chain broken at J, past q_J + W.
+// Writes the span's lane records; returns BEND / CONT, or NONE for a span that
+// cannot go on (past the input without an end of block).
+#define ZS_SG_K_NONE 0u
+#define ZS_SG_K_BEND 2u
+#define ZS_SG_K_CONT 4u
 template <bool D64>
-__global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                                                    const uint32_t* __restrict__ in_len,
-                                                    const uint32_t* __restrict__ list, int wbits,
-                                                    const uint64_t* __restrict__ found,
-                                                    const uint32_t* __restrict__ counter, zs_seg_blk* __restrict__ blk,
-                                                    zs_seg_lane* __restrict__ lanes, zcode* __restrict__ tcache,
-                                                    uint32_t smin) {
-  __shared__ zs_sg_sync_lds L;
-  volatile zs_sg_sync_lds& V = L;
-  const uint32_t b = blockIdx.x, lane = threadIdx.x;
-  if (b >= *counter) return;
-  zs_seg_blk& Bk = blk[b];
-  const uint32_t m = zs_u(Bk.m), r = zs_u(Bk.r);
-  if (m == ZS_SEG_NONE) return;
-  const uint32_t s = zs_u(list[m]);
-  const uint32_t n = zs_u(in_len[s]);
+static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uint32_t n, uint32_t sym0, uint32_t pe0,
+                                      uint32_t nl, uint32_t S, uint32_t lbits, uint32_t dbits, uint32_t dofs,
+                                      zs_seg_lane* __restrict__ recs, uint32_t& send, bool& bad_out) {
+  const uint32_t lane = threadIdx.x;
   const uint32_t nbits = 8u * n;
-  const uint32_t f = (uint32_t)found[m * ZS_SPLIT_MAX + r];
-  // the nominal end: the next candidate's start
-  uint32_t nend = nbits;
-  {
-    const uint64_t fx = found[m * ZS_SPLIT_MAX + lane];
-    const uint64_t later = __builtin_amdgcn_ballot_w64(lane > r && fx != ~0ull);
-    if (later) nend = (uint32_t)found[m * ZS_SPLIT_MAX + (uint32_t)__builtin_ctzll(later)];
-    nend = zs_u(nend);
-  }
-  const uint8_t* src = in + in_off[s];
-  // ---- header (wave-uniform)
-  zs_wave_reader R;
-  R.n = n;
-  R.sh = (uint32_t)((uintptr_t)src & 3u);
-  R.w4 = reinterpret_cast<const uint32_t*>(src - R.sh);
-  R.last = (R.sh + n - 1u) >> 2;
-  R.inw = L.inw;
-  zs_wr_stage(R, ((f >> 3) + R.sh) >> 2);
-  zs_wr_seek(R, f >> 3);
-  zs_wr_take(R, f & 7u);
-  bool good = true;
-  const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
-  if (r == 0 && wrap) {  // plain zlib / gzip headers only (inflate.ts:377-580), as the lane path
-    const uint32_t b0 = zs_wr_take(R, 8), b1 = zs_wr_take(R, 8);
-    if ((wrap & 2) && b0 == 0x1f && b1 == 0x8b) {
-      const uint32_t cm = zs_wr_take(R, 8), flg = zs_wr_take(R, 8);
-      zs_wr_take(R, 32);
-      zs_wr_take(R, 16);
-      good = cm == 8 && flg == 0;
-    } else if (wrap & 1) {
-      good = !(((b0 << 8) | b1) % 31 || (b0 & 15) != 8 || (b0 >> 4) + 8 > 15 || (b1 & 0x20));
-    } else {
-      good = false;
-    }
-  }
-  const uint32_t hdr = (uint32_t)zs_wr_bitpos(R);
-  uint32_t last = 0, lbits = 0, dbits = 0, dofs = 0, ntab = 0;
-  if (good) good = zs_sg_header(R, L.codes, L.lens, L.work, D64, last, lbits, dbits, dofs, ntab);
-  const uint32_t sym0 = (uint32_t)zs_wr_bitpos(R);
-  if (good && sym0 > nbits) good = false;
-  if (!good) {
-    if (lane == 0) Bk.flags = 0;
-    return;
-  }
-  for (uint32_t i = lane; i < ntab; i += 64) tcache[(size_t)b * ZS_SEG_TAB + i] = L.codes[i];
-  const uint32_t payload = nend > sym0 ? nend - sym0 : 0u;
-  const uint32_t nl = max(1u, min(ZS_SEG_LANES, payload / smin));
-  const uint32_t S = max(1u, (payload + nl - 1u) / nl);
+  const uint32_t nend = sym0 + nl * S;  // the nominal end
+  const bool cont_ok = nend < nbits;    // (else the block must end in this span)
   const uint32_t lmask = (1u << lbits) - 1u, dmask = (1u << dbits) - 1u, emask = D64 ? 31u : 15u;
   const zcode* lt = L.codes;
   const zcode* dt = L.codes + dofs;
-
-  // ---- lanes: lane j decodes from q = sym0 + j S
   const bool on = lane < nl;
-  const uint32_t q = sym0 + lane * S;
-  for (uint32_t i = 0; i < ZS_SEG_W / 32; i++) L.bm[lane][i] = 0;
-  for (uint32_t i = 0; i < ZS_SEG_NCK; i++) L.ckp[lane][i] = ZS_SEG_NONE;
-  L.prog[lane] = on ? q : ZS_SEG_NONE;
-  L.conf[lane] = lane == 0;
-  L.absorbed[lane] = 0;
-  L.from[lane] = ~0ull;
-  L.kind[lane] = ZS_SG_K_NONE;
-  L.onchain[lane] = 0;
-  if (lane == 0) {
-    L.done = 0;
-    L.ok = 0;
-    L.bend = 0;
+  const bool lastl = lane + 1u == nl;
+  const uint32_t q = sym0 + lane * S, qn = q + S;
+  const uint32_t lim = !on ? q : !lastl ? qn + ZS_SEG_W : cont_ok ? nend : nbits + 64u;
+  for (uint32_t i = 0; i < ZS_SEG_W / 32; i++) {
+    L.own[lane][i] = 0;
+    L.tail[lane][i] = 0;
   }
+  for (uint32_t i = 0; i < ZS_SEG_NCK; i++) {
+    L.okp[lane][i] = ZS_SEG_NONE;
+    L.tkp[lane][i] = ZS_SEG_NONE;
+  }
+  // ---- 1. the lane's own decode
   zs_sg_reader G;
   zs_sg_init(G, src, n);
   if (on) zs_sg_seek(G, q);
-  uint32_t pos = q, cum = 0, nck = 0, nxt = lane + 1, to = ZS_SEG_NONE, end = 0, last_len = 0;
-  uint32_t pe = lane == 0 ? (r == 0 ? 0u : f) : q;  // the end of the symbol before (events)
+  uint32_t pos = q, cum = 0, last_len = 0;
+  uint32_t pe = lane == 0 ? pe0 : q;  // the end of the symbol before (events)
   uint32_t nev = 0, ev_k[ZS_SEG_NEV], ev_sb[ZS_SEG_NEV], ev_c[ZS_SEG_NEV];
-  // End-of-block codes and invalid codes met: those in the lane's window (where
-  // its garbage before the sync point is) in rings of the last ZS_SEG_NEOB, and
-  // the first one past the window (always in the true stream, or past the end).
+  // end-of-block and invalid codes: those in [q, q + W) (where the garbage before
+  // the lane's true start is) in rings of the last ZS_SEG_NEOB, and the first one
+  // past it (in the true stream once the lane is on the chain)
   uint32_t neob = 0, eob_sb[ZS_SEG_NEOB], eob_end[ZS_SEG_NEOB], eob_cum[ZS_SEG_NEOB];
   uint32_t xeob_sb = ZS_SEG_NONE, xeob_end = 0, xeob_cum = 0;
   uint32_t nbad = 0, bad_sb[ZS_SEG_NEOB], xbad = ZS_SEG_NONE;
-  uint32_t cum_end = 0;
 #pragma unroll
   for (uint32_t e = 0; e < ZS_SEG_NEV; e++) ev_k[e] = ev_sb[e] = ev_c[e] = 0;
 #pragma unroll
   for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) eob_sb[e] = eob_end[e] = eob_cum[e] = bad_sb[e] = 0;
-  bool act = on;
-  uint32_t kind = ZS_SG_K_NONE;
-  // (a safety net: every iteration but a stalled one moves a lane on by a bit)
-  const uint32_t max_iter = 2u * (nbits + 64u - sym0) + 4096u;
-  for (uint32_t iter = 0;; iter++) {
-    if (!__syncthreads_or(act) || V.done) break;
-    if (iter > max_iter) {
-      act = false;  // (the block is then not OK)
-      kind = ZS_SG_K_STOP;
+  uint32_t ock = 0, tck = 0;  // checkpoint buckets filled
+  // the bitmaps' current word (own words 0 .., tail words ZS_SEG_W / 32 ..) collects
+  // in a register: positions only grow, so each word is stored once
+  constexpr uint32_t NW = ZS_SEG_W / 32u;
+  uint32_t aw = ZS_SEG_NONE, acc = 0;
+  auto put_word = [&]() {
+    if (aw < NW) L.own[lane][aw] = acc;
+    else if (aw != ZS_SEG_NONE) L.tail[lane][aw - NW] = acc;
+  };
+  auto mark = [&](uint32_t w, uint32_t bit) {
+    if (w != aw) {
+      put_word();
+      aw = w;
+      acc = 0;
+    }
+    acc |= 1u << bit;
+  };
+  while (pos < lim) {
+    const uint32_t off = pos - q, toff = pos - qn;
+    if (off < ZS_SEG_W) {
+      mark(off >> 5, off & 31u);
+      if (off >= ock * ZS_SEG_CKB) {
+        L.okp[lane][off / ZS_SEG_CKB] = pos;
+        L.okc[lane][off / ZS_SEG_CKB] = cum;
+        ock = off / ZS_SEG_CKB + 1u;
+      }
+    } else if (toff < ZS_SEG_W) {
+      mark(NW + (toff >> 5), toff & 31u);
+      if (toff >= tck * ZS_SEG_CKB) {
+        L.tkp[lane][toff / ZS_SEG_CKB] = pos;
+        L.tkc[lane][toff / ZS_SEG_CKB] = cum;
+        tck = toff / ZS_SEG_CKB + 1u;
+      }
+    }
+    const uint32_t sb = pos;
+    const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
+    if (y.kind == ZS_SG_BAD) {
+      if (sb - q < ZS_SEG_W) {
+#pragma unroll
+        for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
+          if (e == (nbad & (ZS_SEG_NEOB - 1u))) bad_sb[e] = sb;
+        nbad++;
+      } else if (xbad == ZS_SEG_NONE) {
+        xbad = sb;
+      }
+      pos = sb + 1u;
+      zs_sg_seek(G, pos);
+      pe = pos;
+      last_len = 0;
       continue;
     }
-    if (act && V.absorbed[lane]) {  // the lane before went past this one's window: not on the chain
-      act = false;
-      kind = ZS_SG_K_STOP;
-      V.prog[lane] = ZS_SEG_NONE;
-    }
-    // confirmation travels down the chain one lane per iteration, through lanes
-    // that have stopped already too
-    if (on && !V.conf[lane]) {
-      const unsigned long long fr = V.from[lane];
-      if (fr != ~0ull && V.conf[(uint32_t)(fr >> 32)]) V.conf[lane] = 1;
-    }
-    const bool cf = act && V.conf[lane];
-    // a confirmed lane ends the block at its first end-of-block code at or past
-    // its start (it may have decoded on past it, waiting to be confirmed)
-    if (cf && (neob || xeob_sb != ZS_SEG_NONE)) {
-      const uint32_t st = lane == 0 ? sym0 : (uint32_t)V.from[lane];
-      uint32_t hs = ZS_SEG_NONE;
+    const uint32_t se = zs_sg_bitpos(G);
+    // sub-chunk crossing events: boundaries 262144 k (k >= 1) with pe <= b < se
+    uint32_t bd = (pe + 262143u) & ~262143u;
+    if (bd == 0) bd = 262144u;
+    while (bd < se) {
 #pragma unroll
-      for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
-        if (e < neob && eob_sb[e] >= st && eob_sb[e] < hs) {
-          hs = eob_sb[e];
-          end = eob_end[e];
-          cum_end = eob_cum[e];
+      for (uint32_t e = 0; e < ZS_SEG_NEV; e++)
+        if (e == nev) {
+          ev_k[e] = bd >> 18;
+          ev_sb[e] = sb;
+          ev_c[e] = cum;
         }
-      if (hs == ZS_SEG_NONE && xeob_sb != ZS_SEG_NONE) {
-        hs = xeob_sb;
-        end = xeob_end;
-        cum_end = xeob_cum;
-      }
-      if (hs != ZS_SEG_NONE) {
-        act = false;
-        kind = ZS_SG_K_BEND;
-        V.prog[lane] = ZS_SEG_NONE;
-        V.done = 1;
-      }
+      nev++;
+      bd += 262144u;
     }
-    // past the input (the garbage after a block's end): a confirmed lane has lost
-    // the chain; an unconfirmed one waits to be confirmed (its end of block is
-    // logged) or absorbed
-    bool stall = act && pos >= nbits + 64u;
-    if (stall && cf) {
-      act = false;
-      kind = ZS_SG_K_STOP;
-      V.prog[lane] = ZS_SEG_NONE;
-      V.done = 1;
-    }
-    if (act && !stall) {
-      const uint32_t off = pos - q;
-      if (off < ZS_SEG_W) {
-        V.bm[lane][off >> 5] |= 1u << (off & 31u);
-        if (off >= nck * ZS_SEG_CKB) {
-          V.ckp[lane][off / ZS_SEG_CKB] = pos;
-          V.ckc[lane][off / ZS_SEG_CKB] = cum;
-          nck = off / ZS_SEG_CKB + 1u;
-        }
-      }
-      V.prog[lane] = pos;
-      if (nxt < nl && pos >= sym0 + nxt * S) {
-        if (pos >= sym0 + nxt * S + ZS_SEG_W) {
-          // no symbol start in common within the next lane's window: only a
-          // confirmed lane takes the next range over (an unconfirmed one waits to
-          // be confirmed or absorbed)
-          if (!cf) {
-            stall = true;
-          } else {
-            do {
-              V.absorbed[nxt] = 1;
-              nxt++;
-            } while (nxt < nl && pos >= sym0 + nxt * S + ZS_SEG_W);
+    if (y.kind == ZS_SG_EOB) {
+      if (sb - q < ZS_SEG_W) {
+#pragma unroll
+        for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
+          if (e == (neob & (ZS_SEG_NEOB - 1u))) {
+            eob_sb[e] = sb;
+            eob_end[e] = se;
+            eob_cum[e] = cum;
           }
-        }
-        if (!stall && nxt < nl && pos >= sym0 + nxt * S) {
-          const uint32_t o2 = pos - (sym0 + nxt * S);
-          if (V.prog[nxt] < pos) {
-            stall = true;  // the next lane has not reached here yet
-          } else if ((V.bm[nxt][o2 >> 5] >> (o2 & 31u)) & 1u) {
-            atomicMin((unsigned long long*)&L.from[nxt], ((unsigned long long)lane << 32) | pos);
-            act = false;
-            kind = ZS_SG_K_SYNC;
-            to = nxt;
-            end = pos;
-            cum_end = cum;
-            V.prog[lane] = ZS_SEG_NONE;
-          }
-        }
+        neob = min(neob + 1u, 2u * ZS_SEG_NEOB);  // (a ring: the last ZS_SEG_NEOB)
+      } else if (xeob_sb == ZS_SEG_NONE) {
+        xeob_sb = sb;
+        xeob_end = se;
+        xeob_cum = cum;
       }
+      last_len = 0;
+    } else {
+      cum += y.len;
+      last_len = y.len;
     }
-    if (act && !stall) {
-      const uint32_t sb = pos;
-      const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
-      if (y.kind == ZS_SG_BAD) {
-        if (sb - q < ZS_SEG_W) {
-#pragma unroll
-          for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
-            if (e == (nbad & (ZS_SEG_NEOB - 1u))) bad_sb[e] = sb;
-          nbad++;
-        } else if (xbad == ZS_SEG_NONE) {
-          xbad = sb;
-        }
-        pos = sb + 1u;
-        zs_sg_seek(G, pos);
-        pe = pos;
-      } else {
-        const uint32_t se = zs_sg_bitpos(G);
-        // sub-chunk crossing events: boundaries 262144 k (k >= 1) with pe <= b < se
-        uint32_t bd = (pe + 262143u) & ~262143u;
-        if (bd == 0) bd = 262144u;
-        while (bd < se) {
-#pragma unroll
-          for (uint32_t e = 0; e < ZS_SEG_NEV; e++)
-            if (e == nev) {
-              ev_k[e] = bd >> 18;
-              ev_sb[e] = sb;
-              ev_c[e] = cum;
-            }
-          nev++;
-          bd += 262144u;
-        }
-        if (y.kind == ZS_SG_EOB) {
-          if (sb - q < ZS_SEG_W) {
-#pragma unroll
-            for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
-              if (e == (neob & (ZS_SEG_NEOB - 1u))) {
-                eob_sb[e] = sb;
-                eob_end[e] = se;
-                eob_cum[e] = cum;
-              }
-            neob = min(neob + 1u, 2u * ZS_SEG_NEOB);  // (a ring: the last ZS_SEG_NEOB)
-          } else if (xeob_sb == ZS_SEG_NONE) {
-            xeob_sb = sb;
-            xeob_end = se;
-            xeob_cum = cum;
-          }
-          last_len = 0;
-        } else {
-          cum += y.len;
-          last_len = y.len;
-        }
-        pe = se;
-        pos = se;
-      }
-    }
+    pe = se;
+    pos = se;
   }
-  L.kind[lane] = kind;
-  L.to[lane] = to;
+  put_word();
   __syncthreads();
-  // ---- the chain: lane 0 -> the lane it synced into -> ... -> the end of block
-  if (lane == 0) {
-    uint32_t cur = 0, ok = 0, guard = 0;
-    while (guard++ < ZS_SEG_LANES) {
-      L.onchain[cur] = 1;
-      if (L.kind[cur] == ZS_SG_K_BEND) {
-        ok = 1;
+  // ---- 2. each lane's true start: the first start in its window lane - 1 shares
+  uint32_t sp = lane == 0 ? sym0 : ZS_SEG_NONE;
+  if (on && lane) {
+    for (uint32_t i = 0; i < ZS_SEG_W / 32; i++) {
+      const uint32_t x = L.tail[lane - 1u][i] & L.own[lane][i];
+      if (x) {
+        sp = q + 32u * i + (uint32_t)__builtin_ctz(x);
         break;
       }
-      if (L.kind[cur] != ZS_SG_K_SYNC) break;
-      const uint32_t nx = L.to[cur];
-      if ((uint32_t)(L.from[nx] >> 32) != cur) break;
-      cur = nx;
     }
-    L.ok = ok;
   }
+  L.sync[lane] = sp;
   __syncthreads();
+  // ---- 3. the chain: lanes 0 .. J - 1
+  const uint64_t nos = __builtin_amdgcn_ballot_w64(on && sp == ZS_SEG_NONE);
+  const uint32_t J = nos ? (uint32_t)__builtin_ctzll(nos) : nl;
+  const bool chain = lane < J;
+  const uint32_t start = sp;
+  // the piece's end before any end of block: the next lane's start, or (the chain's
+  // last lane) its stop
+  const uint32_t nxs = lane + 1u < J ? L.sync[lane + 1u] : pos;
+  // the first end-of-block code at or past the start (the chain's lanes are on the true
+  // stream from there), if before the piece's end
+  uint32_t hs = ZS_SEG_NONE, eend = 0, ecum = 0;
+#pragma unroll
+  for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
+    if (e < neob && eob_sb[e] >= start && eob_sb[e] < hs) {
+      hs = eob_sb[e];
+      eend = eob_end[e];
+      ecum = eob_cum[e];
+    }
+  if (hs == ZS_SEG_NONE && xeob_sb != ZS_SEG_NONE) {
+    hs = xeob_sb;
+    eend = xeob_end;
+    ecum = xeob_cum;
+  }
+  const bool has_eob = chain && hs < nxs;
+  const uint64_t eobm = __builtin_amdgcn_ballot_w64(has_eob);
+  const uint32_t JE = eobm ? (uint32_t)__builtin_ctzll(eobm) : ZS_SEG_NONE;  // the lane ending the block
+  const uint32_t jlast = eobm ? JE : J - 1u;
+  uint32_t kind = eobm ? ZS_SG_K_BEND : ZS_SG_K_CONT;
+  // a chain that reaches the input's end needs its end of block; a chain broken at J
+  // continues from its last lane's stop (a true symbol start)
+  if (!eobm && J == nl && !cont_ok) kind = ZS_SG_K_NONE;
+  const bool mine = chain && lane <= jlast;
   bool bad = false;
-  const bool chain = L.onchain[lane] && L.ok;
-  uint32_t start = ZS_SEG_NONE, cnt = 0;
-  if (chain) {
-    start = lane == 0 ? sym0 : (uint32_t)L.from[lane];
-    // the output count at the start: from the last checkpoint at or before it
+  zs_seg_lane& P = recs[lane];
+  P.act = 0;
+  if (mine && kind != ZS_SG_K_NONE) {
+    const uint32_t end = lane == JE ? eend : nxs;
+    // the output count at the start: from the last own checkpoint at or before it
     uint32_t cp = q, cc = 0;
     for (uint32_t c = 0; c < ZS_SEG_NCK; c++) {
-      const uint32_t p = L.ckp[lane][c];
+      const uint32_t p = L.okp[lane][c];
       if (p != ZS_SEG_NONE && p <= start) {
         cp = p;
-        cc = L.ckc[lane][c];
+        cc = L.okc[lane][c];
       }
     }
-    zs_sg_seek(G, cp);
-    uint32_t p = cp;
-    while (p < start) {
-      const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
-      if (y.kind == ZS_SG_BAD) {
-        p = p + 1u;
-        zs_sg_seek(G, p);
-        continue;
-      }
-      if (y.kind != ZS_SG_EOB) cc += y.len;
-      p = zs_sg_bitpos(G);
+    // ... and at the end: the end-of-block code's, the stop's, or from the last tail
+    // checkpoint at or before the next lane's start (with the last symbol's length)
+    uint32_t ce = cum, ll = last_len;
+    if (lane == JE) {
+      ce = ecum;
+      ll = 0;
     }
-    bad |= p != start;
-    cnt = cum_end - cc;
-    if (kind == ZS_SG_K_BEND) last_len = 0;
+    const bool redo_end = lane != JE && lane + 1u < J;
+    uint32_t tp = qn, tc = 0;
+    bool tfound = false;
+    if (redo_end)
+      for (uint32_t c = 0; c < ZS_SEG_NCK; c++) {
+        const uint32_t p = L.tkp[lane][c];
+        if (p != ZS_SEG_NONE && p <= end) {
+          tp = p;
+          tc = L.tkc[lane][c];
+          tfound = true;
+        }
+      }
+    bad |= redo_end && !tfound;
+    // re-decode the stretches [cp, start) and (redo_end) [tp, end)
+    for (uint32_t pass = 0; pass < 2; pass++) {
+      if (pass == 1 && !redo_end) break;
+      uint32_t p = pass ? tp : cp, c = pass ? tc : cc, lp = 0;
+      const uint32_t to = pass ? end : start;
+      zs_sg_seek(G, p);
+      while (p < to) {
+        const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
+        if (y.kind == ZS_SG_BAD) {
+          p = p + 1u;
+          zs_sg_seek(G, p);
+          lp = 0;
+          continue;
+        }
+        lp = y.kind == ZS_SG_EOB ? 0u : y.len;
+        c += lp;
+        p = zs_sg_bitpos(G);
+      }
+      bad |= p != to;
+      if (pass) {
+        ce = c;
+        ll = lp;
+      } else {
+        cc = c;
+      }
+    }
     // the piece's own events, consecutive sub-chunks
     uint32_t k0 = 0, ne = 0;
     uint32_t eo[ZS_SEG_NEV];
@@ -588,47 +518,207 @@ __global__ __launch_bounds__(64) void zs_k_seg_sync(const uint8_t* __restrict__ 
       }
     }
     bad |= nev > ZS_SEG_NEV;
-    // an invalid code, or an end of block before the piece's end, in the true stream
-    // (the rings hold the last ones of the window: any in the true stream is among them)
+    // an invalid code in the true stream
 #pragma unroll
     for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) bad |= e < nbad && bad_sb[e] >= start && bad_sb[e] < end;
     bad |= xbad < end;
-    if (kind == ZS_SG_K_SYNC) {
-#pragma unroll
-      for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) bad |= e < neob && eob_sb[e] >= start;
-      bad |= xeob_sb < end;
-    }
-    zs_seg_lane& P = lanes[(size_t)b * ZS_SEG_LANES + lane];
     P.start = start;
     P.end = end;
-    P.cnt = cnt;
-    P.last_len = last_len;
+    P.cnt = ce - cc;
+    P.last_len = ll;
     P.nev = ne;
     P.ev_k0 = k0;
 #pragma unroll
     for (uint32_t e = 0; e < ZS_SEG_NEV; e++) P.ev_o[e] = eo[e];
-    if (kind == ZS_SG_K_BEND) L.bend = end;
-  } else if (lane < ZS_SEG_LANES) {
-    lanes[(size_t)b * ZS_SEG_LANES + lane].start = ZS_SEG_NONE;
+    if (lane == jlast) L.send = end;
+  } else {
+    P.start = ZS_SEG_NONE;
   }
-  bad = __syncthreads_or(bad);
+  bad_out = __syncthreads_or(bad);
+  send = L.send;
+  return kind;
+}
+
+template <bool D64>
+__global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                                    const uint32_t* __restrict__ in_len,
+                                                    const uint32_t* __restrict__ list, uint32_t n_list,
+                                                    const uint32_t* __restrict__ big, uint32_t n_big, int wbits,
+                                                    const uint64_t* __restrict__ found,
+                                                    const uint32_t* __restrict__ spb, zs_seg_blk* __restrict__ blk,
+                                                    zs_seg_lane* __restrict__ lanes, zcode* __restrict__ tcache,
+                                                    zs_seg_ent* __restrict__ ents, zs_seg_mem* __restrict__ mem,
+                                                    uint32_t* __restrict__ nspan, uint32_t* __restrict__ spans,
+                                                    uint32_t sbits) {
+  __shared__ zs_sg_walk_lds L;
+  const uint32_t lane = threadIdx.x;
+  // the entry: blocks [0, n_list): entry 0 of list member blockIdx.x; then
+  // (ZS_SPLIT_MAX - 1) entries per big member
+  uint32_t m, e, bi = ZS_SEG_NONE;
+  if (blockIdx.x < n_list) {
+    m = blockIdx.x;
+    e = 0;
+  } else {
+    const uint32_t x = blockIdx.x - n_list;
+    bi = x / (ZS_SPLIT_MAX - 1u);
+    if (bi >= n_big) return;
+    e = 1u + x % (ZS_SPLIT_MAX - 1u);
+    m = big[bi];
+  }
+  zs_seg_ent& E = ents[(size_t)m * ZS_SPLIT_MAX + e];
+  uint32_t start = 0;
+  if (e) {
+    const uint64_t f = found[(size_t)bi * ZS_SPLIT_MAX + e];
+    if (f == ~0ull) return;  // (no candidate in this range: the entry record is never read)
+    start = (uint32_t)f;
+  }
   if (lane == 0) {
-    Bk.hdr = r == 0 ? hdr : f;
-    Bk.sym0 = sym0;
-    Bk.end = L.bend;
-    Bk.lbits = lbits;
-    Bk.dbits = dbits;
-    Bk.dofs = dofs;
-    Bk.nl = nl;
-    Bk.S = S;
-    Bk.flags = (L.ok && !bad ? ZS_SEG_B_OK : 0u) | (last ? ZS_SEG_B_FINAL : 0u);
+    E.start = start;
+    E.first = ZS_SEG_NONE;
+    E.end = 0;
+    E.flags = 0;
+  }
+  // where the walk may stop: the later entries' starts (a big member's), found
+  // in order of their ranges, so in order of position
+  uint32_t later = ZS_SEG_NONE;  // this lane's: the start of entry `lane` if later than e
+  if (bi != ZS_SEG_NONE && lane > e && lane < ZS_SPLIT_MAX) {
+    const uint64_t f = found[(size_t)bi * ZS_SPLIT_MAX + lane];
+    if (f != ~0ull) later = (uint32_t)f;
+  }
+  const uint32_t s = list[m];
+  const uint32_t n = in_len[s];
+  const uint32_t nbits = 8u * n;
+  const uint8_t* src = in + in_off[s];
+  const uint32_t sb0 = spb[m], cap = spb[m + 1] - sb0;
+  zs_seg_mem& M = mem[m];
+  zs_wave_reader R;
+  R.n = n;
+  R.sh = (uint32_t)((uintptr_t)src & 3u);
+  R.w4 = reinterpret_cast<const uint32_t*>(src - R.sh);
+  R.last = (R.sh + n - 1u) >> 2;
+  R.inw = L.inw;
+  zs_wr_stage(R, ((start >> 3) + R.sh) >> 2);
+  zs_wr_seek(R, start >> 3);
+  zs_wr_take(R, start & 7u);
+  bool good = true;
+  const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;  // inflate.ts:152-160
+  if (e == 0 && wrap) {  // plain zlib / gzip headers only (inflate.ts:377-580), as the lane path
+    const uint32_t b0 = zs_wr_take(R, 8), b1 = zs_wr_take(R, 8);
+    if ((wrap & 2) && b0 == 0x1f && b1 == 0x8b) {
+      const uint32_t cm = zs_wr_take(R, 8), flg = zs_wr_take(R, 8);
+      zs_wr_take(R, 32);
+      zs_wr_take(R, 16);
+      good = cm == 8 && flg == 0;
+    } else if (wrap & 1) {
+      good = !(((b0 << 8) | b1) % 31 || (b0 & 15) != 8 || (b0 >> 4) + 8 > 15 || (b1 & 0x20));
+    } else {
+      good = false;
+    }
+  }
+  uint32_t hdr = (uint32_t)zs_wr_bitpos(R);
+  uint32_t pe0 = e == 0 ? 0u : start;  // sub-chunk events before the first symbol go to it
+  uint32_t prevb = ZS_SEG_NONE;       // the entry's last span
+  uint32_t flags_e = 0;
+  // bits per lane: seg_bits for the entry's first block, then from the size of the
+  // block before (a zlib stream's blocks are alike): the block in one span of
+  // about 60 lanes, S >= ZS_SEG_W (a lane's window ends before the next lane's start)
+  uint32_t S = sbits;
+  while (good) {
+    // ---- a block: its header (wave-uniform) and tables
+    if (hdr != (uint32_t)zs_wr_bitpos(R)) {
+      zs_wr_stage(R, ((hdr >> 3) + R.sh) >> 2);
+      zs_wr_seek(R, hdr >> 3);
+      zs_wr_take(R, hdr & 7u);
+    }
+    uint32_t last = 0, lbits = 0, dbits = 0, dofs = 0, ntab = 0;
+    good = zs_sg_header(R, L.codes, L.lens, L.work, D64, last, lbits, dbits, dofs, ntab);
+    const uint32_t sym0 = (uint32_t)zs_wr_bitpos(R);
+    if (good && sym0 > nbits) good = false;
+    if (!good) break;
+    __syncthreads();
+    uint32_t tab = ZS_SEG_NONE, cur = sym0;
+    bool first = true;
+    for (;;) {
+      // ---- a span
+      uint32_t b = 0;
+      if (lane == 0) b = atomicAdd(&M.nalloc, 1u);
+      b = zs_u(__shfl(b, 0));
+      if (b >= cap) {
+        good = false;
+        break;
+      }
+      b += sb0;
+      if (lane == 0) spans[atomicAdd(nspan, 1u)] = b;  // (the decode's work list)
+      if (first) {
+        tab = b;
+        for (uint32_t i = lane; i < ntab; i += 64) tcache[(size_t)b * ZS_SEG_TAB + i] = L.codes[i];
+      }
+      if (cur >= nbits) {
+        good = false;
+        break;
+      }
+      const uint32_t nl = max(1u, min(ZS_SEG_LANES, (nbits - cur + S - 1u) / S));
+      uint32_t send = 0;
+      bool sbad = false;
+      const uint32_t k = zs_sg_span<D64>(L, src, n, cur, pe0, nl, S, lbits, dbits, dofs,
+                                         lanes + (size_t)b * ZS_SEG_LANES, send, sbad);
+      if (lane == 0) {
+        zs_seg_blk& Bk = blk[b];
+        Bk.m = m;
+        Bk.e = e;
+        Bk.hdr = first ? hdr : cur;
+        Bk.sym0 = cur;
+        Bk.end = send;
+        Bk.lbits = lbits;
+        Bk.dbits = dbits;
+        Bk.dofs = dofs;
+        Bk.tab = tab;
+        Bk.nl = nl;
+        Bk.S = S;
+        Bk.next = ZS_SEG_NONE;
+        Bk.flags = (k && !sbad ? ZS_SEG_B_OK : 0u) | (first ? ZS_SEG_B_FIRST : 0u) |
+                   (k == ZS_SG_K_BEND ? ZS_SEG_B_EOB : 0u) | (k == ZS_SG_K_BEND && last ? ZS_SEG_B_FINAL : 0u);
+        if (prevb == ZS_SEG_NONE) E.first = b;
+        else blk[prevb].next = b;
+      }
+      prevb = b;
+      if (!k || sbad) {
+        good = false;
+        break;
+      }
+      first = false;
+      pe0 = send;
+      cur = send;
+      if (k == ZS_SG_K_BEND) break;
+    }
+    if (!good) break;
+    // ---- the block ended at cur: the final one, or at a later entry's start
+    S = min(ZS_SEG_SMAX, max(ZS_SEG_W, (cur - hdr) / 60u));
+    hdr = cur;
+    if (last) {
+      flags_e = 3u;
+      break;
+    }
+    if (__builtin_amdgcn_ballot_w64(later == cur)) {
+      flags_e = 1u;
+      break;
+    }
+    if (cur >= nbits) {
+      good = false;
+      break;
+    }
+  }
+  if (lane == 0) {
+    E.end = hdr;
+    E.flags = good ? flags_e : 0u;
   }
 }
 
 // ------------------------------------------------------------------- plan
-// One wave per member: the blocks chained by their ends, the pieces placed,
-// the trailer and the capacity checked, and (REFW) the reference's call state
-// at each piece start -- tools/emu/emu_seg.py models exactly this walk.
+// One wave per member: its entries chained from entry 0 (each walk ended where
+// the next one starts), their spans in order, the pieces placed, the trailer
+// and the capacity checked, and (REFW) the reference's call state at each piece
+// start -- tools/emu/emu_seg.py models exactly this walk.
 struct zs_sg_calls {
   uint32_t B, wn, wh, cend;
   __device__ void end_call(uint32_t at) {  // zs_refcalls_t::end_call
@@ -658,32 +748,24 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ in_len,
                                                     const uint32_t* __restrict__ out_cap,
                                                     const uint32_t* __restrict__ list, uint32_t n_list, int wbits,
-                                                    int refw, const uint32_t* __restrict__ cidx,
-                                                    zs_seg_blk* __restrict__ blk, zs_seg_lane* __restrict__ lanes,
+                                                    int refw, const zs_seg_blk* __restrict__ blk,
+                                                    zs_seg_lane* __restrict__ lanes, const zs_seg_ent* __restrict__ ents,
                                                     zs_seg_mem* __restrict__ mem, const uint32_t* __restrict__ pbase,
                                                     uint4* __restrict__ ptab) {
-  __shared__ uint32_t bidx[ZS_SPLIT_MAX], bhdr[ZS_SPLIT_MAX], bend[ZS_SPLIT_MAX], bfl[ZS_SPLIT_MAX];
   __shared__ zs_seg_lane P[ZS_SEG_LANES];
-  __shared__ uint32_t s_bad, s_r, s_next, s_O, s_k, s_prev, s_plen, s_first;
+  __shared__ uint32_t s_bad, s_O, s_k, s_plen, s_first, s_prevg;
   __shared__ zs_sg_calls s_C;
   const uint32_t m = blockIdx.x, lane = threadIdx.x;
   if (m >= n_list) return;
   zs_seg_mem& M = mem[m];
-  if (M.bad) return;
   const uint32_t s = list[m];
-  {
-    const uint32_t bi = cidx[m * ZS_SPLIT_MAX + lane];
-    bidx[lane] = bi;
-    bhdr[lane] = bi != ZS_SEG_NONE ? blk[bi].hdr : ZS_SEG_NONE;
-    bend[lane] = bi != ZS_SEG_NONE ? blk[bi].end : 0u;
-    bfl[lane] = bi != ZS_SEG_NONE ? blk[bi].flags : 0u;
-  }
+  const zs_seg_ent* E = ents + (size_t)m * ZS_SPLIT_MAX;
+  const uint32_t e_start = E[lane].start;  // (lane < ZS_SPLIT_MAX = 64)
   if (lane == 0) {
     s_bad = 0;
-    s_r = 0;
     s_O = 0;
     s_k = 0;
-    s_prev = ZS_SEG_NONE;
+    s_prevg = ZS_SEG_NONE;
     s_plen = 0;
     s_first = 1;
     s_C.B = 0;
@@ -693,103 +775,112 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
   }
   __syncthreads();
   const uint32_t pb = pbase[m], pmax = pbase[m + 1] - pb;
-  uint32_t guard = 0;
-  for (;;) {
-    const uint32_t r = s_r;
-    const uint32_t bi = bidx[r];
-    if (s_bad || bi == ZS_SEG_NONE || !(bfl[r] & ZS_SEG_B_OK) || guard++ > ZS_SPLIT_MAX) {
-      if (lane == 0) s_bad = 1;
+  uint32_t e = 0, guard = 0, fin_end = 0;
+  bool fin = false;
+  while (!s_bad) {
+    const zs_seg_ent En = E[e];
+    if (!(En.flags & 1u) || guard++ > ZS_SPLIT_MAX) {
+      s_bad = 1;
       break;
     }
-    P[lane] = lanes[(size_t)bi * ZS_SEG_LANES + lane];
-    __syncthreads();
-    if (lane == 0) {
-      zs_sg_calls C = s_C;
-      uint32_t O = s_O, k = s_k, prev = s_prev, plen = s_plen;
-      bool first = s_first != 0, bad = false;
-      for (uint32_t l = 0; l < ZS_SEG_LANES && !bad; l++) {
-        zs_seg_lane& p = P[l];
-        if (p.start == ZS_SEG_NONE) continue;
-        bool merge = false;
-        if (!first && refw) {
-          if (l == 0) {
-            C.fills(O);  // the end-of-block code before it, at output O
-          } else {
-            C.fills(O - plen);  // the last symbol of the piece before
-            // a start within 144 bits before a sub-chunk end: the piece before decodes this one too
-            merge = p.start + 144u > 8u * C.cend;
-          }
-        }
-        if (merge) {
-          zs_seg_lane& q = P[prev];  // (the piece before is in this block: l > 0)
-          q.dend = p.end;
-          q.dcnt += p.cnt;
-          p.act = 0;
-          if (k - 1 < pmax) ptab[pb + k - 1].y = q.dcnt;
-        } else {
-          p.O = O;
-          p.off = ((O + 7u) & ~7u) + ZS_SEG_PAD * k;
-          p.dend = p.end;
-          p.dcnt = p.cnt;
-          p.B = C.B;
-          p.wn = C.wn;
-          p.wh = C.wh;
-          p.cend = C.cend;
-          p.act = 1u | (l == 0 ? 0u : 2u);
-          if (k >= pmax) bad = true;
-          else ptab[pb + k] = make_uint4(O, p.cnt, p.off, 0u);
-          k++;
-          prev = l;
-        }
-        if (refw) {
-          for (uint32_t e = 0; e < p.nev; e++) {
-            bad |= 32768u * (p.ev_k0 + e) != C.cend;  // events come one sub-chunk at a time (boundary k: cend = 32768 k)
-            const uint32_t o = O + p.ev_o[e];
-            C.fills(o);
-            C.end_call(o);
-            C.cend += 32768u;
-          }
-        }
-        O += p.cnt;
-        plen = p.last_len;
-        first = false;
+    for (uint32_t b = En.first; b != ZS_SEG_NONE && !s_bad;) {
+      const zs_seg_blk Bk = blk[b];
+      if (!(Bk.flags & ZS_SEG_B_OK)) {
+        s_bad = 1;
+        break;
       }
-      s_C = C;
-      s_O = O;
-      s_k = k;
-      s_prev = ZS_SEG_NONE;
-      s_plen = plen;
-      s_first = first ? 1u : 0u;
-      if (bad) s_bad = 1;
-      // the next block starts where this one ended
-      uint32_t nx = ZS_SEG_NONE;
-      if (!(bfl[r] & ZS_SEG_B_FINAL))
-        for (uint32_t rr = r + 1; rr < ZS_SPLIT_MAX; rr++)
-          if (bhdr[rr] == bend[r]) {
-            nx = rr;
-            break;
+      P[lane] = lanes[(size_t)b * ZS_SEG_LANES + lane];
+      __syncthreads();
+      if (lane == 0) {
+        zs_sg_calls C = s_C;
+        uint32_t O = s_O, k = s_k, prevg = s_prevg, plen = s_plen;
+        bool first = s_first != 0, bad = false;
+        const bool newblk = (Bk.flags & ZS_SEG_B_FIRST) != 0;
+        for (uint32_t l = 0; l < ZS_SEG_LANES && !bad; l++) {
+          zs_seg_lane& p = P[l];
+          if (p.start == ZS_SEG_NONE) continue;
+          bool merge = false;
+          if (!first && refw) {
+            if (l == 0 && newblk) {
+              C.fills(O);  // the end-of-block code before it, at output O
+            } else {
+              C.fills(O - plen);  // the last symbol of the piece before
+              // a start within 144 bits before a sub-chunk end: the piece before decodes this one too
+              merge = p.start + 144u > 8u * C.cend;
+            }
           }
-      s_next = nx;
-    }
-    __syncthreads();
-    // the pieces' plan back to HBM
-    if (P[lane].start != ZS_SEG_NONE) lanes[(size_t)bi * ZS_SEG_LANES + lane] = P[lane];
-    __syncthreads();
-    if (bfl[r] & ZS_SEG_B_FINAL) break;
-    if (lane == 0) {
-      if (s_next == ZS_SEG_NONE) s_bad = 1;
-      else s_r = s_next;
+          if (merge) {
+            // the piece before is in this block: in this span, or the entry's span before
+            const bool here = prevg / ZS_SEG_LANES == b;
+            zs_seg_lane& q = here ? P[prevg % ZS_SEG_LANES] : lanes[prevg];
+            q.dend = p.end;
+            q.dcnt += p.cnt;
+            p.act = 0;
+            if (k - 1 < pmax) ptab[pb + k - 1].y = q.dcnt;
+          } else {
+            p.O = O;
+            p.off = ((O + 7u) & ~7u) + ZS_SEG_PAD * k;
+            p.dend = p.end;
+            p.dcnt = p.cnt;
+            p.B = C.B;
+            p.wn = C.wn;
+            p.wh = C.wh;
+            p.cend = C.cend;
+            p.act = 1u | (l == 0 && newblk ? 0u : 2u);
+            if (k >= pmax) bad = true;
+            else ptab[pb + k] = make_uint4(O, p.cnt, p.off, 0u);
+            k++;
+            prevg = b * ZS_SEG_LANES + l;
+          }
+          if (refw) {
+            for (uint32_t x = 0; x < p.nev; x++) {
+              bad |= 32768u * (p.ev_k0 + x) != C.cend;  // events come one sub-chunk at a time (boundary k: cend = 32768 k)
+              const uint32_t o = O + p.ev_o[x];
+              C.fills(o);
+              C.end_call(o);
+              C.cend += 32768u;
+            }
+          }
+          O += p.cnt;
+          plen = p.last_len;
+          first = false;
+        }
+        s_C = C;
+        s_O = O;
+        s_k = k;
+        s_prevg = prevg;
+        s_plen = plen;
+        s_first = first ? 1u : 0u;
+        if (bad) s_bad = 1;
+      }
+      __syncthreads();
+      // the pieces' plan back to HBM
+      if (P[lane].start != ZS_SEG_NONE) lanes[(size_t)b * ZS_SEG_LANES + lane] = P[lane];
+      __threadfence_block();
+      __syncthreads();
+      b = Bk.next;
     }
     __syncthreads();
     if (s_bad) break;
+    if (En.flags & 2u) {
+      fin = true;
+      fin_end = En.end;
+      break;
+    }
+    // the entry whose start is where this walk stopped
+    const uint64_t nx = __builtin_amdgcn_ballot_w64(lane > e && e_start == En.end);
+    if (!nx) {
+      s_bad = 1;
+      break;
+    }
+    e = (uint32_t)__builtin_ctzll(nx);
   }
   __syncthreads();
   if (lane == 0) {
-    bool bad = s_bad != 0;
+    bool bad = s_bad != 0 || !fin;
     const uint32_t total = s_O;
     const uint32_t n = in_len[s];
-    const uint32_t e = bend[s_r];
-    uint32_t consumed = (e + 7u) >> 3, want = 0;
+    uint32_t consumed = (fin_end + 7u) >> 3, want = 0;
     const int wrap = wbits < 0 ? 0 : (wbits >> 4) + 5;
     if (!bad && wrap) {  // the trailer (inflate.ts:1006-1036); the check value is verified after the checksum pass
       const uint8_t* t = in + in_off[s] + consumed;
@@ -841,7 +932,12 @@ struct zs_sg_out {
     if (P + k - F > 64u) flush();
   }
   // the value at piece position x < P: the ring holds the last 64, older ones are stored
+#if ZS_SEG_EXP & 1
+  uint32_t far = 0;
+  __device__ __forceinline__ uint32_t get(uint32_t x) { far += x + 64u < P; return x + 64u >= P ? ring[x & 63u] : dst[x]; }
+#else
   __device__ __forceinline__ uint32_t get(uint32_t x) const { return x + 64u >= P ? ring[x & 63u] : dst[x]; }
+#endif
   __device__ __forceinline__ void finish() {
     flush();
     if (F < P) *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & 63u));
@@ -896,12 +992,23 @@ static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint
   return true;
 }
 
+#ifndef ZS_SEG_EXP
+#define ZS_SEG_EXP 0  // instrumentation (timing experiments only; 0 in the product): 1 per-span decode clocks
+#endif
+#if ZS_SEG_EXP & 1
+#define ZS_SEG_DBG_N 65536u
+__device__ unsigned long long zs_seg_dbg[ZS_SEG_DBG_N][4];  // per span slot: start, end (max), symbols (max lane), far reads (max lane)
+extern "C" int zs_seg_dbg_fetch(void* out, unsigned long long bytes) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_seg_dbg), bytes < sizeof(zs_seg_dbg) ? bytes : sizeof(zs_seg_dbg));
+}
+#endif
 template <bool D64, bool REFW>
 __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict__ in,
                                                       const uint64_t* __restrict__ in_off,
                                                       const uint32_t* __restrict__ in_len,
                                                       const uint32_t* __restrict__ list,
-                                                      const uint32_t* __restrict__ counter,
+                                                      const uint32_t* __restrict__ nspan,
+                                                      const uint32_t* __restrict__ spans,
                                                       const zs_seg_blk* __restrict__ blk,
                                                       const zs_seg_lane* __restrict__ lanes,
                                                       const zcode* __restrict__ tcache, zs_seg_mem* __restrict__ mem,
@@ -909,16 +1016,30 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
                                                       uint16_t* __restrict__ scratch) {
   __shared__ zcode codes[ZS_SEG_TAB];
   __shared__ __attribute__((aligned(16))) uint16_t ring[ZS_SEG_LANES][64];
-  const uint32_t b = blockIdx.x, lane = threadIdx.x;
-  if (b >= *counter) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t ns = *nspan;
+  for (uint32_t k = blockIdx.x; k < ns; k += gridDim.x) {
+  const uint32_t b = zs_u(spans[k]);
   const zs_seg_blk& Bk = blk[b];
   const uint32_t m = zs_u(Bk.m);
-  if (m == ZS_SEG_NONE || !(Bk.flags & ZS_SEG_B_OK) || mem[m].bad) return;
-  const uint32_t ntab = ZS_SEG_TAB;
-  for (uint32_t i = lane; i < ntab; i += 64) codes[i] = tcache[(size_t)b * ZS_SEG_TAB + i];
+  if (m == ZS_SEG_NONE || !(Bk.flags & ZS_SEG_B_OK) || mem[m].bad) continue;
+  const uint32_t ntab = ZS_SEG_TAB, tab = zs_u(Bk.tab);
+  __syncthreads();  // (the previous span's tables are no longer read)
+  for (uint32_t i = lane; i < ntab; i += 64) codes[i] = tcache[(size_t)tab * ZS_SEG_TAB + i];
   __syncthreads();
   const zs_seg_lane& p = lanes[(size_t)b * ZS_SEG_LANES + lane];
-  if (lane >= zs_u(Bk.nl) || p.start == ZS_SEG_NONE || !(p.act & 1u)) return;
+#if ZS_SEG_EXP & 1
+  const unsigned long long dbg_t0 = wall_clock64();
+  if (lane == 0 && b < ZS_SEG_DBG_N) {
+    zs_seg_dbg[b][0] = dbg_t0;
+    zs_seg_dbg[b][1] = 0;
+    zs_seg_dbg[b][2] = 0;
+    zs_seg_dbg[b][3] = 0;
+  }
+  __syncthreads();
+  uint32_t dbg_sym = 0;
+#endif
+  if (lane >= zs_u(Bk.nl) || p.start == ZS_SEG_NONE || !(p.act & 1u)) continue;
   const uint32_t s = list[m];
   const uint32_t lmask = (1u << Bk.lbits) - 1u, dmask = (1u << Bk.dbits) - 1u, emask = D64 ? 31u : 15u;
   const zcode* lt = codes;
@@ -946,6 +1067,9 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
     if (W.P - W.F >= 32u) W.flush();
     const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
     const uint32_t o = O + W.P;
+#if ZS_SEG_EXP & 1
+    dbg_sym++;
+#endif
     if (y.kind == ZS_SG_LIT) {
       if (REFW) C.symbol(sb, o, 1u, y.l1, 0u, 0u, 0u, false);
       W.room(1);
@@ -979,6 +1103,14 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
   bad |= sb > dend || W.P != p.dcnt;
   if (!bad) W.finish();
   if (bad) atomicOr(&mem[m].bad, 1u);
+#if ZS_SEG_EXP & 1
+  if (b < ZS_SEG_DBG_N) {
+    atomicMax(&zs_seg_dbg[b][1], wall_clock64());
+    atomicMax(&zs_seg_dbg[b][2], (unsigned long long)dbg_sym);
+    atomicMax(&zs_seg_dbg[b][3], (unsigned long long)W.far);
+  }
+#endif
+  }
 }
 
 // ---------------------------------------------------------------- resolve
@@ -1001,7 +1133,8 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
                                                         const uint16_t* __restrict__ scratch, uint8_t* __restrict__ out,
                                                         const uint64_t* __restrict__ out_off,
                                                         zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out,
-                                                        uint32_t* __restrict__ n_ok) {
+                                                        uint32_t* __restrict__ n_ok, uint32_t* __restrict__ n_left,
+                                                        uint32_t* __restrict__ left) {
   extern __shared__ __attribute__((aligned(16))) uint32_t zs_rring[];  // 64 KiB of bytes
   __shared__ uint4 tab[ZS_SG_RES_PT];
   uint8_t* ring = reinterpret_cast<uint8_t*>(zs_rring);
@@ -1013,6 +1146,7 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
       zs_lane_res r = {1u, 0u, 0u, 0u};
       res[s] = r;
       lens_out[s] = 0;
+      left[atomicAdd(n_left, 1u)] = s;  // (the wave kernel's list)
     }
     return;
   }
@@ -1095,21 +1229,25 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
   far = __syncthreads_or(far);
   if (t == 0) {
     if (!far) atomicAdd(n_ok, 1u);  // (statistics: zs_last_inflate_seg_count)
+    else left[atomicAdd(n_left, 1u)] = s;
     zs_lane_res r = {far ? 1u : 0u, far ? 0u : M.total, M.consumed, M.want};
     res[s] = r;
     lens_out[s] = far ? 0u : M.total;
   }
 }
 
-template __global__ void zs_k_seg_sync<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, int,
-                                              const uint64_t*, const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*,
-                                              uint32_t);
-template __global__ void zs_k_seg_sync<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, int,
-                                             const uint64_t*, const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*,
-                                             uint32_t);
+template __global__ void zs_k_seg_walk<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,
+                                              uint32_t, const uint32_t*, uint32_t, int, const uint64_t*,
+                                              const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*, zs_seg_ent*,
+                                              zs_seg_mem*, uint32_t*, uint32_t*, uint32_t);
+template __global__ void zs_k_seg_walk<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,
+                                             uint32_t, const uint32_t*, uint32_t, int, const uint64_t*,
+                                             const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*, zs_seg_ent*,
+                                             zs_seg_mem*, uint32_t*, uint32_t*, uint32_t);
 #define ZS_SEG_DEC_INST(D, W)                                                                                       \
   template __global__ void zs_k_seg_decode<D, W>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, \
-                                                 const uint32_t*, const zs_seg_blk*, const zs_seg_lane*,           \
+                                                 const uint32_t*, const uint32_t*, const zs_seg_blk*,              \
+                                                 const zs_seg_lane*,                                               \
                                                  const zcode*, zs_seg_mem*, const uint64_t*, uint16_t*);
 ZS_SEG_DEC_INST(false, false)
 ZS_SEG_DEC_INST(false, true)

@@ -44,25 +44,20 @@ static __host__ __device__ inline uint32_t zs_wave_ring_bytes(bool d64) { return
 // REFW: a deflate / zlib / gzip member with the reference's window-wrap copy
 // reproduced (flags & ZS_INF_REF_WRAP); the other instance (deflate64, or
 // inflate_ref_wrap = 0) carries no call bookkeeping.
+// one member s, by the whole wave
 template <bool REFW>
-__global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restrict__ in,
-                                                        const uint64_t* __restrict__ in_off,
-                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
-                                                        const uint64_t* __restrict__ out_off,
-                                                        const uint32_t* __restrict__ out_cap, int wbits,
-                                                        const uint32_t* __restrict__ list, uint32_t n_list,
-                                                        zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out,
-                                                        uint32_t skip_done) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t zs_wsm[];
+static __device__ __forceinline__ void zs_wave_member(uint8_t* zs_wsm, const uint8_t* __restrict__ in,
+                                                      const uint64_t* __restrict__ in_off,
+                                                      const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                      const uint64_t* __restrict__ out_off,
+                                                      const uint32_t* __restrict__ out_cap, int wbits,
+                                                      zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out,
+                                                      const uint32_t s) {
   const bool d64 = wbits == -16;
   uint8_t* ring = zs_wsm;
   const uint32_t rmask = zs_wave_ring_bytes(d64) - 1u;
   zs_wave_tabs& W = *reinterpret_cast<zs_wave_tabs*>(zs_wsm + zs_wave_ring_bytes(d64));
-  if (blockIdx.x >= n_list) return;
   const uint32_t lane = threadIdx.x;
-  const uint32_t s = zs_u(list[blockIdx.x]);
-  // skip_done: the members the segmented decode (inflate_seg.hip) finished already
-  if (skip_done && zs_u(res[s].bail) == 0) return;
   const uint8_t* src = in + in_off[s];
   zs_wave_reader R;
   R.n = zs_u(in_len[s]);
@@ -286,9 +281,29 @@ __global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restric
 
 size_t zs_inflate_wave_lds_bytes(bool d64) { return zs_wave_ring_bytes(d64) + sizeof(zs_wave_tabs); }
 
+// list[0 .. n_list): the members.  skip_done: list is the segmented decode's
+// leftovers (inflate_seg.hip), n_dev their count: a grid of fixed size walks it,
+// so the usual case -- none -- costs no dispatch of one workgroup per member.
+template <bool REFW>
+__global__ __launch_bounds__(64) void zs_k_inflate_wave(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off,
+                                                        const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_off,
+                                                        const uint32_t* __restrict__ out_cap, int wbits,
+                                                        const uint32_t* __restrict__ list, uint32_t n_list,
+                                                        zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out,
+                                                        const uint32_t* __restrict__ n_dev) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t zs_wsm[];
+  const uint32_t nl = n_dev ? min(n_list, zs_u(*n_dev)) : n_list;
+  for (uint32_t k = blockIdx.x; k < nl; k += gridDim.x) {
+    __syncthreads();  // (the LDS of the member before is free)
+    zs_wave_member<REFW>(zs_wsm, in, in_off, in_len, out, out_off, out_cap, wbits, res, lens_out, zs_u(list[k]));
+  }
+}
+
 template __global__ void zs_k_inflate_wave<false>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                                   const uint64_t*, const uint32_t*, int, const uint32_t*, uint32_t,
-                                                  zs_lane_res*, uint32_t*, uint32_t);
+                                                  zs_lane_res*, uint32_t*, const uint32_t*);
 template __global__ void zs_k_inflate_wave<true>(const uint8_t*, const uint64_t*, const uint32_t*, uint8_t*,
                                                  const uint64_t*, const uint32_t*, int, const uint32_t*, uint32_t,
-                                                 zs_lane_res*, uint32_t*, uint32_t);
+                                                 zs_lane_res*, uint32_t*, const uint32_t*);

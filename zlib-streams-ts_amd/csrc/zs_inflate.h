@@ -63,7 +63,7 @@ __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, con
 template <bool REFW>
 __global__ void zs_k_inflate_wave(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                                   const uint64_t* out_off, const uint32_t* out_cap, int wbits, const uint32_t* list,
-                                  uint32_t n_list, zs_lane_res* res, uint32_t* lens_out, uint32_t skip_done);
+                                  uint32_t n_list, zs_lane_res* res, uint32_t* lens_out, const uint32_t* n_dev);
 __global__ void zs_k_inflate_lane_verify(zs_lane_res* res, const uint32_t* check, uint32_t n);
 size_t zs_inflate_smem_bytes(int wbits);
 size_t zs_inflate_lane_lds_bytes(bool root);

@@ -7,8 +7,10 @@
 #include "zs_inftab.h"
 #include "zs_split.h"
 
-#define ZS_SEG_LANES 64u    // pieces per block wave (one lane each)
-#define ZS_SEG_W 2048u      // bits of a lane's start window whose symbol starts it records (the sync bitmap)
+#define ZS_SEG_LANES 64u    // pieces per span (one lane each)
+#ifndef ZS_SEG_W
+#define ZS_SEG_W 1024u  // bits of a lane's start window whose symbol starts it records (the sync bitmaps)
+#endif
 #define ZS_SEG_CKB 128u     // spacing of a lane's (position, output count) checkpoints in its window
 #define ZS_SEG_NCK (ZS_SEG_W / ZS_SEG_CKB)
 #define ZS_SEG_NEV 4u       // sub-chunk crossing events a lane records
@@ -16,26 +18,34 @@
 #define ZS_SEG_PAD 16u      // u16 values of padding behind each piece's scratch
 #define ZS_SEG_TAB (ENOUGH_LENS + ENOUGH_DISTS_9)  // cached table entries per block
 #define ZS_SEG_NONE 0xffffffffu
+#define ZS_SEG_BIG_BITS (1u << 21)  // members with more input bits: block starts from the finder as extra entries
+#define ZS_SEG_SPLIT_BITS (1u << 18)  // deflate64 members with more input bits: the split decode (long copies)
+#define ZS_SEG_BLOCK_BITS 16384u    // span slots per member: one per this many input bits (+ capi.cpp's margin)
+#define ZS_SEG_SMAX 8192u           // bits per lane at most (a span's lanes: seg_bits, then from the block before)
 
-// block flags
-#define ZS_SEG_B_OK 1u     // header parsed, tables cached, its pieces chain to an end of block
-#define ZS_SEG_B_FINAL 2u  // BFINAL set
+// span flags
+#define ZS_SEG_B_OK 1u     // header parsed (FIRST), the span's pieces chain from its start to its end
+#define ZS_SEG_B_FINAL 2u  // ends the member's final block
+#define ZS_SEG_B_FIRST 4u  // starts a block (its header at hdr)
+#define ZS_SEG_B_EOB 8u    // ends its block (else the entry's next span continues it)
 
-// One candidate block (zs_k_split_find's found[] entry, given a compact index by zs_k_seg_alloc).
+// One span: a stretch of one block whose symbols a wave's lanes decode from
+// sym0 + j S (zs_k_seg_walk); its lanes' pieces in zs_seg_lane[span * 64 + j].
 struct zs_seg_blk {
-  uint32_t m, r;     // member (list index), range of the finder
-  uint32_t hdr;      // bit of the block header
-  uint32_t sym0;     // bit of the first symbol
-  uint32_t end;      // bit past the end-of-block code
+  uint32_t m, e;     // member (list index), entry
+  uint32_t hdr;      // bit of the block header (FIRST), else = sym0
+  uint32_t sym0;     // bit of the span's first symbol
+  uint32_t end;      // bit where the span ends (past the end-of-block code, or the next span's sym0)
   uint32_t flags;
-  uint32_t lbits, dbits, dofs;  // table roots, distance table offset in the cached codes
+  uint32_t lbits, dbits, dofs, tab;  // table roots, distance table offset, the span slot caching the tables
   uint32_t nl, S;    // lanes, bits per lane
-  uint32_t pad;
+  uint32_t next;     // the entry's next span (ZS_SEG_NONE: its last)
+  uint32_t pad[3];
 };
 
-// One lane of a block wave: a piece of the block, [start, end) in bits.
+// One lane of a span: a piece of the block, [start, end) in bits.
 struct zs_seg_lane {
-  // zs_k_seg_sync
+  // zs_k_seg_walk
   uint32_t start, end;   // start ZS_SEG_NONE: no piece (the lane was absorbed by the one before)
   uint32_t cnt;          // output values of the piece
   uint32_t last_len;     // values of its last symbol (0: an end of block)
@@ -50,25 +60,31 @@ struct zs_seg_lane {
   uint32_t act;          // bit 0: decoded (a piece that is not merged), bit 1: the fast flag
 };
 
-struct zs_seg_mem {
-  uint32_t bad, total, consumed, want, npieces;
-  uint32_t pad[3];
+// One entry of a member: where a walk starts (entry 0: the member's first bit;
+// a big member's entries e >= 1: the finder's block start in bit range e).
+struct zs_seg_ent {
+  uint32_t start, first, end, flags;  // first span; end: the block boundary it stopped at; flags 1 ok, 2 final
 };
 
-__global__ void zs_k_seg_alloc(const uint64_t* found, uint32_t n_list, uint32_t* cidx, zs_seg_blk* blk,
-                               uint32_t* counter, uint32_t cap_blocks, zs_seg_mem* mem);
+struct zs_seg_mem {
+  uint32_t bad, total, consumed, want, npieces, nalloc;  // nalloc: span slots taken (zs_k_seg_walk)
+  uint32_t pad[2];
+};
+
 template <bool D64>
-__global__ void zs_k_seg_sync(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* list,
-                              int wbits, const uint64_t* found, const uint32_t* counter, zs_seg_blk* blk,
-                              zs_seg_lane* lanes, zcode* tcache, uint32_t smin);
+__global__ void zs_k_seg_walk(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* list,
+                              uint32_t n_list, const uint32_t* big, uint32_t n_big, int wbits, const uint64_t* found,
+                              const uint32_t* spb, zs_seg_blk* blk, zs_seg_lane* lanes, zcode* tcache,
+                              zs_seg_ent* ents, zs_seg_mem* mem, uint32_t* nspan, uint32_t* spans, uint32_t sbits);
 __global__ void zs_k_seg_plan(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                               const uint32_t* out_cap, const uint32_t* list, uint32_t n_list, int wbits, int refw,
-                              const uint32_t* cidx, zs_seg_blk* blk, zs_seg_lane* lanes, zs_seg_mem* mem,
+                              const zs_seg_blk* blk, zs_seg_lane* lanes, const zs_seg_ent* ents, zs_seg_mem* mem,
                               const uint32_t* pbase, uint4* ptab);
 template <bool D64, bool REFW>
 __global__ void zs_k_seg_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* list,
-                                const uint32_t* counter, const zs_seg_blk* blk, const zs_seg_lane* lanes,
-                                const zcode* tcache, zs_seg_mem* mem, const uint64_t* sbase, uint16_t* scratch);
+                                const uint32_t* nspan, const uint32_t* spans, const zs_seg_blk* blk, const zs_seg_lane* lanes, const zcode* tcache,
+                                zs_seg_mem* mem, const uint64_t* sbase, uint16_t* scratch);
 __global__ void zs_k_seg_resolve(const uint32_t* list, const zs_seg_mem* mem, const uint32_t* pbase,
                                  const uint4* ptab, const uint64_t* sbase, const uint16_t* scratch, uint8_t* out,
-                                 const uint64_t* out_off, zs_lane_res* res, uint32_t* lens_out, uint32_t* n_ok);
+                                 const uint64_t* out_off, zs_lane_res* res, uint32_t* lens_out, uint32_t* n_ok,
+                                 uint32_t* n_left, uint32_t* left);
