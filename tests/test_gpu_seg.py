@@ -98,18 +98,26 @@ def test_segmented_decode_without_the_window_wrap_copy(engine):
     assert [g[3] for g in got] == [s for s, _ in ms]
 
 
-def test_deflate64_fixtures_through_the_segmented_decode(engine):
+def test_deflate64_fixtures_in_a_small_batch(engine):
     """The reference's test/data deflate64 fixtures (decoded sizes / digests
-    pinned by inflate_small.json), each as a "large" member of a small batch."""
+    pinned by inflate_small.json), each a "large" member of a small batch: the
+    high-expansion ones (long copies: a cap past 64 KiB, >= 8 output bytes per
+    input byte) take the split decode, the others the segmented one."""
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "inflate_small.json")))
     fx = [(open(os.path.join(ROOT, "tests", "golden", "d64", c["name"][4:]), "rb").read(), c["out_len"],
            c["out_sha256"]) for c in g["cases"] if c["name"].startswith("d64_") and c.get("ok")]
     with _opts(engine, seg_small_min=256):
         got = engine.decompress_batch_raw([d for d, _, _ in fx], "deflate64-raw", [n for _, n, _ in fx])
-        nseg = engine.last_seg_count()
     for (d, n, h), r in zip(fx, got):
         assert r[0] == 1 and len(r[3]) == n and hashlib.sha256(r[3]).hexdigest() == h and r[4] == len(d)
-    assert nseg >= len(fx) // 2
+    # the same fixtures with caps that hide the expansion (<= 64 KiB where they fit): the segmented decode
+    small = [(d, n, h) for d, n, h in fx if n <= 65536]
+    with _opts(engine, seg_small_min=256):
+        got = engine.decompress_batch_raw([d for d, _, _ in small], "deflate64-raw", [65536] * len(small))
+        nseg = engine.last_seg_count()
+    for (d, n, h), r in zip(small, got):
+        assert r[0] == 1 and len(r[3]) == n and hashlib.sha256(r[3]).hexdigest() == h and r[4] == len(d)
+    assert nseg >= 1
 
 
 def test_damaged_members_take_the_other_paths(engine):

@@ -118,6 +118,8 @@ struct zs_ctx {
   uint32_t seg_bits = 2048;         // input bits per lane of an entry's first block (later ones: from the block before)
   uint32_t seg_small_batch = 16384; // batches of at most this many members ...
   uint32_t seg_small_min = 4096;    // ... send members with more input bytes than this to it too
+  bool seg_wide = true;             // the 2048-bit sync window for a batch of few large members
+  uint32_t ncu = 256;               // compute units of the device
   Buf glist, gfound, gbig, gbigs, gspb, gspl, gflist, gent, gblk, glanes, gtab, gmem, gpbase, gplist, gsbase, gscr, gcnt;
   std::vector<uint32_t> hglist, hgpbase, hgspb, hgbig, hgbig_s;
   bool seg_used = false;            // the last inflate batch ran it
@@ -241,6 +243,11 @@ int zs_ctx_create(int device, zs_ctx** out) {
     zs_ctx_destroy(c);
     return fail(ZS_MEM_ERROR, "%s", "cannot create the side stream");
   }
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+      c->ncu = (uint32_t)ncu;
+  }
   // the chain builders use lane-ordered LDS atomics where the device applies them so:
   // check before any use; a device that violates it gets the ballot-ranked form
   uint64_t bad = 0;
@@ -325,6 +332,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   }
   else if (!strcmp(name, "inflate_split")) c->inflate_split = value != 0;
   else if (!strcmp(name, "inflate_seg")) c->inflate_seg = value != 0;
+  else if (!strcmp(name, "seg_wide")) c->seg_wide = value != 0;
   else if (!strcmp(name, "seg_bits")) {
     if (value < (int)ZS_SEG_W || value > (int)ZS_SEG_SMAX) return fail(ZS_STREAM_ERROR, "seg_bits must be 1024 .. 8192");
     c->seg_bits = (uint32_t)value;
@@ -1128,12 +1136,17 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
     if (int r = mark(c, sd, "seg_find")) return r;
   }
   const uint32_t nwalk = ng + nbig * (ZS_SPLIT_MAX - 1u);
-  if (d64)
-    zs_k_seg_walk<true><<<nwalk, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, ng, c->gbig.as<uint32_t>(), nbig, wbits, gf,
-                                              gspb, gb, gln, gt, ge, gm, cnt + 2, c->gspl.as<uint32_t>(), c->seg_bits);
-  else
-    zs_k_seg_walk<false><<<nwalk, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, ng, c->gbig.as<uint32_t>(), nbig, wbits, gf,
-                                               gspb, gb, gln, gt, ge, gm, cnt + 2, c->gspl.as<uint32_t>(), c->seg_bits);
+  // The sync window: 2048 bits when the walks all fit the chip at once (the 2048-bit
+  // instance takes 49 KB of LDS: three per CU) and the members are large (blocks
+  // wide enough for lanes of >= 2048 bits), so that fewer neighbours fail to meet
+  // (512 x 256 KiB: 5.3 -> 4.2 ms); otherwise 1024 (occupancy: 1,024 x 256 KiB 7.6 vs 6.6 ms)
+  uint64_t gbits = 0;
+  for (uint32_t k = 0; k < ng; k++) gbits += 8ull * in_len[c->hglist[k]];
+  const bool w2k = c->seg_wide && nwalk <= 3u * c->ncu && gbits >= 65536ull * 8 * ng;
+  auto walk = d64 ? (w2k ? zs_k_seg_walk<true, 2048u> : zs_k_seg_walk<true, 1024u>)
+                  : (w2k ? zs_k_seg_walk<false, 2048u> : zs_k_seg_walk<false, 1024u>);
+  walk<<<nwalk, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, ng, c->gbig.as<uint32_t>(), nbig, wbits, gf, gspb, gb, gln, gt,
+                             ge, gm, cnt + 2, c->gspl.as<uint32_t>(), std::max<uint32_t>(c->seg_bits, w2k ? 2048u : 0u));
   if (int r = mark(c, sd, "seg_walk")) return r;
   zs_k_seg_plan<<<ng, 64, 0, sd>>>(d_in, d_ioff, d_ilen, d_ocap, gl, ng, wbits, refw ? 1 : 0, gb, gln, ge, gm,
                                    c->gpbase.as<uint32_t>(), c->gplist.as<uint4>());
@@ -1269,10 +1282,13 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       constexpr size_t kSplitScratch = 2ull << 30;
       constexpr uint32_t kPieceCapMax = 4u << 20;  // values per piece
       for (uint32_t i = 0; i < n; i++) {
-        if (in_len[i] <= big_min) continue;
+        if (!zs_inf_large(in_len[i], out_cap[i], big_min)) continue;
         // (the segmented decode keeps bit positions in 32 bits; members with long
-        // blocks of long copies -- deflate64 -- decode faster split, with a wave per block)
-        if (c->inflate_seg && in_len[i] < (1u << 29) && !(splittable && wbits == -16 && 8ull * in_len[i] > ZS_SEG_SPLIT_BITS)) {
+        // blocks or long copies -- large deflate64 ones, high expansions -- decode
+        // faster with a wave per block / per member, which copies 64 bytes at a time)
+        const bool longcopies = zs_inf_expands(in_len[i], out_cap[i]) ||
+                                (wbits == -16 && 8ull * in_len[i] > ZS_SEG_SPLIT_BITS);
+        if (c->inflate_seg && in_len[i] < (1u << 29) && !longcopies) {
           c->hglist.push_back(i);
           continue;
         }

@@ -396,10 +396,11 @@ __global__ __launch_bounds__(64) ZS_LANE_WAVES(4) void zs_k_inflate_lane(const u
   const uint32_t s = REFW && list ? list[li] : li;
   // (members of 512 MB or more too: the bookkeeping's bit positions are 32-bit; the exact path takes them)
   if (REFW && !list &&
-      (res[s].bail == 0 || out_cap[s] <= 65536u || (wave_min && in_len[s] > wave_min) || in_len[s] >= (1u << 29)))
+      (res[s].bail == 0 || out_cap[s] <= 65536u || zs_inf_large(in_len[s], out_cap[s], wave_min) ||
+       in_len[s] >= (1u << 29)))
     return;
   // a large member: the REFW instance, zs_k_inflate_wave or the split path decodes it
-  if (!REFW && wave_min && in_len[s] > wave_min) return;
+  if (!REFW && zs_inf_large(in_len[s], out_cap[s], wave_min)) return;
   zs_lane_tabs& T = tabs[s];
   zs_lane_lds& F = *reinterpret_cast<zs_lane_lds*>(LL + threadIdx.x * lstride);
   uint16_t* const lroot = ROOT ? reinterpret_cast<zs_lane_lds_root*>(&F)->lroot : nullptr;

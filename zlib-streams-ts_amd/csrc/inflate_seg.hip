@@ -232,15 +232,16 @@ static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* l
 // true stream (the lane before is confirmed, so is it).  The span ends at the
 // end-of-block code of a confirmed lane, or -- its last lane confirmed past the
 // span's nominal end -- at a symbol start, where the next span continues.
+template <uint32_t W>
 struct zs_sg_walk_lds {
   uint32_t inw[ZS_WIN_IN];
   zcode codes[ZS_SEG_TAB];
   uint16_t lens[320];
   uint16_t work[288];
-  uint32_t own[ZS_SEG_LANES][ZS_SEG_W / 32];   // each lane's symbol starts in [q, q + W)
-  uint32_t tail[ZS_SEG_LANES][ZS_SEG_W / 32];  // ... and in [q + S, q + S + W): the next lane's window
-  uint32_t okp[ZS_SEG_LANES][ZS_SEG_NCK], okc[ZS_SEG_LANES][ZS_SEG_NCK];  // checkpoints (position, count) in each
-  uint32_t tkp[ZS_SEG_LANES][ZS_SEG_NCK], tkc[ZS_SEG_LANES][ZS_SEG_NCK];
+  uint32_t own[ZS_SEG_LANES][W / 32];   // each lane's symbol starts in [q, q + W)
+  uint32_t tail[ZS_SEG_LANES][W / 32];  // ... and in [q + S, q + S + W): the next lane's window
+  uint32_t okp[ZS_SEG_LANES][W / ZS_SEG_CKB], okc[ZS_SEG_LANES][W / ZS_SEG_CKB];  // checkpoints (position, count) in each
+  uint32_t tkp[ZS_SEG_LANES][W / ZS_SEG_CKB], tkc[ZS_SEG_LANES][W / ZS_SEG_CKB];
   uint32_t sync[ZS_SEG_LANES];  // lane j's start on the true stream: the first start it shares with lane j - 1
   uint32_t send;
 };
@@ -266,8 +267,8 @@ struct zs_sg_walk_lds {
 #define ZS_SG_K_NONE 0u
 #define ZS_SG_K_BEND 2u
 #define ZS_SG_K_CONT 4u
-template <bool D64>
-static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uint32_t n, uint32_t sym0, uint32_t pe0,
+template <bool D64, uint32_t W>
+static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, uint32_t n, uint32_t sym0, uint32_t pe0,
                                       uint32_t nl, uint32_t S, uint32_t lbits, uint32_t dbits, uint32_t dofs,
                                       zs_seg_lane* __restrict__ recs, uint32_t& send, bool& bad_out) {
   const uint32_t lane = threadIdx.x;
@@ -280,12 +281,12 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
   const bool on = lane < nl;
   const bool lastl = lane + 1u == nl;
   const uint32_t q = sym0 + lane * S, qn = q + S;
-  const uint32_t lim = !on ? q : !lastl ? qn + ZS_SEG_W : cont_ok ? nend : nbits + 64u;
-  for (uint32_t i = 0; i < ZS_SEG_W / 32; i++) {
+  const uint32_t lim = !on ? q : !lastl ? qn + W : cont_ok ? nend : nbits + 64u;
+  for (uint32_t i = 0; i < W / 32; i++) {
     L.own[lane][i] = 0;
     L.tail[lane][i] = 0;
   }
-  for (uint32_t i = 0; i < ZS_SEG_NCK; i++) {
+  for (uint32_t i = 0; i < (W / ZS_SEG_CKB); i++) {
     L.okp[lane][i] = ZS_SEG_NONE;
     L.tkp[lane][i] = ZS_SEG_NONE;
   }
@@ -307,9 +308,9 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
 #pragma unroll
   for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) eob_sb[e] = eob_end[e] = eob_cum[e] = bad_sb[e] = 0;
   uint32_t ock = 0, tck = 0;  // checkpoint buckets filled
-  // the bitmaps' current word (own words 0 .., tail words ZS_SEG_W / 32 ..) collects
+  // the bitmaps' current word (own words 0 .., tail words W / 32 ..) collects
   // in a register: positions only grow, so each word is stored once
-  constexpr uint32_t NW = ZS_SEG_W / 32u;
+  constexpr uint32_t NW = W / 32u;
   uint32_t aw = ZS_SEG_NONE, acc = 0;
   auto put_word = [&]() {
     if (aw < NW) L.own[lane][aw] = acc;
@@ -325,14 +326,14 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
   };
   while (pos < lim) {
     const uint32_t off = pos - q, toff = pos - qn;
-    if (off < ZS_SEG_W) {
+    if (off < W) {
       mark(off >> 5, off & 31u);
       if (off >= ock * ZS_SEG_CKB) {
         L.okp[lane][off / ZS_SEG_CKB] = pos;
         L.okc[lane][off / ZS_SEG_CKB] = cum;
         ock = off / ZS_SEG_CKB + 1u;
       }
-    } else if (toff < ZS_SEG_W) {
+    } else if (toff < W) {
       mark(NW + (toff >> 5), toff & 31u);
       if (toff >= tck * ZS_SEG_CKB) {
         L.tkp[lane][toff / ZS_SEG_CKB] = pos;
@@ -343,7 +344,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
     const uint32_t sb = pos;
     const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
     if (y.kind == ZS_SG_BAD) {
-      if (sb - q < ZS_SEG_W) {
+      if (sb - q < W) {
 #pragma unroll
         for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
           if (e == (nbad & (ZS_SEG_NEOB - 1u))) bad_sb[e] = sb;
@@ -373,7 +374,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
       bd += 262144u;
     }
     if (y.kind == ZS_SG_EOB) {
-      if (sb - q < ZS_SEG_W) {
+      if (sb - q < W) {
 #pragma unroll
         for (uint32_t e = 0; e < ZS_SEG_NEOB; e++)
           if (e == (neob & (ZS_SEG_NEOB - 1u))) {
@@ -400,7 +401,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
   // ---- 2. each lane's true start: the first start in its window lane - 1 shares
   uint32_t sp = lane == 0 ? sym0 : ZS_SEG_NONE;
   if (on && lane) {
-    for (uint32_t i = 0; i < ZS_SEG_W / 32; i++) {
+    for (uint32_t i = 0; i < W / 32; i++) {
       const uint32_t x = L.tail[lane - 1u][i] & L.own[lane][i];
       if (x) {
         sp = q + 32u * i + (uint32_t)__builtin_ctz(x);
@@ -449,7 +450,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
     const uint32_t end = lane == JE ? eend : nxs;
     // the output count at the start: from the last own checkpoint at or before it
     uint32_t cp = q, cc = 0;
-    for (uint32_t c = 0; c < ZS_SEG_NCK; c++) {
+    for (uint32_t c = 0; c < (W / ZS_SEG_CKB); c++) {
       const uint32_t p = L.okp[lane][c];
       if (p != ZS_SEG_NONE && p <= start) {
         cp = p;
@@ -467,7 +468,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
     uint32_t tp = qn, tc = 0;
     bool tfound = false;
     if (redo_end)
-      for (uint32_t c = 0; c < ZS_SEG_NCK; c++) {
+      for (uint32_t c = 0; c < (W / ZS_SEG_CKB); c++) {
         const uint32_t p = L.tkp[lane][c];
         if (p != ZS_SEG_NONE && p <= end) {
           tp = p;
@@ -539,7 +540,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds& L, const uint8_t* src, uin
   return kind;
 }
 
-template <bool D64>
+template <bool D64, uint32_t W>
 __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                     const uint32_t* __restrict__ in_len,
                                                     const uint32_t* __restrict__ list, uint32_t n_list,
@@ -550,7 +551,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
                                                     zs_seg_ent* __restrict__ ents, zs_seg_mem* __restrict__ mem,
                                                     uint32_t* __restrict__ nspan, uint32_t* __restrict__ spans,
                                                     uint32_t sbits) {
-  __shared__ zs_sg_walk_lds L;
+  __shared__ zs_sg_walk_lds<W> L;
   const uint32_t lane = threadIdx.x;
   // the entry: blocks [0, n_list): entry 0 of list member blockIdx.x; then
   // (ZS_SPLIT_MAX - 1) entries per big member
@@ -660,7 +661,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
       const uint32_t nl = max(1u, min(ZS_SEG_LANES, (nbits - cur + S - 1u) / S));
       uint32_t send = 0;
       bool sbad = false;
-      const uint32_t k = zs_sg_span<D64>(L, src, n, cur, pe0, nl, S, lbits, dbits, dofs,
+      const uint32_t k = zs_sg_span<D64, W>(L, src, n, cur, pe0, nl, S, lbits, dbits, dofs,
                                          lanes + (size_t)b * ZS_SEG_LANES, send, sbad);
       if (lane == 0) {
         zs_seg_blk& Bk = blk[b];
@@ -693,7 +694,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
     }
     if (!good) break;
     // ---- the block ended at cur: the final one, or at a later entry's start
-    S = min(ZS_SEG_SMAX, max(ZS_SEG_W, (cur - hdr) / 60u));
+    S = min(ZS_SEG_SMAX, max(W, (cur - hdr) / 60u));
     hdr = cur;
     if (last) {
       flags_e = 3u;
@@ -911,6 +912,9 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
 }
 
 // ----------------------------------------------------------------- decode
+#ifndef ZS_SG_RING
+#define ZS_SG_RING 64u  // u16 values of a lane's LDS output ring (a power of two >= 64)
+#endif
 // One lane's u16 output (bytes, or markers 255 + k: the value k positions
 // before the piece): a 64-value LDS ring, whole 16-byte units to HBM (the
 // piece's scratch is 16-byte aligned and padded, so no unit is shared).
@@ -919,28 +923,33 @@ struct zs_sg_out {
   uint16_t* ring;
   uint32_t P, F;
   __device__ __forceinline__ void put(uint32_t v) {
-    ring[P & 63u] = (uint16_t)v;
+    ring[P & (ZS_SG_RING - 1u)] = (uint16_t)v;
     P++;
   }
   __device__ __forceinline__ void flush() {
     while (F + 8u <= P) {
-      *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & 63u));
+      *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & (ZS_SG_RING - 1u)));
       F += 8u;
     }
   }
   __device__ __forceinline__ void room(uint32_t k) {  // room for k more values
-    if (P + k - F > 64u) flush();
+    if (P + k - F > ZS_SG_RING) flush();
   }
   // the value at piece position x < P: the ring holds the last 64, older ones are stored
 #if ZS_SEG_EXP & 1
   uint32_t far = 0;
-  __device__ __forceinline__ uint32_t get(uint32_t x) { far += x + 64u < P; return x + 64u >= P ? ring[x & 63u] : dst[x]; }
+  __device__ __forceinline__ uint32_t get(uint32_t x) {
+    far += x + ZS_SG_RING < P;
+    return x + ZS_SG_RING >= P ? ring[x & (ZS_SG_RING - 1u)] : dst[x];
+  }
 #else
-  __device__ __forceinline__ uint32_t get(uint32_t x) const { return x + 64u >= P ? ring[x & 63u] : dst[x]; }
+  __device__ __forceinline__ uint32_t get(uint32_t x) const {
+    return x + ZS_SG_RING >= P ? ring[x & (ZS_SG_RING - 1u)] : dst[x];
+  }
 #endif
   __device__ __forceinline__ void finish() {
     flush();
-    if (F < P) *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & 63u));
+    if (F < P) *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & (ZS_SG_RING - 1u)));
   }
 };
 
@@ -1015,7 +1024,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
                                                       const uint64_t* __restrict__ sbase,
                                                       uint16_t* __restrict__ scratch) {
   __shared__ zcode codes[ZS_SEG_TAB];
-  __shared__ __attribute__((aligned(16))) uint16_t ring[ZS_SEG_LANES][64];
+  __shared__ __attribute__((aligned(16))) uint16_t ring[ZS_SEG_LANES][ZS_SG_RING];
   const uint32_t lane = threadIdx.x;
   const uint32_t ns = *nspan;
   for (uint32_t k = blockIdx.x; k < ns; k += gridDim.x) {
@@ -1064,7 +1073,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
   bool bad = false;
   uint32_t sb = p.start;
   while (sb < dend) {
-    if (W.P - W.F >= 32u) W.flush();
+    if (W.P - W.F >= ZS_SG_RING / 2u) W.flush();
     const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
     const uint32_t o = O + W.P;
 #if ZS_SEG_EXP & 1
@@ -1236,14 +1245,15 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
   }
 }
 
-template __global__ void zs_k_seg_walk<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,
-                                              uint32_t, const uint32_t*, uint32_t, int, const uint64_t*,
-                                              const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*, zs_seg_ent*,
-                                              zs_seg_mem*, uint32_t*, uint32_t*, uint32_t);
-template __global__ void zs_k_seg_walk<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,
-                                             uint32_t, const uint32_t*, uint32_t, int, const uint64_t*,
-                                             const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*, zs_seg_ent*,
-                                             zs_seg_mem*, uint32_t*, uint32_t*, uint32_t);
+#define ZS_SEG_WALK_INST(D, W)                                                                                     \
+  template __global__ void zs_k_seg_walk<D, W>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,  \
+                                               uint32_t, const uint32_t*, uint32_t, int, const uint64_t*,          \
+                                               const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*, zs_seg_ent*,    \
+                                               zs_seg_mem*, uint32_t*, uint32_t*, uint32_t);
+ZS_SEG_WALK_INST(false, 1024u)
+ZS_SEG_WALK_INST(true, 1024u)
+ZS_SEG_WALK_INST(false, 2048u)
+ZS_SEG_WALK_INST(true, 2048u)
 #define ZS_SEG_DEC_INST(D, W)                                                                                       \
   template __global__ void zs_k_seg_decode<D, W>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, \
                                                  const uint32_t*, const uint32_t*, const zs_seg_blk*,              \

@@ -54,6 +54,17 @@ struct zs_lane_res {
 __global__ void zs_k_inflate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,
                              const uint64_t* out_off, const uint32_t* out_cap, int wbits, zs_inflate_result* res,
                              const zs_lane_res* only, int flags);
+// A member the lane kernel leaves to the large-member paths (the segmented, split
+// or wave decode) when wave_min is set: more input bytes than wave_min, or a high
+// expansion (a cap past 64 KiB and at least 8 bytes of it per input byte: long
+// copies, which one lane makes byte by byte -- deflate64's zeros_100k.deflate64 took a
+// lane 4.3 ms; the wave decoders copy 64 bytes at a time)
+static __host__ __device__ inline bool zs_inf_expands(uint32_t in_len, uint32_t out_cap) {
+  return out_cap > 65536u && out_cap / 8u >= in_len;
+}
+static __host__ __device__ inline bool zs_inf_large(uint32_t in_len, uint32_t out_cap, uint32_t wave_min) {
+  return wave_min && (in_len > wave_min || zs_inf_expands(in_len, out_cap));
+}
 struct zs_lane_tabs;
 template <int RT, bool REFW>
 __global__ void zs_k_inflate_lane(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint8_t* out,

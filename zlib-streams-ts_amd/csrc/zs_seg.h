@@ -8,11 +8,9 @@
 #include "zs_split.h"
 
 #define ZS_SEG_LANES 64u    // pieces per span (one lane each)
-#ifndef ZS_SEG_W
-#define ZS_SEG_W 1024u  // bits of a lane's start window whose symbol starts it records (the sync bitmaps)
-#endif
+#define ZS_SEG_W 1024u      // bits of a lane's start window whose symbol starts it records (the sync bitmaps; 2048 in
+                            // the walk instance for batches of few large members: fewer chains that do not meet)
 #define ZS_SEG_CKB 128u     // spacing of a lane's (position, output count) checkpoints in its window
-#define ZS_SEG_NCK (ZS_SEG_W / ZS_SEG_CKB)
 #define ZS_SEG_NEV 4u       // sub-chunk crossing events a lane records
 #define ZS_SEG_NEOB 4u      // end-of-block codes a lane logs
 #define ZS_SEG_PAD 16u      // u16 values of padding behind each piece's scratch
@@ -71,7 +69,7 @@ struct zs_seg_mem {
   uint32_t pad[2];
 };
 
-template <bool D64>
+template <bool D64, uint32_t W>  // W: the sync window (1024, or 2048 for a batch of few large members)
 __global__ void zs_k_seg_walk(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* list,
                               uint32_t n_list, const uint32_t* big, uint32_t n_big, int wbits, const uint64_t* found,
                               const uint32_t* spb, zs_seg_blk* blk, zs_seg_lane* lanes, zcode* tcache,
