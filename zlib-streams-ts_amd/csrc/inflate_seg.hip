@@ -243,6 +243,7 @@ struct zs_sg_walk_lds {
   uint32_t okp[ZS_SEG_LANES][W / ZS_SEG_CKB], okc[ZS_SEG_LANES][W / ZS_SEG_CKB];  // checkpoints (position, count) in each
   uint32_t tkp[ZS_SEG_LANES][W / ZS_SEG_CKB], tkc[ZS_SEG_LANES][W / ZS_SEG_CKB];
   uint32_t sync[ZS_SEG_LANES];  // lane j's start on the true stream: the first start it shares with lane j - 1
+  uint32_t odone[ZS_SEG_LANES];  // words of own[j] complete (lane j has moved past them)
   uint32_t send;
 };
 
@@ -290,6 +291,10 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
     L.okp[lane][i] = ZS_SEG_NONE;
     L.tkp[lane][i] = ZS_SEG_NONE;
   }
+  L.odone[lane] = 0;
+  volatile uint32_t* const vodone = L.odone;
+  volatile uint32_t* const vown_next = lane + 1u < nl ? L.own[lane + 1u] : L.own[lane];
+  bool left_own = false;
   // ---- 1. the lane's own decode
   zs_sg_reader G;
   zs_sg_init(G, src, n);
@@ -319,6 +324,10 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
   auto mark = [&](uint32_t w, uint32_t bit) {
     if (w != aw) {
       put_word();
+      if (w < NW) {  // own words below w are final: the lane before may stop on them
+        asm volatile("" ::: "memory");
+        vodone[lane] = w;
+      }
       aw = w;
       acc = 0;
     }
@@ -333,12 +342,24 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
         L.okc[lane][off / ZS_SEG_CKB] = cum;
         ock = off / ZS_SEG_CKB + 1u;
       }
-    } else if (toff < W) {
-      mark(NW + (toff >> 5), toff & 31u);
-      if (toff >= tck * ZS_SEG_CKB) {
-        L.tkp[lane][toff / ZS_SEG_CKB] = pos;
-        L.tkc[lane][toff / ZS_SEG_CKB] = cum;
-        tck = toff / ZS_SEG_CKB + 1u;
+    } else {
+      if (!left_own) {  // own[] complete
+        put_word();
+        aw = ZS_SEG_NONE;
+        asm volatile("" ::: "memory");
+        vodone[lane] = NW;
+        left_own = true;
+      }
+      if (toff < W) {
+        mark(NW + (toff >> 5), toff & 31u);
+        if (toff >= tck * ZS_SEG_CKB) {
+          L.tkp[lane][toff / ZS_SEG_CKB] = pos;
+          L.tkc[lane][toff / ZS_SEG_CKB] = cum;
+          tck = toff / ZS_SEG_CKB + 1u;
+        }
+        // a start the next lane has recorded (its window complete): the two meet here
+        // or earlier (step 2 finds the first), the rest of the tail is not needed
+        if (lane + 1u < nl && (toff >> 5) < vodone[lane + 1u] && ((vown_next[toff >> 5] >> (toff & 31u)) & 1u)) break;
       }
     }
     const uint32_t sb = pos;
@@ -956,6 +977,22 @@ struct zs_sg_out {
 // n values from piece position x0 (negative: markers for the history before
 // the piece); false: a marker further back than a u16 says
 static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint32_t n) {
+  if (x0 < 0) {
+    // the part before the piece: markers 255 + k, k falling by one per value (the
+    // first, the furthest back, must fit a u16), eight per round
+    const uint32_t back = (uint32_t)(-x0);
+    if (back > ZS_SPLIT_MARK_MAX) return false;
+    const uint32_t m = min(n, back);
+    for (uint32_t i = 0; i < m; i += 8) {
+      W.room(8);
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++)
+        if (i + j < m) W.put(255u + back - (i + j));
+    }
+    if (m == n) return true;
+    n -= m;
+    x0 = 0;
+  }
   const int32_t d = (int32_t)W.P - x0;
   if (x0 >= 0 && d >= 8) {
     for (uint32_t i = 0; i < n; i += 8) {
@@ -985,20 +1022,7 @@ static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint
     }
     return true;
   }
-  for (uint32_t i = 0; i < n; i++) {
-    const int32_t x = x0 + (int32_t)i;
-    uint32_t v;
-    if (x < 0) {
-      const uint32_t back = (uint32_t)(-x);
-      if (back > ZS_SPLIT_MARK_MAX) return false;
-      v = 255u + back;
-    } else {
-      v = W.get((uint32_t)x);
-    }
-    if ((i & 7u) == 0) W.room(8);
-    W.put(v);
-  }
-  return true;
+  return true;  // (x0 >= 0 here: one of the two paths above)
 }
 
 #ifndef ZS_SEG_EXP
