@@ -232,16 +232,25 @@ static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* l
 // true stream (the lane before is confirmed, so is it).  The span ends at the
 // end-of-block code of a confirmed lane, or -- its last lane confirmed past the
 // span's nominal end -- at a symbol start, where the next span continues.
+// (a checkpoint: the position's offset in its window | the lane's output count << 12;
+// a count past 2^20 -- garbage only -- comes out wrong, which the decode's count check catches)
+#define ZS_SG_CK(off, cum) ((off) | ((cum) << 12))
 template <uint32_t W>
 struct zs_sg_walk_lds {
-  uint32_t inw[ZS_WIN_IN];
   zcode codes[ZS_SEG_TAB];
-  uint16_t lens[320];
-  uint16_t work[288];
-  uint32_t own[ZS_SEG_LANES][W / 32];   // each lane's symbol starts in [q, q + W)
-  uint32_t tail[ZS_SEG_LANES][W / 32];  // ... and in [q + S, q + S + W): the next lane's window
-  uint32_t okp[ZS_SEG_LANES][W / ZS_SEG_CKB], okc[ZS_SEG_LANES][W / ZS_SEG_CKB];  // checkpoints (position, count) in each
-  uint32_t tkp[ZS_SEG_LANES][W / ZS_SEG_CKB], tkc[ZS_SEG_LANES][W / ZS_SEG_CKB];
+  union {
+    struct {  // a block header (between spans)
+      uint32_t inw[ZS_WIN_IN];
+      uint16_t lens[320];
+      uint16_t work[288];
+    } h;
+    struct {  // a span
+      uint32_t own[ZS_SEG_LANES][W / 32];   // each lane's symbol starts in [q, q + W)
+      uint32_t tail[ZS_SEG_LANES][W / 32];  // ... and in [q + S, q + S + W): the next lane's window
+      uint32_t ock[ZS_SEG_LANES][W / ZS_SEG_CKB];  // checkpoints in each (ZS_SG_CK)
+      uint32_t tck[ZS_SEG_LANES][W / ZS_SEG_CKB];
+    } s;
+  };
   uint32_t sync[ZS_SEG_LANES];  // lane j's start on the true stream: the first start it shares with lane j - 1
   uint32_t odone[ZS_SEG_LANES];  // words of own[j] complete (lane j has moved past them)
   uint32_t send;
@@ -284,16 +293,16 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
   const uint32_t q = sym0 + lane * S, qn = q + S;
   const uint32_t lim = !on ? q : !lastl ? qn + W : cont_ok ? nend : nbits + 64u;
   for (uint32_t i = 0; i < W / 32; i++) {
-    L.own[lane][i] = 0;
-    L.tail[lane][i] = 0;
+    L.s.own[lane][i] = 0;
+    L.s.tail[lane][i] = 0;
   }
   for (uint32_t i = 0; i < (W / ZS_SEG_CKB); i++) {
-    L.okp[lane][i] = ZS_SEG_NONE;
-    L.tkp[lane][i] = ZS_SEG_NONE;
+    L.s.ock[lane][i] = ZS_SEG_NONE;
+    L.s.tck[lane][i] = ZS_SEG_NONE;
   }
   L.odone[lane] = 0;
   volatile uint32_t* const vodone = L.odone;
-  volatile uint32_t* const vown_next = lane + 1u < nl ? L.own[lane + 1u] : L.own[lane];
+  volatile uint32_t* const vown_next = lane + 1u < nl ? L.s.own[lane + 1u] : L.s.own[lane];
   bool left_own = false;
   // ---- 1. the lane's own decode
   zs_sg_reader G;
@@ -318,8 +327,8 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
   constexpr uint32_t NW = W / 32u;
   uint32_t aw = ZS_SEG_NONE, acc = 0;
   auto put_word = [&]() {
-    if (aw < NW) L.own[lane][aw] = acc;
-    else if (aw != ZS_SEG_NONE) L.tail[lane][aw - NW] = acc;
+    if (aw < NW) L.s.own[lane][aw] = acc;
+    else if (aw != ZS_SEG_NONE) L.s.tail[lane][aw - NW] = acc;
   };
   auto mark = [&](uint32_t w, uint32_t bit) {
     if (w != aw) {
@@ -338,8 +347,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
     if (off < W) {
       mark(off >> 5, off & 31u);
       if (off >= ock * ZS_SEG_CKB) {
-        L.okp[lane][off / ZS_SEG_CKB] = pos;
-        L.okc[lane][off / ZS_SEG_CKB] = cum;
+        L.s.ock[lane][off / ZS_SEG_CKB] = ZS_SG_CK(off, cum);
         ock = off / ZS_SEG_CKB + 1u;
       }
     } else {
@@ -353,8 +361,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
       if (toff < W) {
         mark(NW + (toff >> 5), toff & 31u);
         if (toff >= tck * ZS_SEG_CKB) {
-          L.tkp[lane][toff / ZS_SEG_CKB] = pos;
-          L.tkc[lane][toff / ZS_SEG_CKB] = cum;
+          L.s.tck[lane][toff / ZS_SEG_CKB] = ZS_SG_CK(toff, cum);
           tck = toff / ZS_SEG_CKB + 1u;
         }
         // a start the next lane has recorded (its window complete): the two meet here
@@ -423,7 +430,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
   uint32_t sp = lane == 0 ? sym0 : ZS_SEG_NONE;
   if (on && lane) {
     for (uint32_t i = 0; i < W / 32; i++) {
-      const uint32_t x = L.tail[lane - 1u][i] & L.own[lane][i];
+      const uint32_t x = L.s.tail[lane - 1u][i] & L.s.own[lane][i];
       if (x) {
         sp = q + 32u * i + (uint32_t)__builtin_ctz(x);
         break;
@@ -472,10 +479,10 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
     // the output count at the start: from the last own checkpoint at or before it
     uint32_t cp = q, cc = 0;
     for (uint32_t c = 0; c < (W / ZS_SEG_CKB); c++) {
-      const uint32_t p = L.okp[lane][c];
-      if (p != ZS_SEG_NONE && p <= start) {
+      const uint32_t v = L.s.ock[lane][c], p = q + (v & 0xfffu);
+      if (v != ZS_SEG_NONE && p <= start) {
         cp = p;
-        cc = L.okc[lane][c];
+        cc = v >> 12;
       }
     }
     // ... and at the end: the end-of-block code's, the stop's, or from the last tail
@@ -490,10 +497,10 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
     bool tfound = false;
     if (redo_end)
       for (uint32_t c = 0; c < (W / ZS_SEG_CKB); c++) {
-        const uint32_t p = L.tkp[lane][c];
-        if (p != ZS_SEG_NONE && p <= end) {
+        const uint32_t v = L.s.tck[lane][c], p = qn + (v & 0xfffu);
+        if (v != ZS_SEG_NONE && p <= end) {
           tp = p;
-          tc = L.tkc[lane][c];
+          tc = v >> 12;
           tfound = true;
         }
       }
@@ -618,7 +625,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
   R.sh = (uint32_t)((uintptr_t)src & 3u);
   R.w4 = reinterpret_cast<const uint32_t*>(src - R.sh);
   R.last = (R.sh + n - 1u) >> 2;
-  R.inw = L.inw;
+  R.inw = L.h.inw;
   zs_wr_stage(R, ((start >> 3) + R.sh) >> 2);
   zs_wr_seek(R, start >> 3);
   zs_wr_take(R, start & 7u);
@@ -647,13 +654,13 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
   uint32_t S = sbits;
   while (good) {
     // ---- a block: its header (wave-uniform) and tables
-    if (hdr != (uint32_t)zs_wr_bitpos(R)) {
+    if (prevb != ZS_SEG_NONE || hdr != (uint32_t)zs_wr_bitpos(R)) {  // (a span has reused the staging LDS)
       zs_wr_stage(R, ((hdr >> 3) + R.sh) >> 2);
       zs_wr_seek(R, hdr >> 3);
       zs_wr_take(R, hdr & 7u);
     }
     uint32_t last = 0, lbits = 0, dbits = 0, dofs = 0, ntab = 0;
-    good = zs_sg_header(R, L.codes, L.lens, L.work, D64, last, lbits, dbits, dofs, ntab);
+    good = zs_sg_header(R, L.codes, L.h.lens, L.h.work, D64, last, lbits, dbits, dofs, ntab);
     const uint32_t sym0 = (uint32_t)zs_wr_bitpos(R);
     if (good && sym0 > nbits) good = false;
     if (!good) break;
