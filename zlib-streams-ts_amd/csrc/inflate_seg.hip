@@ -1014,18 +1014,33 @@ static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint
     }
     return true;
   }
-  if (x0 >= 0) {  // period d < 8
+  if (x0 >= 0) {  // period d < 8: the first dd = d * ceil(8 / d) values one by one, then a
+                  // copy from dd back (the pattern repeats at dd >= 8 too), eight per round
+    const uint32_t dd = (uint32_t)d * ((8u + (uint32_t)d - 1u) / (uint32_t)d);
+    const uint32_t first = min(n, dd);
     uint32_t v[8];
 #pragma unroll
     for (uint32_t j = 0; j < 8; j++) v[j] = (int32_t)j < d ? W.get((uint32_t)x0 + j) : 0u;
     uint32_t j = 0;
-    for (uint32_t i = 0; i < n; i++) {
-      if ((i & 7u) == 0) W.room(8);
+    W.room(16);
+    for (uint32_t i = 0; i < first; i++) {
       uint32_t x = v[0];
 #pragma unroll
       for (uint32_t t = 1; t < 8; t++) x = t == j ? v[t] : x;
       W.put(x);
       j = j + 1 == (uint32_t)d ? 0u : j + 1;
+    }
+    const uint32_t rest = n - first;
+    const uint32_t xs = W.P - dd;
+    for (uint32_t i = 0; i < rest; i += 8) {
+      W.room(8);
+      uint32_t u[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) u[k] = W.get(xs + i + k);
+      const uint32_t k8 = min(8u, rest - i);
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++)
+        if (k < k8) W.put(u[k]);
     }
     return true;
   }
