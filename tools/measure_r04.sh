@@ -3,7 +3,7 @@
 # BASELINE config's bench line (inflate configs with their per-rank shard sweeps),
 # rocprofv3 kernel trace + FETCH/WRITE passes and SQ passes.  Logs under $1; copy
 # the summaries into profiles/r04/ with tools/collect_r04.sh.
-# usage: tools/measure_r04.sh OUTDIR [tests|benches|ibenches|dbenches|profiles|sq|all]...
+# usage: tools/measure_r04.sh OUTDIR [tests|benches|ibenches|dbenches|profiles[12]|sq[12]|all]...
 set -u
 OUT=$1; shift
 WHAT=${*:-all}
@@ -40,20 +40,28 @@ run c5_gzip_l6 200 python3 bench.py $C5G --no-shard-sweep --no-e2e
 run c4_l9 300 python3 bench.py $C4L9 --no-shard-sweep --no-e2e
 run c4_l1 300 python3 bench.py $C4L1 --no-shard-sweep --no-e2e
 fi
-if want profiles; then
+if want profiles || want profiles1; then
 run prof_c2 300 tools/profile.sh "$OUT/prof_c2"
 run prof_c3 300 tools/profile.sh "$OUT/prof_c3" $C3
 run prof_c4_decode 300 tools/profile.sh "$OUT/prof_c4_decode" $C4D
 run prof_c5_gunzip 300 tools/profile.sh "$OUT/prof_c5_gunzip" $C5I
+fi
+if want profiles || want profiles2; then
 run prof_c5_d64 300 tools/profile.sh "$OUT/prof_c5_d64" $C5D
 run prof_c5_gzip_l6 300 tools/profile.sh "$OUT/prof_c5_gzip_l6" $C5G
 run prof_c4_l9 300 tools/profile.sh "$OUT/prof_c4_l9" $C4L9
 run prof_c4_l1 300 tools/profile.sh "$OUT/prof_c4_l1" $C4L1
 fi
-if want sq; then
+if want sq || want sq1; then
 run sq_c2 500 tools/pmc_sq.sh "$OUT/sq_c2"
 run sq_c3 500 tools/pmc_sq.sh "$OUT/sq_c3" $C3
 run sq_c4_decode 500 tools/pmc_sq.sh "$OUT/sq_c4_decode" $C4D
 run sq_c5_gunzip 500 tools/pmc_sq.sh "$OUT/sq_c5_gunzip" $C5I
+fi
+if want sq || want sq2; then
+run sq_c5_d64 500 tools/pmc_sq.sh "$OUT/sq_c5_d64" $C5D
+run sq_c5_gzip_l6 500 tools/pmc_sq.sh "$OUT/sq_c5_gzip_l6" $C5G
+run sq_c4_l9 500 tools/pmc_sq.sh "$OUT/sq_c4_l9" $C4L9
+run sq_c4_l1 500 tools/pmc_sq.sh "$OUT/sq_c4_l1" $C4L1
 fi
 echo measure-done
