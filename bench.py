@@ -710,6 +710,8 @@ def main_inflate(args):
                                lambda m: oracle.decompress(m, dec_fmt, cap=L), L, N, key)
         name = {"deflate64-raw": "deflate64-raw decode (C5-ii)", "gzip": "gunzip + crc32 (C5-i)"}.get(
             dec_fmt, "inflate %s L6 members (C3)" % dec_fmt)
+        if dec_fmt == "deflate-raw" and L == 262144:  # the C4 streams decoded back (reference-exact)
+            name = "inflate deflate-raw L6, %d x 256 KiB members (C4 decoded back)" % N_glob
         line = {
             "metric": "uncompressed MB/s, %s" % name,
             "value": round(out_total / (elapsed / args.steps) / 1e6, 2), "unit": "MB/s", "n_gpus": D.world,
