@@ -235,7 +235,19 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * waves per stream of the levels 4..9 lazy parse (two: 512-position segments,
  * two rounds' speculative passes at once);
  * "fast_group" (default 1): levels 1..3 replay deflate_fast a group of 64
- * positions at a time from speculative per-lane chain walks (0: step by step).
+ * positions at a time from speculative per-lane chain walks (0: step by step);
+ * "lane_order" (default 1 when the self-test passes, else 0 and 1 is refused):
+ * the chain builders rank equal hashes by same-address LDS atomics applying in
+ * lane order (1) or by ballots (0);
+ * "inflate_seg" (default 1): batches of at most "seg_small_batch" (default
+ * 16,384) members decode every member with more than "seg_small_min" (default
+ * 4096) input bytes -- and, in any batch, every member over inflate_wave_min --
+ * by the segmented decode (inflate_seg.hip: blocks walked in order, each cut
+ * across 64 lanes, the reference's calls tracked per piece); large deflate64
+ * members and high-expansion members (cap > 64 KiB, >= 8 output bytes per
+ * input byte) take the split / wave decoders instead; "seg_bits" (1024..8192,
+ * default 2048): input bits per lane of an entry's first block; "seg_wide"
+ * (default 1): the 2048-bit sync window for a batch of few large members.
  * These options never change output bytes.  "inflate_ref_wrap" (default 1)
  * does: 1 reproduces the reference's inflate_fast window-wrap copy
  * (inffast.ts:133-147), which changes the output of members whose match

@@ -277,6 +277,7 @@ def test_large_members_decode_as_the_reference(engine):
     assert min(len(c) for c in comps) > 32768
     outs = engine.decompress_batch(comps, "deflate-raw", [L] * N)
     assert engine.last_lane_count() == N
+    assert engine.last_seg_count() == N  # every member finished by the segmented decode (inflate_seg.hip)
     drecs = golden_io.batch("t256_l6_raw_dec")
     assert all((len(o), hashlib.sha256(o).digest()[:16]) == drecs[i] for i, o in enumerate(outs))
     changed = [i for i in range(N) if outs[i] != srcs[i]]
@@ -314,6 +315,7 @@ def test_large_member_shard_decodes_as_the_reference(engine, n):
     srcs, comps = _t256_l6_raw(engine, 0, n)
     outs = engine.decompress_batch(comps, "deflate-raw", [L] * n)
     assert engine.last_lane_count() == n
+    assert engine.last_seg_count() == n  # the segmented decode finished every member
     drecs = golden_io.batch("t256_l6_raw_dec")[:n]
     bad = [i for i, o in enumerate(outs) if (len(o), hashlib.sha256(o).digest()[:16]) != drecs[i]]
     assert not bad, bad[:10]

@@ -1,0 +1,4 @@
+L="zlib-streams-ts_amd/libzsgpu.so variants/r32/libzsgpu.so"
+bash tools/dbg/lib_ab.sh "--mode inflate --stream-bytes 262144 --replicas 1 --corpus text --streams 4096" $L
+bash tools/dbg/lib_ab.sh "--mode inflate --stream-bytes 262144 --replicas 1 --corpus text --streams 512" $L
+bash tools/dbg/lib_ab.sh "--mode inflate --format gzip --replicas 1 --streams 8192" $L

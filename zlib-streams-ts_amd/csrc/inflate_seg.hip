@@ -941,10 +941,13 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
 
 // ----------------------------------------------------------------- decode
 #ifndef ZS_SG_RING
-#define ZS_SG_RING 64u  // u16 values of a lane's LDS output ring (a power of two >= 64)
+#define ZS_SG_RING 32u  // u16 values of a lane's LDS output ring (a power of two; 32 vs 64: 10 instead of 14 KB of
+                        // LDS per wave, C5-i 11.0 -> 10.2 ms)
 #endif
+// room(k) flushes whole 8-value units: up to 7 values stay, so k + 7 must fit (the largest k is 16)
+static_assert(ZS_SG_RING >= 16u + 7u && (ZS_SG_RING & (ZS_SG_RING - 1u)) == 0, "decode ring too small");
 // One lane's u16 output (bytes, or markers 255 + k: the value k positions
-// before the piece): a 64-value LDS ring, whole 16-byte units to HBM (the
+// before the piece): a ZS_SG_RING-value LDS ring, whole 16-byte units to HBM (the
 // piece's scratch is 16-byte aligned and padded, so no unit is shared).
 struct zs_sg_out {
   uint16_t* dst;
