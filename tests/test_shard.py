@@ -42,6 +42,31 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _gz_members():
+    return [oracle.compress(x, 6, "gzip")[1] for x in _inputs()]
+
+
+def _decode_worker(rank, world, port, q):
+    """The decode flow of bench.py's C4/C5 lines at world size 3: each rank
+    gunzips its shard; one batch of 9 members and one of 2 members (rank 2's
+    shard is empty, so it joins the collectives with zero-length tensors)."""
+    import torch.distributed as dist
+    import zsamd.shard as shard
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dec = lambda xs: [oracle.decompress(x, "gzip")[1] for x in xs]
+        got = []
+        for members in (_gz_members(), _gz_members()[:2]):
+            outs, sizes, offs, joined = shard.compress_sharded(members, dec, gather_to=world - 1)
+            got.append(([len(o) for o in outs], sizes.tolist(), offs.tolist(), joined))
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
 def test_shard_ranges_cover_batch():
     import zsamd.shard as shard
 
@@ -72,3 +97,27 @@ def test_two_rank_gloo_batch_equals_single_process():
         assert local == ref_sizes[lo:hi]
         assert sizes == ref_sizes and offs == ref_offs
         assert joined == (b"".join(ref) if rank == 0 else None)
+
+
+def test_three_rank_gloo_decode_equals_single_process():
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_decode_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    plain = _inputs()
+    for case, n in enumerate((len(plain), 2)):
+        ref = plain[:n]
+        ref_sizes = [len(r) for r in ref]
+        ref_offs = [sum(ref_sizes[:i]) for i in range(n)]
+        for rank, got in res:
+            local, sizes, offs, joined = got[case]
+            lo, hi = rank * n // world, (rank + 1) * n // world
+            assert local == ref_sizes[lo:hi]
+            assert sizes == ref_sizes and offs == ref_offs
+            assert joined == (b"".join(ref) if rank == world - 1 else None)
