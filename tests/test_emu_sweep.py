@@ -60,3 +60,35 @@ def test_sweep_model_matches_longest_match(emu, tmp_path, level):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout, r.stdout
     assert " 0 in 7-bit" not in r.stdout  # both signature forms were exercised
+
+
+DEMAND_SRC = os.path.join(ROOT, "tools", "emu", "emu_demand.c")
+# (chain, nice, good, lazy) per level, deflate.ts:84-100 configuration_table
+LEVELS_DW = {4: (16, 16, 4, 4), 5: (32, 32, 8, 16), 6: (128, 128, 8, 16), 7: (256, 128, 8, 32), 8: (1024, 258, 32, 128),
+             9: (4096, 258, 32, 258)}
+
+
+@pytest.fixture(scope="module")
+def emu_demand(tmp_path_factory):
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    exe = str(tmp_path_factory.mktemp("emu") / "emu_demand")
+    subprocess.run(["gcc", "-O2", "-o", exe, DEMAND_SRC], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("level", sorted(LEVELS_DW))
+def test_demand_walk_model_matches_serial_parse(emu_demand, tmp_path, level):
+    """The demand mode (option demand: zs_k_sweep takes chain >> 2 steps, zs_k_parse_dw walks steps chain >> 2 + 1
+    .. chain where the parse asks for the full budget): its walk rule (stop at limit or where member positions stop
+    falling) gives longest_match's full-budget result at every walked position, and the parse over it emits the
+    serial deflate_slow's symbols."""
+    streams = _streams()
+    blob = struct.pack("<I", len(streams)) + struct.pack("<%dI" % len(streams), *map(len, streams)) + b"".join(streams)
+    f = tmp_path / "streams.bin"
+    f.write_bytes(blob)
+    chain, nice, good, lazy = LEVELS_DW[level]
+    r = subprocess.run([emu_demand, str(f), str(chain), str(nice), str(good), str(lazy)], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "walk mismatches 0, streams with other symbols 0" in r.stdout, r.stdout

@@ -1,6 +1,7 @@
 """GPU parity: the HIP deflate engine against the reference's goldens and the oracle."""
 import hashlib
 import random
+import struct
 
 import pytest
 
@@ -83,17 +84,30 @@ def test_sweep_match_table_equals_chain_walk(engine, level):
     inputs.append(bytes(x & 0x7F for x in corpus.rand(91 + level, 65536)))
     inputs.append(bytes(0x41 + (x & 3) for x in corpus.rand(92 + level, 65536)))
     inputs.append(bytes(x & 0x7F for x in corpus.rand(93, 20000)) + corpus.text(94, 45537))
+    # (match_sweep, demand): the full sweep, the chain walk, and the demand-mode sweep (chain >> 2 steps; the
+    # parse walks the rest where it asks for the full budget, zs_k_parse_dw)
     tables, outs = [], []
     try:
-        for sweep in (1, 0):
+        for sweep, demand in ((1, 0), (0, 0), (1, 1)):
             engine.set_option("match_sweep", sweep)
+            engine.set_option("demand", demand)
             outs.append(engine.compress_batch_raw(inputs, "deflate-raw", level))
             tables.append([engine.debug_fetch(1, i, 8 * len(d)) for i, d in enumerate(inputs)])
     finally:
         engine.set_option("match_sweep", 1)
+        engine.set_option("demand", 0)
     for i, d in enumerate(inputs):
         assert tables[0][i] == tables[1][i], (i, len(d))
-        assert outs[0][i] == outs[1][i] and outs[0][i][1] == oracle.compress(d, level, "deflate-raw")[1], (i, len(d))
+        want = oracle.compress(d, level, "deflate-raw")[1]
+        assert outs[0][i] == outs[1][i] == outs[2][i] and outs[0][i][1] == want, (i, len(d))
+        # demand mode: the chain >> 2 results are the full sweep's; a full-budget result is the full sweep's or
+        # left open (ZS_MORE | the position's member index) at levels 4..7
+        full = struct.unpack("<%dI" % (2 * len(d)), tables[0][i])
+        dem = struct.unpack("<%dI" % (2 * len(d)), tables[2][i])
+        assert full[1::2] == dem[1::2], (i, len(d))
+        opened = sum(1 for a, b in zip(full[0::2], dem[0::2]) if a != b)
+        assert all(a == b or (b >> 16) == 0xFFFF for a, b in zip(full[0::2], dem[0::2])), (i, len(d))
+        assert level <= 7 or opened == 0
 
 
 def test_output_capacity_too_small_reports_buf_error(engine):

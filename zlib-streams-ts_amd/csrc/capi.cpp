@@ -96,6 +96,7 @@ struct zs_ctx {
   int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
   int cur_pw = 1;            // waves per stream of the current deflate batch's parse (zs_k_parse / _2w / _4w)
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
+  bool demand = false;       // L4..7: the sweep takes chain >> 2 steps, zs_k_parse_dw walks the rest where the parse needs them (exact; slower)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
   // the chain builders (zs_k_bucket, zs_k_prev, zs_k_fast) let same-address LDS atomics of
   // one instruction apply in lane order (1) or rank equal hashes by ballots (0); 0 when the
@@ -343,6 +344,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
     if (value < 0) return fail(ZS_STREAM_ERROR, "seg_small_min must be >= 0");
     c->seg_small_min = (uint32_t)value;
   }
+  else if (!strcmp(name, "demand")) c->demand = value != 0;
   else if (!strcmp(name, "parse_waves")) {
     if (value < 0 || value > 4 || value == 3) return fail(ZS_STREAM_ERROR, "parse_waves must be 0, 1, 2 or 4");
     c->parse_waves = value;
@@ -460,13 +462,23 @@ static int deflate_stored_batch(zs_ctx* c, int wrap, uint32_t n, const uint8_t* 
 // The L4..9 parse runs two waves per stream (zs_k_parse_2w: 512-position
 // segments, two rounds' speculative passes at once) for a batch of n streams?
 // The whole batch decides (chunks of one batch share the scratch layout).
-static int parse_waves_for(const zs_ctx* c, uint32_t n) {
+// Levels 4..7 with the sweep (option demand, default on): the sweep takes the
+// first chain >> 2 steps of every position and zs_k_parse_dw walks the rest
+// where the parse asks for the full budget (ZS_PARSEDW_WAVES waves per stream).
+// Levels 8, 9 sweep the whole chain (on text their chains end within chain >> 2).
+static int parse_waves_for(const zs_ctx* c, uint32_t n, int level) {
+  if (c->demand && c->match_sweep && level >= 4 && level <= 7) return ZS_PARSEDW_WAVES;
   if (c->parse_waves) return c->parse_waves;
   return n < ZS_PARSE2W_AUTO ? 2 : 1;
 }
-static uint32_t parse_seg(int w) { return w == 4 ? ZS_PARSE4W_SEG : w == 2 ? ZS_PARSE2W_SEG : ZS_PARSE_SEG; }
+static uint32_t parse_seg(int w) {
+  return w == ZS_PARSEDW_WAVES ? ZS_PARSEDW_SEG : w == 4 ? ZS_PARSE4W_SEG : w == 2 ? ZS_PARSE2W_SEG : ZS_PARSE_SEG;
+}
 static uint32_t parse_seg_words(int w) {
-  return w == 4 ? ZS_PARSE4W_SEG_WORDS : w == 2 ? ZS_PARSE2W_SEG_WORDS : ZS_PARSE_SEG_WORDS;
+  return w == ZS_PARSEDW_WAVES ? ZS_PARSEDW_SEG_WORDS
+         : w == 4              ? ZS_PARSE4W_SEG_WORDS
+         : w == 2              ? ZS_PARSE2W_SEG_WORDS
+                               : ZS_PARSE_SEG_WORDS;
 }
 
 // The deflate launch sequence of a batch (levels 1..9) on stream st.
@@ -495,7 +507,7 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
                                                                                c->prevd.as<uint16_t>(), 65537u);
       MARK("bucket");
       zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
-                                     cfg.chain, cfg.nice);
+                                     cfg.chain, cfg.nice, c->cur_pw == ZS_PARSEDW_WAVES ? 1 : 0);
       MARK("sweep");
       if (max_len > 65537u) {
         zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
@@ -512,9 +524,15 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
       MARK("match");
     }
     const int pw = c->cur_pw;  // waves per stream of the lazy parse (deflate_parse.hip)
-    auto parse = pw == 4 ? zs_k_parse_4w : pw == 2 ? zs_k_parse_2w : zs_k_parse;
-    parse<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), syms, d_bk, d_st, pscr,
-                                 cfg.good, cfg.lazy);
+    if (pw == ZS_PARSEDW_WAVES) {
+      zs_k_parse_dw<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), syms, d_bk,
+                                           d_st, pscr, cfg.good, cfg.lazy, c->prevd.as<uint16_t>(), cfg.chain,
+                                           cfg.nice);
+    } else {
+      auto parse = pw == 4 ? zs_k_parse_4w : pw == 2 ? zs_k_parse_2w : zs_k_parse;
+      parse<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), syms, d_bk, d_st,
+                                   pscr, cfg.good, cfg.lazy);
+    }
     MARK("parse");
   } else {
     const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
@@ -610,7 +628,7 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
   HIPCHK(c->prevd.ensure(2 * P + 64));
   HIPCHK(c->mres.ensure(8 * P + 64));
   HIPCHK(c->syms.ensure(4 * (P + n) + 64));
-  c->cur_pw = level >= 4 ? parse_waves_for(c, n) : 1;
+  c->cur_pw = level >= 4 ? parse_waves_for(c, n, level) : 1;
   if (level >= 4)
     HIPCHK(c->pscr.ensure(4ull * parse_seg_words(c->cur_pw) * (P / parse_seg(c->cur_pw) + n + 1)));
   HIPCHK(c->blocks.ensure(sizeof(zs_block) * (size_t)B));

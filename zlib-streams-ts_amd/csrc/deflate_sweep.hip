@@ -435,11 +435,14 @@ extern "C" int zs_sw_stats(unsigned long long* out) {
 template <bool A7, bool MW>
 static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, uint16_t* mw, uint32_t* next,
                                                uint32_t n, const uint16_t* mem, uint2* out, int chain,
-                                               int nice_cfg) {
+                                               int nice_cfg, bool demand) {
   using Sig = SwSig<A7>;
   const uint32_t m = n - 2;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t budget = (uint32_t)chain, budget_s = (uint32_t)chain >> 2;
+  // the steps swept: the full chain, or (demand) the first chain >> 2 -- the rest
+  // only where the parse asks for the full budget (zs_k_parse_dw)
+  const uint32_t sbud = demand ? budget_s : budget;
   const uint32_t nchunks = (m + 63) / 64;
   auto put_rec = [&](int j, uint4 r) {
     const uint32_t i = (uint32_t)j & (ZS_SW_RING - 1);
@@ -462,28 +465,41 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
   // per-wave LDS window as their records are built, so the distances after
   // the sweep read positions from LDS instead of HBM (chain + 64 <= ZS_SW_MW)
   int mw0 = 0;  // member index of mw[0] (k0 - budget)
-  auto load_rec = [&](int j) {  // key 0 = no member: fails every liveness test
+  auto load_rec_q = [&](int j, uint32_t q) {  // key 0 = no member: fails every liveness test
     const bool in = j >= 0 && (uint32_t)j < m;
-    const uint32_t q = in ? mem[j] : 0u;
     if (MW && (uint32_t)(j - mw0) < ZS_SW_MW) mw[j - mw0] = (uint16_t)q;  // (block 1 back reaches below k0 - budget when budget < 64)
     put_rec(j, in ? make_rec(q) : make_uint4(0, 0, 0, 0));
   };
+  auto fetch = [&](int j) -> uint32_t { return j >= 0 && (uint32_t)j < m ? (uint32_t)mem[j] : 0u; };
+  auto load_rec = [&](int j) { load_rec_q(j, fetch(j)); };
   auto member = [&](int j) -> uint32_t { return MW ? (uint32_t)mw[j - mw0] : (uint32_t)mem[j]; };
   auto rmbits = [&](const Sig& S, uint32_t slot) -> uint32_t {  // a ring record's matched bits
     const uint2 ab = R->ab[slot];
     return S.mbits(ab.x, ab.y, A7 ? 0u : R->c[slot]);
   };
-  for (;;) {
+  // chunks are claimed one ahead: the next chunk's members (its own and the
+  // block before) are loaded while this one is swept
+  auto claim = [&]() -> uint32_t {
     uint32_t c = 0;
     if (lane == 0) c = atomicAdd(next, 1u);
-    c = __builtin_amdgcn_readfirstlane(c);
+    return __builtin_amdgcn_readfirstlane(c);
+  };
+  uint32_t c = claim();
+  uint32_t pf_p = fetch((int)(64 * c + lane)), pf_b = fetch((int)(64 * c + lane) - 64);
+  for (;;) {
     if (c >= nchunks) break;
+    const uint32_t cn = claim();
     const int k0 = (int)(64 * c);
     const int k = k0 + (int)lane;
     const bool own = (uint32_t)k < m;
     SW_STAT(0, 1);
-    const uint32_t p = own ? mem[k] : 0u;
-    mw0 = k0 - (int)budget;
+    const uint32_t p = pf_p, qb = pf_b;  // (0 past the members)
+    if (cn < nchunks) {
+      pf_p = fetch((int)(64 * cn + lane));
+      pf_b = fetch((int)(64 * cn + lane) - 64);
+    }
+    c = cn;
+    mw0 = k0 - (int)sbud - (demand ? 1 : 0);  // (demand: member k - sbud - 1 for the probe below)
     if (MW) mw[k - mw0] = (uint16_t)p;
     Sig S;
     S.own(win, p);
@@ -500,7 +516,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     put_rec(k, own ? make_rec(p) : make_uint4(0, 0, 0, 0));
-    load_rec(k - 64);
+    load_rec_q(k - 64, qb);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
 
@@ -588,7 +604,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
       return r;
     };
     // steps 2..4 (masked)
-    if (budget >= 4u) {
+    if (sbud >= 4u) {
       uint32_t sc[3];
       uint64_t lm = 0;
 #pragma unroll
@@ -667,7 +683,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         t0 = t1 + 1u;
       }
     };
-    for (uint32_t b = 0; budget > 4u && alive_m; b++) {
+    for (uint32_t b = 0; sbud > 4u && alive_m; b++) {
       // block b = steps (64b, 64b + 64]: members k0 - 64b - 64 ... k0 - 64b + 62, i.e. the blocks b and b + 1 back
       if (b >= 1) {
         __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -677,11 +693,11 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         __builtin_amdgcn_wave_barrier();
       }
       const uint32_t ta = b == 0 ? 5u : 64u * b + 1u;
-      const uint32_t tb = min(64u * b + 64u, budget);
+      const uint32_t tb = min(64u * b + 64u, sbud);
       // step t of this block at slot base - t
       const uint32_t base = (((uint32_t)(k - 64 * (int)b - 64)) & (ZS_SW_RING - 1)) + 64u * b + 64u;
       run(base, ta, tb);
-      if (tb >= budget) break;
+      if (tb >= sbud) break;
     }
     if (!snapped) {  // every chain ended before step chain >> 2
       thr_s = thr;
@@ -698,7 +714,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         if (tail) {  // maxc <= 12: min(lcp, maxc) exactly, first maximum in chain order (deflate.ts:1082-1105)
           uint32_t b = 2u << 16, bs = 2u << 16;
           for (uint32_t t = 1; t <= budget && (int)t <= k; t++) {
-            const uint32_t q = member(k - (int)t);
+            const uint32_t q = t <= sbud ? member(k - (int)t) : (uint32_t)mem[k - (int)t];
             const uint32_t key = (sw_hash(sw_word(win, q)) << 16) | q;
             if (t == 1u ? key < khead : key <= klim) break;
             uint32_t len = 12;
@@ -711,9 +727,9 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
             if (t <= budget_s) bs = max(bs, sc);
           }
           L = b >> 16;
-          D = L > 2u ? p - member(k - (int)(0xffffu - (b & 0xffffu))) : 0u;
+          D = L > 2u ? p - (uint32_t)mem[k - (int)(0xffffu - (b & 0xffffu))] : 0u;
           Ls = bs >> 16;
-          Ds = Ls > 2u ? p - member(k - (int)(0xffffu - (bs & 0xffffu))) : 0u;
+          Ds = Ls > 2u ? p - (uint32_t)mem[k - (int)(0xffffu - (bs & 0xffffu))] : 0u;
         } else {
           if (bt) {
             L = Sig::len(thr >> 3);
@@ -742,6 +758,15 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         }
         rx = (L << 16) | (L > 2u ? D : 0u) | (head & 0x8000u);
         ry = (Ls << 16) | (Ls > 2u ? Ds : 0u);
+        // demand: the full-budget result is settled unless the chain is still
+        // live at step chain >> 2 + 1 below nice; then rx = ZS_MORE | k for the
+        // parse's continuation walk (a live step 2 means the head is not at
+        // MAX_DIST: no slide-NIL flag is lost)
+        if (demand && !tail && L < nice && (int)sbud < k) {
+          // (the ring loads filled the member window from k0 - 64 up: LDS unless sbud = 64)
+          const uint32_t q = MW && sbud < 64u ? member(k - (int)sbud - 1) : (uint32_t)mem[k - (int)sbud - 1];
+          if (((sw_hash(sw_word(win, q)) << 16) | q) > klim) rx = ZS_MORE | (uint32_t)k;
+        }
       }
       out[p] = make_uint2(rx, ry);
     }
@@ -752,7 +777,7 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
                                                    const uint32_t* __restrict__ in_len,
                                                    const uint64_t* __restrict__ pos_base,
                                                    const uint16_t* __restrict__ members, uint2* __restrict__ mres,
-                                                   int chain, int nice_cfg) {
+                                                   int chain, int nice_cfg, int demand) {
   __shared__ __attribute__((aligned(16))) SwRing ring[16];
   __shared__ __attribute__((aligned(16))) uint32_t win[ZS_SW_WIN_WORDS];
   __shared__ uint16_t mwin[16][ZS_SW_MW];
@@ -794,11 +819,12 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
   const uint16_t* mem = members + pos_base[s];
   uint2* out = mres + pos_base[s];
   uint16_t* const mw = mwin[threadIdx.x >> 6];
-  if (chain + 64 <= (int)ZS_SW_MW) {
-    if (a7) sw_body<true, true>(win, R, mw, &next, n, mem, out, chain, nice_cfg);
-    else sw_body<false, true>(win, R, mw, &next, n, mem, out, chain, nice_cfg);
+  const bool dm = demand != 0;
+  if ((dm ? (chain >> 2) + 1 : chain) + 64 <= (int)ZS_SW_MW) {
+    if (a7) sw_body<true, true>(win, R, mw, &next, n, mem, out, chain, nice_cfg, dm);
+    else sw_body<false, true>(win, R, mw, &next, n, mem, out, chain, nice_cfg, dm);
   } else {  // levels 8, 9: positions from HBM
-    if (a7) sw_body<true, false>(win, R, mw, &next, n, mem, out, chain, nice_cfg);
-    else sw_body<false, false>(win, R, mw, &next, n, mem, out, chain, nice_cfg);
+    if (a7) sw_body<true, false>(win, R, mw, &next, n, mem, out, chain, nice_cfg, dm);
+    else sw_body<false, false>(win, R, mw, &next, n, mem, out, chain, nice_cfg, dm);
   }
 }

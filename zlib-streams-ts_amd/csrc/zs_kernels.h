@@ -40,8 +40,9 @@ __global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint
 template <bool ORD>
 __global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                             uint16_t* members, uint2* mres);
+// demand = 1: steps 1 .. chain >> 2 only; an entry the parse may need further is ZS_MORE | member (zs_k_parse_dw)
 __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                           const uint16_t* members, uint2* mres, int chain, int nice);
+                           const uint16_t* members, uint2* mres, int chain, int nice, int demand);
 // the lazy parse (deflate_parse.hip): pass A stages 32 match-table entries per lane in LDS
 #define ZS_PARSE_DECL(name)                                                                                        \
   __global__ void name(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base, \
@@ -50,6 +51,11 @@ __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint
 ZS_PARSE_DECL(zs_k_parse)
 ZS_PARSE_DECL(zs_k_parse_2w)  // two waves per stream, ZS_PARSE2W_SEG-position segments
 ZS_PARSE_DECL(zs_k_parse_4w)  // four waves per stream, ZS_PARSE4W_SEG-position segments
+// the parse over a demand-mode match table: continues the open entries' chain walks (16 waves per stream)
+__global__ void zs_k_parse_dw(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                              const uint64_t* pos_base, const uint32_t* blk_base, const uint2* mres, uint32_t* syms,
+                              zs_block* blocks, zs_stream* streams, uint32_t* scratch, int good, int lazy,
+                              const uint16_t* members, int chain, int nice);
 // parse scratch words per 1024-position segment (deflate_parse.hip)
 #define ZS_PARSE_SEG 1024u
 #define ZS_PARSE_SEG_WORDS 3596u
@@ -57,6 +63,9 @@ ZS_PARSE_DECL(zs_k_parse_4w)  // four waves per stream, ZS_PARSE4W_SEG-position 
 #define ZS_PARSE2W_SEG_WORDS 2060u
 #define ZS_PARSE4W_SEG 256u
 #define ZS_PARSE4W_SEG_WORDS 1292u
+#define ZS_PARSEDW_SEG 64u
+#define ZS_PARSEDW_SEG_WORDS 716u
+#define ZS_PARSEDW_WAVES 16
 template <int NW, bool ORD>
 __global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,
