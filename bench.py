@@ -585,10 +585,17 @@ def main_inflate(args):
     d_status, d_phase, d_msg, d_len, d_cons = i32(), i32(), i32(), i32(), i32()
     stream = torch.cuda.current_stream(D.dev)
 
+    N_all = len(entries)
+
     def step():
         eng.decompress_device(dec_fmt, N, d_in.data_ptr(), in_off, in_len, d_out.data_ptr(), out_off, out_cap,
                               d_status.data_ptr(), d_phase.data_ptr(), d_msg.data_ptr(), d_len.data_ptr(),
                               d_cons.data_ptr(), stream.cuda_stream)
+        if D.world > 1:
+            # the final size gather (RCCL all_gather over xGMI), as the compress step: the global
+            # output layout on every rank
+            sizes = shard.gather_sizes(d_len, N_all)
+            shard.global_offsets(sizes)
 
     for _ in range(args.warmup):
         step()

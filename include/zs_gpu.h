@@ -36,11 +36,12 @@
  *     which the stream layer reports as "init failed: -2", streams.ts:53), or
  *     ZS_MEM_ERROR when device memory cannot be obtained.  zs_last_error()
  *     describes the last failure on the calling thread.
- *   - Output offsets must be multiples of 4 bytes (the engine writes 32-bit
- *     words; ZS_STREAM_ERROR otherwise), and so must deflate's capacities; an
- *     inflate capacity may be any size, and the decoders may write the bytes up
- *     to it rounded up to a multiple of 4.  Inputs may be packed at any byte
- *     offset.
+ *   - Output offsets and capacities of the device entry points must be
+ *     multiples of 4 bytes (the engine writes 32-bit words; ZS_STREAM_ERROR
+ *     otherwise): no store leaves [out_off[i], out_off[i] + out_cap[i]).  The
+ *     host-buffer entries take any inflate capacity (they round it up inside
+ *     their own staging and copy back only the bytes produced).  Inputs may be
+ *     packed at any byte offset.
  */
 #ifndef ZS_GPU_H
 #define ZS_GPU_H

@@ -366,5 +366,84 @@ def test_c5_gunzip_shard_of_1024_members(engine):
     assert all((len(c), hashlib.sha256(c).digest()[:16]) == r for c, r in zip(gz, recs))
     res = engine.decompress_batch_detailed(gz, "gzip", [L] * N)
     assert engine.last_lane_count() == N
+    assert engine.last_seg_count() == N  # the per-rank shard runs on the segmented decode
     for s, r in zip(src, res):
         assert r[0] == 1 and r[3] == s and (r[5] & 0xffffffff) == zlib.crc32(s)
+
+
+def test_c5_deflate64_shard_of_rank_0(engine):
+    """C5-ii at the per-rank size of 8 GPUs, built as bench.py builds it: the 8,192 T-corpus raw-L6 members
+    (pinned by the reference golden batch_t64_l6_raw) with the reference's test/data deflate64 fixtures interleaved
+    (inflate_small.json digests), sharded by shard_range; rank 0's 1,025 entries decoded as deflate64-raw with
+    default options, every corpus member equal to its source and every fixture to its digest."""
+    import json
+    import os
+    import zsamd
+    import zsamd.shard as shard
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    g = json.load(open(os.path.join(root, "tests", "golden", "inflate_small.json")))
+    fx = [(open(os.path.join(root, "tests", "golden", "d64", c["name"][4:]), "rb").read(), c["out_len"],
+           c["out_sha256"]) for c in g["cases"] if c["name"].startswith("d64_") and c.get("ok")]
+    S, L = 8192, 65536
+    gstep = S // len(fx)
+    entries = []
+    for i in range(S):
+        if i % gstep == gstep // 2 and i // gstep < len(fx):
+            entries.append(("f", i // gstep))
+        entries.append(("u", i))
+    lo, hi = shard.shard_range(len(entries), 8, 0)
+    mine = entries[lo:hi]
+    us = [e[1] for e in mine if e[0] == "u"]
+    host = zsamd.corpus("text", us[0], len(us), L)
+    src = {u: bytes(host[k * L:(k + 1) * L]) for k, u in enumerate(us)}
+    comp = dict(zip(us, engine.compress_batch([src[u] for u in us], "deflate-raw", 6)))
+    recs = golden_io.batch("t64_l6_raw")
+    assert all((len(comp[u]), hashlib.sha256(comp[u]).digest()[:16]) == recs[u] for u in us)
+    members = [comp[e[1]] if e[0] == "u" else fx[e[1]][0] for e in mine]
+    caps = [L if e[0] == "u" else (fx[e[1]][1] + 3) & ~3 for e in mine]
+    res = engine.decompress_batch_raw(members, "deflate64-raw", caps)
+    assert len(mine) == 1025 and sum(1 for e in mine if e[0] == "f") >= 1
+    for e, r in zip(mine, res):
+        assert r[0] == 1, e
+        if e[0] == "u":
+            assert r[3] == src[e[1]], e
+        else:
+            assert len(r[3]) == fx[e[1]][1] and hashlib.sha256(r[3]).hexdigest() == fx[e[1]][2], e
+
+
+def test_device_inflate_rejects_unaligned_capacities(engine):
+    """The device entry points' output capacities are multiples of 4 (the decoders store whole words): an
+    unaligned one is ZS_STREAM_ERROR before anything runs; the host entry takes any capacity."""
+    import torch
+    import zsamd
+
+    comp = engine.compress_batch([b"hello hello hello"], "deflate-raw", 6)[0]
+    d_in = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+    d_out = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    i32 = lambda: torch.zeros(1, dtype=torch.int32, device="cuda")
+    bufs = [i32() for _ in range(5)]
+    args = ("deflate-raw", 1, d_in.data_ptr(), (ctypes.c_uint64 * 1)(0), (ctypes.c_uint32 * 1)(len(comp)),
+            d_out.data_ptr(), (ctypes.c_uint64 * 1)(0))
+    with pytest.raises(zsamd.ZsError):
+        engine.decompress_device(*args, (ctypes.c_uint32 * 1)(17), *[b.data_ptr() for b in bufs])
+    engine.decompress_device(*args, (ctypes.c_uint32 * 1)(20), *[b.data_ptr() for b in bufs])
+    torch.cuda.synchronize()
+    assert int(bufs[0][0]) == 1 and bytes(d_out[:17].cpu().numpy()) == b"hello hello hello"
+    assert engine.decompress_batch([comp], "deflate-raw", [17]) == [b"hello hello hello"]
+
+
+@pytest.mark.gpu
+def test_host_batch_packs_produced_bytes_over_several_chunks(engine):
+    """The host-buffer decode of a batch of >= 32 MB input runs as four chunks and packs each chunk's outputs by the
+    bytes produced, not by capacity: a last chunk that expands far past 4x the batch input grows the pack buffers
+    once the chunks before it are scattered, and every member comes back exact (capi.cpp host_batch_run)."""
+    import numpy as np
+
+    rng = np.random.default_rng(5)
+    srcs = [rng.integers(0, 256, 600_000, dtype=np.uint8).tobytes() for _ in range(56)] + [bytes(40 << 20)] * 8
+    comp = engine.compress_batch(srcs, "deflate-raw", 1)
+    assert sum(map(len, comp)) >= 32 << 20
+    got = engine.decompress_batch(comp, "deflate-raw", [len(s) for s in srcs])
+    assert [len(g) for g in got] == [len(s) for s in srcs]
+    assert all(g == s for g, s in zip(got, srcs))

@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 class _opts:
     DEFAULTS = {"inflate_seg": 1, "seg_bits": 2048, "seg_small_batch": 16384, "seg_small_min": 4096,
-                "inflate_fast": 1, "inflate_ref_wrap": 1, "inflate_wave_min": 32768}
+                "inflate_fast": 1, "inflate_ref_wrap": 1, "inflate_wave_min": 32768, "seg_scratch_mb": 16384}
 
     def __init__(self, engine, **kw):
         self.e, self.kw = engine, kw
@@ -57,17 +57,18 @@ def test_segmented_decode_equals_the_reference(engine, fmt):
     comps = [c for _, c in ms]
     caps = [len(s) + 16 for s, _ in ms]
     got = engine.decompress_batch_detailed(comps, fmt, caps)
-    assert engine.last_seg_count() == len(ms)
+    assert engine.last_seg_count() == len(ms)  # every member finished by the segmented decode
     ok = 0
     for i, ((s, c), g) in enumerate(zip(ms, got)):
         st, out, cons, ph, msg = oracle.decompress(c, fmt, cap=len(s) + 16, reference_bugs=True)
-        assert (g[0], g[1]) == (st, ph), i
+        # status, phase, message and consumed bytes of every member, the failing ones too
+        assert (g[0], g[1], g[2], g[4]) == (st, ph, msg, cons), (i, g[:3], g[4], st, ph, msg, cons)
         if st == 1:
             ok += 1
-            assert g[3] == out and g[4] == cons == len(c), i
+            assert g[3] == out and cons == len(c), i
             if fmt != "deflate-raw":
                 assert (g[5] & 0xffffffff) == (oracle.crc32(out) if fmt == "gzip" else oracle.adler32(out)), i
-    assert ok >= len(ms) // 2
+    assert ok >= 1
 
 
 @pytest.mark.parametrize("bits", [1024, 8192])
@@ -156,3 +157,21 @@ def test_segmented_and_lane_paths_agree_on_a_mixed_batch(engine):
     for (s, c), g in zip(ms, got):  # (the window-wrap copy can fail a gzip member's CRC, as in the reference)
         st, out, cons, ph, msg = oracle.decompress(c, "gzip", cap=len(s) + 8, reference_bugs=True)
         assert (g[0], g[1]) == (st, ph) and (st != 1 or g[3] == out)
+
+
+def test_scratch_budget_sends_the_rest_to_the_other_paths(engine):
+    """The segmented decode's u16 piece scratch (2 bytes per byte of capacity) is bounded per batch (option
+    seg_scratch_mb): with a 1 MiB budget only the first few members of 256 take it, the others the wave kernel,
+    and every member still equals its source."""
+    import zsamd
+
+    N, L = 256, 65536
+    host = zsamd.corpus("text", 0, N, L)
+    src = [bytes(host[i * L:(i + 1) * L]) for i in range(N)]
+    comp = engine.compress_batch(src, "deflate-raw", 6)
+    with _opts(engine, seg_scratch_mb=1):
+        got = engine.decompress_batch(comp, "deflate-raw", [L] * N)
+        nseg = engine.last_seg_count()
+    engine.set_option("seg_scratch_mb", 16384)
+    assert 0 < nseg < N // 4
+    assert got == src

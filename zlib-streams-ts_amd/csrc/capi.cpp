@@ -120,6 +120,7 @@ struct zs_ctx {
   uint32_t seg_small_batch = 16384; // batches of at most this many members ...
   uint32_t seg_small_min = 4096;    // ... send members with more input bytes than this to it too
   bool seg_wide = true;             // the 2048-bit sync window for a batch of few large members
+  uint64_t seg_scratch_max = 16ull << 30;  // bytes of u16 piece scratch the segmented decode may take per batch
   uint32_t ncu = 256;               // compute units of the device
   Buf glist, gfound, gbig, gbigs, gspb, gspl, gflist, gent, gblk, glanes, gtab, gmem, gpbase, gplist, gsbase, gscr, gcnt;
   std::vector<uint32_t> hglist, hgpbase, hgspb, hgbig, hgbig_s;
@@ -234,8 +235,10 @@ int zs_ctx_create(int device, zs_ctx** out) {
     delete c;
     return fail(ZS_MEM_ERROR, "%s", hipGetErrorString(e));
   }
+  int prio_lo = 0, prio_hi = 0;  // (numerically lower = higher priority)
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipEventCreateWithFlags(&c->join2, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess ||
@@ -334,6 +337,10 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "inflate_split")) c->inflate_split = value != 0;
   else if (!strcmp(name, "inflate_seg")) c->inflate_seg = value != 0;
   else if (!strcmp(name, "seg_wide")) c->seg_wide = value != 0;
+  else if (!strcmp(name, "seg_scratch_mb")) {
+    if (value < 0) return fail(ZS_STREAM_ERROR, "seg_scratch_mb must be >= 0");
+    c->seg_scratch_max = (uint64_t)value << 20;
+  }
   else if (!strcmp(name, "seg_bits")) {
     if (value < (int)ZS_SEG_W || value > (int)ZS_SEG_SMAX) return fail(ZS_STREAM_ERROR, "seg_bits must be 1024 .. 8192");
     c->seg_bits = (uint32_t)value;
@@ -704,9 +711,9 @@ __global__ void zs_k_compact(const uint8_t* __restrict__ src, const uint64_t* __
 // entries (array r at d_res + r n), res_host the caller's nres arrays, of which
 // res_host[len_idx] is the output length.  Outputs land at out + out_off[i].
 template <class Launch>
-static int host_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                      const std::vector<uint32_t>& ocap, uint32_t nres, uint32_t* const* res_host, uint32_t len_idx,
-                      uint8_t* out, const uint64_t* out_off, Launch launch) {
+static int host_batch_run(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                          const std::vector<uint32_t>& ocap, uint32_t nres, uint32_t* const* res_host,
+                          uint32_t len_idx, uint8_t* out, const uint64_t* out_off, Launch launch) {
   std::vector<uint64_t> doff(n), ooff(n);
   uint64_t tin = 0, tout = 0;
   for (uint32_t i = 0; i < n; i++) {
@@ -718,8 +725,11 @@ static int host_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* 
   HIPCHK(c->d_in.ensure(tin + 16));
   HIPCHK(c->h_in.ensure(tin + 16));
   HIPCHK(c->d_out.ensure(tout + 16));
-  HIPCHK(c->d_pack.ensure(tout + 16));
-  HIPCHK(c->h_out.ensure(tout + 16));
+  // the packed outputs (d_pack, h_out) hold produced bytes, not capacities: a
+  // first guess, grown in after_kernels once the chunks before are scattered
+  const uint64_t pack0 = std::min<uint64_t>(tout, std::max<uint64_t>(4 * tin, 64ull << 20)) + 16;
+  HIPCHK(c->d_pack.ensure(pack0));
+  HIPCHK(c->h_out.ensure(pack0));
   HIPCHK(c->d_res.ensure(4ull * nres * n + 16));
   HIPCHK(c->h_res.ensure(4ull * nres * n + 16));
   HIPCHK(c->d_offs.ensure(16ull * n + 16));
@@ -742,6 +752,19 @@ static int host_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* 
   uint32_t* hres = c->h_res.as<uint32_t>();
   uint64_t* hoffs = c->h_offs.as<uint64_t>();
   std::vector<uint64_t> poff(n);
+  std::vector<char> scattered(K, 0);
+  uint64_t packed = 0;  // bytes of the pack buffers in use (chunks not yet scattered)
+  // chunk k's bytes are in pinned memory: into the caller's buffers
+  auto after_copy = [&](uint32_t k) -> int {
+    if (scattered[k]) return ZS_OK;
+    const uint32_t a = bnd[k], b = bnd[k + 1];
+    HIPCHK(hipEventSynchronize(ev_out[k]));
+    uint64_t bytes = 0;
+    for (uint32_t i = a; i < b; i++) bytes += res_host[len_idx][i];
+    par_copy(b - a, out, out_off + a, c->h_out.as<uint8_t>(), poff.data() + a, res_host[len_idx] + a, bytes);
+    scattered[k] = 1;
+    return ZS_OK;
+  };
   // chunk k's results are in: the caller's arrays, then its compaction and D2H (stream d2h)
   auto after_kernels = [&](uint32_t k) -> int {
     const uint32_t a = bnd[k], b = bnd[k + 1], m = b - a;
@@ -749,33 +772,39 @@ static int host_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* 
     for (uint32_t r = 0; r < nres; r++)
       if (res_host[r]) memcpy(res_host[r] + a, hres + (size_t)r * n + a, 4ull * m);
     const uint32_t* len = res_host[len_idx];
-    uint64_t P = ooff[a];
+    uint64_t Pk = 0;
     for (uint32_t i = a; i < b; i++) {
       if (len[i] > ocap[i])
         return fail(ZS_MEM_ERROR, "stream %s reported more output than its capacity", std::to_string(i).c_str());
+      Pk += ((uint64_t)len[i] + 3) & ~3ull;
+    }
+    if (packed + Pk + 16 > std::min(c->d_pack.cap, c->h_out.cap)) {
+      // the pack buffers are full: scatter the chunks still in them, then start over (grown)
+      for (uint32_t j = 0; j < k; j++) {
+        const int rc = after_copy(j);
+        if (rc != ZS_OK) return rc;
+      }
+      packed = 0;
+      HIPCHK(c->d_pack.ensure(Pk + 16));
+      HIPCHK(c->h_out.ensure(Pk + 16));
+    }
+    uint64_t P = packed;
+    for (uint32_t i = a; i < b; i++) {
       hoffs[2 * a + (i - a)] = ooff[i];
       hoffs[2 * a + m + (i - a)] = poff[i] = P;
       P += ((uint64_t)len[i] + 3) & ~3ull;
     }
-    if (P > ooff[a]) {
+    if (P > packed) {
       uint64_t* doffs = c->d_offs.as<uint64_t>() + 2 * a;
       HIPCHK(hipMemcpyAsync(doffs, hoffs + 2 * a, 16ull * m, hipMemcpyHostToDevice, c->d2h));
       zs_k_compact<<<m, 256, 0, c->d2h>>>(c->d_out.as<uint8_t>(), doffs, dres + (size_t)len_idx * n + a,
                                           c->d_pack.as<uint8_t>(), m);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(c->h_out.as<uint8_t>() + ooff[a], c->d_pack.as<uint8_t>() + ooff[a], P - ooff[a],
+      HIPCHK(hipMemcpyAsync(c->h_out.as<uint8_t>() + packed, c->d_pack.as<uint8_t>() + packed, P - packed,
                             hipMemcpyDeviceToHost, c->d2h));
     }
+    packed = P;
     HIPCHK(hipEventRecord(ev_out[k], c->d2h));
-    return ZS_OK;
-  };
-  // chunk k's bytes are in pinned memory: into the caller's buffers
-  auto after_copy = [&](uint32_t k) -> int {
-    const uint32_t a = bnd[k], b = bnd[k + 1];
-    HIPCHK(hipEventSynchronize(ev_out[k]));
-    uint64_t bytes = 0;
-    for (uint32_t i = a; i < b; i++) bytes += res_host[len_idx][i];
-    par_copy(b - a, out, out_off + a, c->h_out.as<uint8_t>(), poff.data() + a, res_host[len_idx] + a, bytes);
     return ZS_OK;
   };
   for (uint32_t k = 0; k < K; k++) {
@@ -800,6 +829,21 @@ static int host_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* 
   int rc = after_kernels(K - 1);
   if (rc == ZS_OK && K >= 2) rc = after_copy(K - 2);
   if (rc == ZS_OK) rc = after_copy(K - 1);
+  return rc;
+}
+
+// host_batch_run, and on any error the copies and kernels it left in flight
+// are waited for before returning (the next call reuses the staging buffers)
+template <class Launch>
+static int host_batch(zs_ctx* c, uint32_t n, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                      const std::vector<uint32_t>& ocap, uint32_t nres, uint32_t* const* res_host, uint32_t len_idx,
+                      uint8_t* out, const uint64_t* out_off, Launch launch) {
+  const int rc = host_batch_run(c, n, in, in_off, in_len, ocap, nres, res_host, len_idx, out, out_off, launch);
+  if (rc != ZS_OK) {
+    (void)hipStreamSynchronize(c->h2d);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->d2h);
+  }
   return rc;
 }
 
@@ -1076,6 +1120,16 @@ __global__ void zs_k_inflate_check(const uint8_t* in, const uint64_t* in_off, co
 // stream, after the caller's stream reaches this point; then the wave kernel over
 // the same members for any the pieces could not finish (skip_done: the others
 // return at once), the exact kernel after it for whatever fails there.
+// a member's pieces' bound and its u16 scratch elements in the segmented decode (seg_launch)
+static uint32_t seg_pmax(uint32_t in_len) {
+  const uint64_t nbits = 8ull * in_len;
+  const uint64_t spans = nbits / ZS_SEG_BLOCK_BITS + 2 * nbits / (64ull * ZS_SEG_W) + 8;
+  return (uint32_t)std::min<uint64_t>(spans * ZS_SEG_LANES, nbits / ZS_SEG_W + spans + 1);
+}
+static uint64_t seg_scratch_elems(uint32_t in_len, uint32_t out_cap) {
+  return (((uint64_t)out_cap + 7) & ~7ull) + ZS_SEG_PAD * (uint64_t)seg_pmax(in_len) + 16;
+}
+
 static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* d_ioff,
                       const uint32_t* d_ilen, uint8_t* d_out, const uint64_t* d_ooff, const uint32_t* d_ocap,
                       const uint32_t* in_len, const uint32_t* out_cap, zs_lane_res* lres) {
@@ -1094,10 +1148,9 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
     const uint32_t i = c->hglist[k];
     const uint64_t nbits = 8ull * in_len[i];
     const uint64_t spans = nbits / ZS_SEG_BLOCK_BITS + 2 * nbits / (64ull * ZS_SEG_W) + 8;
-    const uint32_t pmax = (uint32_t)std::min<uint64_t>(spans * ZS_SEG_LANES, nbits / ZS_SEG_W + spans + 1);
     c->hgspb[k + 1] = c->hgspb[k] + (uint32_t)spans;
-    c->hgpbase[k + 1] = c->hgpbase[k] + pmax;
-    c->hgsbase[k + 1] = c->hgsbase[k] + ((((uint64_t)out_cap[i] + 7) & ~7ull) + ZS_SEG_PAD * (uint64_t)pmax + 16);
+    c->hgpbase[k + 1] = c->hgpbase[k] + seg_pmax(in_len[i]);
+    c->hgsbase[k + 1] = c->hgsbase[k] + seg_scratch_elems(in_len[i], out_cap[i]);
     if (nbits > ZS_SEG_BIG_BITS) c->hgbig.push_back(k);
   }
   const uint32_t nb = c->hgspb[ng], nbig = (uint32_t)c->hgbig.size();
@@ -1227,10 +1280,12 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
   if (!c->keep_counts) c->seg_used = false;
-  // every decoder stores whole dwords: up to 3 bytes past a member's end, inside its
-  // capacity rounded up to a multiple of 4 -- which the next 4-aligned offset cannot overlap
+  // the decoders store whole dwords (up to 3 bytes past a member's end): offsets and
+  // capacities are multiples of 4 so that no store leaves the member's region (the
+  // host entries round the caller's capacities up inside their own staging)
   for (uint32_t i = 0; i < n; i++)
-    if (out_off[i] & 3) return fail(ZS_STREAM_ERROR, "output offsets must be multiples of 4");
+    if ((out_off[i] & 3) || (out_cap[i] & 3))
+      return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
   MetaLayout ml(n);
   c->hmeta.resize(ml.bytes);
   c->last_n = n;
@@ -1299,6 +1354,9 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
     if (big_min) {
       constexpr size_t kSplitScratch = 2ull << 30;
       constexpr uint32_t kPieceCapMax = 4u << 20;  // values per piece
+      // the segmented decode's u16 scratch (2 bytes per byte of capacity) is
+      // bounded too (option seg_scratch_mb): members past it take the split / wave kernels
+      uint64_t seg_bytes = 0;
       for (uint32_t i = 0; i < n; i++) {
         if (!zs_inf_large(in_len[i], out_cap[i], big_min)) continue;
         // (the segmented decode keeps bit positions in 32 bits; members with long
@@ -1306,7 +1364,9 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
         // faster with a wave per block / per member, which copies 64 bytes at a time)
         const bool longcopies = zs_inf_expands(in_len[i], out_cap[i]) ||
                                 (wbits == -16 && 8ull * in_len[i] > ZS_SEG_SPLIT_BITS);
-        if (c->inflate_seg && in_len[i] < (1u << 29) && !longcopies) {
+        if (c->inflate_seg && in_len[i] < (1u << 29) && !longcopies &&
+            seg_bytes + 2 * seg_scratch_elems(in_len[i], out_cap[i]) <= c->seg_scratch_max) {
+          seg_bytes += 2 * seg_scratch_elems(in_len[i], out_cap[i]);
           c->hglist.push_back(i);
           continue;
         }
@@ -1323,14 +1383,7 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       }
       if (!c->hwlist.empty() || !c->hslist.empty() || !c->hglist.empty()) wave_min = big_min;
     }
-    c->seg_used |= !c->hglist.empty();
-    if (!c->hglist.empty()) {
-      const int r = seg_launch(c, st, wbits, n, d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, in_len, out_cap, lres);
-      if (r != ZS_OK) return r;
-      // (the join below waits for the side stream's last kernel)
-      if (c->hwlist.empty()) HIPCHK(hipEventRecord(c->join, c->side));
-    }
-    if (!c->hslist.empty()) {  // on the third stream, beside the segmented decode
+    if (!c->hslist.empty()) {  // on the third stream (high priority), beside the segmented decode
       const uint32_t ns = (uint32_t)c->hslist.size();
       HIPCHK(c->slist.ensure(4ull * ns));
       HIPCHK(c->sfound.ensure(8ull * ZS_SPLIT_MAX * ns));
@@ -1364,6 +1417,16 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
       HIPCHK(hipGetLastError());
       if (int r = mark(c, c->side2, "split_resolve")) return r;
       HIPCHK(hipEventRecord(c->join2, c->side2));
+    }
+    // the segmented decode after the split kernels are queued: its grids would
+    // otherwise fill the chip ahead of the split decode's few long pieces (C5-ii:
+    // the 2.19 MB fixture's split decode took 8.0 ms beside it, 2.5 ms alone)
+    c->seg_used |= !c->hglist.empty();
+    if (!c->hglist.empty()) {
+      const int r = seg_launch(c, st, wbits, n, d_in, d_ioff, d_ilen, d_out, d_ooff, d_ocap, in_len, out_cap, lres);
+      if (r != ZS_OK) return r;
+      // (the join below waits for the side stream's last kernel)
+      if (c->hwlist.empty()) HIPCHK(hipEventRecord(c->join, c->side));
     }
     if (!c->hwlist.empty()) {
       const uint32_t nw = (uint32_t)c->hwlist.size();

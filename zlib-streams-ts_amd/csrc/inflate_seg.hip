@@ -953,6 +953,7 @@ struct zs_sg_out {
   uint16_t* dst;
   uint16_t* ring;
   uint32_t P, F;
+  bool ovf;  // a reservation the ring could not hold (guarded statically; a run that sees it bails the member)
   __device__ __forceinline__ void put(uint32_t v) {
     ring[P & (ZS_SG_RING - 1u)] = (uint16_t)v;
     P++;
@@ -964,7 +965,10 @@ struct zs_sg_out {
     }
   }
   __device__ __forceinline__ void room(uint32_t k) {  // room for k more values
-    if (P + k - F > ZS_SG_RING) flush();
+    if (P + k - F > ZS_SG_RING) {
+      flush();
+      ovf |= P + k - F > ZS_SG_RING;
+    }
   }
   // the value at piece position x < P: the ring holds the last 64, older ones are stored
 #if ZS_SEG_EXP & 1
@@ -1110,6 +1114,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
   W.ring = ring[lane];
   W.P = 0;
   W.F = 0;
+  W.ovf = false;
   const uint32_t O = p.O, dend = p.dend;
   zs_refcalls_t<uint32_t> C;
   C.B = p.B;
@@ -1158,7 +1163,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
     }
     sb = zs_sg_bitpos(G);
   }
-  bad |= sb > dend || W.P != p.dcnt;
+  bad |= sb > dend || W.P != p.dcnt || W.ovf;
   if (!bad) W.finish();
   if (bad) atomicOr(&mem[m].bad, 1u);
 #if ZS_SEG_EXP & 1
@@ -1281,8 +1286,9 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
 #pragma unroll
     for (uint32_t q = 0; q < ZS_SG_RES_E; q++) cur[q] = nxt[q];
   }
-  if (M.total & 3u) {
-    if (t == 0) dst[wdone] = zs_rring[wdone & 0x3fffu];  // the last word's bytes past the end lie inside the capacity
+  if (M.total & 3u) {  // the last bytes one by one: nothing is stored past the member's end
+    uint8_t* db = out + out_off[s];
+    if (t < (M.total & 3u)) db[4u * wdone + t] = ring[(4u * wdone + t) & 0xffffu];
   }
   far = __syncthreads_or(far);
   if (t == 0) {

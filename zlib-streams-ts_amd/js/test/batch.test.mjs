@@ -6,6 +6,7 @@ import { createHash } from "crypto";
 import { readFileSync } from "fs";
 import { dirname, join } from "path";
 import { fileURLToPath } from "url";
+import { MessageChannel } from "worker_threads";
 
 import * as corpus from "../../../tests/golden/corpus.mjs";
 import * as api from "../streams-api.mjs";
@@ -67,6 +68,21 @@ async function main() {
     const back = await api.decompressBatch(await api.compressBatch(inputs, format), format);
     back.forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(inputs[i])) === 0, `round trip ${format} ${i}`));
   }
+  // the inputs are copied when the call is made: modifying or transferring (detaching) them before the
+  // batch settles changes nothing
+  const want = await api.compressBatch(inputs, "deflate-raw");
+  const mut = inputs.map((x) => new Uint8Array(x));
+  const pm = api.compressBatch(mut, "deflate-raw");
+  mut.forEach((x) => x.fill(0x41));
+  (await pm).forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(want[i])) === 0, `input modified after the call ${i}`));
+  const moved = inputs.map((x) => new Uint8Array(x));
+  const pt = api.compressBatch(moved, "deflate-raw");
+  const { port1, port2 } = new MessageChannel();
+  port1.postMessage(null, moved.map((x) => x.buffer));
+  expect(moved[0].length === 0, "transfer detached the input");
+  (await pt).forEach((b, i) => expect(Buffer.compare(Buffer.from(b), Buffer.from(want[i])) === 0, `input transferred after the call ${i}`));
+  port1.close();
+  port2.close();
   // level 0 (deflate_stored) against the reference-made layout goldens
   const l0 = JSON.parse(readFileSync(join(golden, "deflate_level0.json"), "utf8")).cases.filter((c) => c.n <= 300000);
   for (const format of ["deflate", "deflate-raw", "gzip"]) {

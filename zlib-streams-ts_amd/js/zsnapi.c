@@ -1,12 +1,12 @@
 /*
  * zsnapi.c -- the thin N-API addon between the JavaScript host side
  * (streams-api.mjs) and libzsgpu.so (include/zs_gpu.h).  Plain C against
- * node_api.h (N-API v8): it borrows the callers' Uint8Array backing stores for
- * the duration of one call (napi_get_typedarray_info; the arrays are held by a
- * reference until the batch settles, SURVEY.md 8(b) "Ownership"), hands their
- * addresses straight to zs_deflate_batch / zs_inflate_batch (the library packs
- * them into its pinned staging on the worker thread: no copy on the JS thread),
- * and returns the outputs as views of ONE external ArrayBuffer that the batch's
+ * node_api.h (N-API v8): it reads the callers' Uint8Array backing stores for
+ * the duration of one call (napi_get_typedarray_info, SURVEY.md 8(b)
+ * "Ownership"), copies them into one buffer the batch owns before the call
+ * returns (the caller may then modify, transfer or detach its buffers: N-API
+ * cannot pin an ArrayBuffer), hands that to zs_deflate_batch /
+ * zs_inflate_batch on the worker thread, and returns the outputs as views of ONE external ArrayBuffer that the batch's
  * output buffer becomes (freed when the views are collected: no copy back
  * either).  The batch calls return Promises: the GPU work runs on a libuv
  * worker thread (napi_async_work), so the event loop keeps running.  A batch
@@ -188,10 +188,10 @@ static int32_t arg_i32(napi_env env, napi_value v, int32_t dflt) {
   return x;
 }
 
-/* One batch in flight: the borrowed inputs (kept alive by `keep` until the
- * batch settles; the caller must not modify them meanwhile, as with the
- * reference's write()), the GPU work on a libuv worker thread (napi_async_work),
- * results built back on the JS thread. */
+/* One batch in flight: a copy of the inputs taken on the JS thread when the
+ * call is made (the caller may modify, transfer or detach its buffers right
+ * after: N-API cannot pin an ArrayBuffer's memory), the GPU work on a libuv
+ * worker thread (napi_async_work), results built back on the JS thread. */
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
@@ -203,10 +203,9 @@ typedef struct {
   uint64_t *in_off, *out_off;
   uint32_t *in_len, *cap, *olen, *cons, *check;
   int32_t *status, *phase, *msg;
-  const uint8_t *base; /* inputs: base + in_off[i] (the callers' own buffers) */
+  uint8_t *base;       /* inputs: base + in_off[i] (the job's own copy) */
   uint8_t *out;
   int out_given;       /* out now belongs to the results' external ArrayBuffer */
-  napi_ref keep;       /* a JS array holding the input Uint8Arrays */
   int rc;
   char err[512];
 } job;
@@ -214,7 +213,7 @@ typedef struct {
 static void job_free(job *j) {
   if (!j) return;
   free(j->in_off); free(j->out_off); free(j->in_len); free(j->cap); free(j->olen); free(j->cons); free(j->check);
-  free(j->status); free(j->phase); free(j->msg);
+  free(j->status); free(j->phase); free(j->msg); free(j->base);
   if (!j->out_given) {
     if (j->unbounded) zs_free(j->out);
     else free(j->out);
@@ -328,28 +327,22 @@ static void job_complete(napi_env env, napi_status st, void *data) {
     napi_reject_deferred(env, j->deferred, e);
   }
   napi_delete_async_work(env, j->work);
-  if (j->keep) napi_delete_reference(env, j->keep);
   job_free(j);
 }
 
-/* the inputs by address (base = the lowest), the Uint8Arrays kept alive in a
- * fresh array until the batch settles */
-static int borrow_inputs(napi_env env, job *j, napi_value arr, const view *v) {
-  uintptr_t lo = 0;
-  for (uint32_t i = 0; i < j->n; i++)
-    if (v[i].n && (!lo || (uintptr_t)v[i].p < lo)) lo = (uintptr_t)v[i].p;
-  j->base = (const uint8_t *)lo;
+/* the inputs copied, packed, into one buffer the job owns */
+static int copy_inputs(job *j, const view *v) {
+  uint64_t tot = 0;
   for (uint32_t i = 0; i < j->n; i++) {
-    j->in_off[i] = v[i].n ? (uint64_t)((uintptr_t)v[i].p - lo) : 0;
+    j->in_off[i] = tot;
     j->in_len[i] = (uint32_t)v[i].n;
+    tot += v[i].n;
   }
-  napi_value hold;
-  if (napi_create_array_with_length(env, j->n, &hold) != napi_ok) return -1;
-  for (uint32_t i = 0; i < j->n; i++) {
-    napi_value e;
-    if (napi_get_element(env, arr, i, &e) != napi_ok || napi_set_element(env, hold, i, e) != napi_ok) return -1;
-  }
-  return napi_create_reference(env, hold, 1, &j->keep) == napi_ok ? 0 : -1;
+  j->base = (uint8_t *)malloc(tot ? tot : 1);
+  if (!j->base) return -1;
+  for (uint32_t i = 0; i < j->n; i++)
+    if (v[i].n) memcpy(j->base + j->in_off[i], v[i].p, v[i].n);
+  return 0;
 }
 
 static napi_value queue_job(napi_env env, job *j, const char *name) {
@@ -358,7 +351,6 @@ static napi_value queue_job(napi_env env, job *j, const char *name) {
       napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name) != napi_ok ||
       napi_create_async_work(env, NULL, res_name, job_execute, job_complete, j, &j->work) != napi_ok ||
       napi_queue_async_work(env, j->work) != napi_ok) {
-    if (j->keep) napi_delete_reference(env, j->keep);
     job_free(j);
     return throw_code(env, ZS_MEM_ERROR, "could not queue the batch");
   }
@@ -394,9 +386,8 @@ static napi_value CompressBatch(napi_env env, napi_callback_info info) {
     tout += j->cap[i];
   }
   j->out = (uint8_t *)malloc(tout ? tout : 1);  /* (uninitialised: only the outputs are written) */
-  if (!j->out || borrow_inputs(env, j, argv[0], v) != 0) {
+  if (!j->out || copy_inputs(j, v) != 0) {
     free(v);
-    if (j->keep) napi_delete_reference(env, j->keep);
     job_free(j);
     return throw_code(env, ZS_MEM_ERROR, "out of host memory");
   }
@@ -447,9 +438,8 @@ static napi_value DecompressBatch(napi_env env, napi_callback_info info) {
     tout += j->cap[i];
   }
   j->out = j->unbounded ? NULL : (uint8_t *)malloc(tout ? tout : 1);  /* unbounded: the library allocates it */
-  if ((!j->unbounded && !j->out) || borrow_inputs(env, j, argv[0], v) != 0) {
+  if ((!j->unbounded && !j->out) || copy_inputs(j, v) != 0) {
     free(v);
-    if (j->keep) napi_delete_reference(env, j->keep);
     job_free(j);
     return throw_code(env, ZS_MEM_ERROR, "out of host memory");
   }
