@@ -96,6 +96,8 @@ struct zs_ctx {
   int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
   int cur_pw = 1;            // waves per stream of the current deflate batch's parse (zs_k_parse / _2w / _4w)
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
+  int pipeline = 1;          // L4..9 deflate batches: chunks pipelined over two streams (1: off; measured slower)
+  std::vector<hipEvent_t> dev;  // the pipeline's sweep-done events
   bool demand = false;       // L4..7: the sweep takes chain >> 2 steps, zs_k_parse_dw walks the rest where the parse needs them (exact; slower)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
   // the chain builders (zs_k_bucket, zs_k_prev, zs_k_fast) let same-address LDS atomics of
@@ -299,6 +301,7 @@ void zs_ctx_destroy(zs_ctx* c) {
     if (b->p) (void)hipHostFree(b->p);
   if (c->d_offs.p) (void)hipFree(c->d_offs.p);
   for (hipEvent_t e : c->hev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->dev) (void)hipEventDestroy(e);
   for (hipStream_t q : {c->h2d, c->d2h})
     if (q) {
       (void)hipStreamSynchronize(q);
@@ -352,6 +355,10 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
     c->seg_small_min = (uint32_t)value;
   }
   else if (!strcmp(name, "demand")) c->demand = value != 0;
+  else if (!strcmp(name, "pipeline")) {
+    if (value < 0 || value > 64) return fail(ZS_STREAM_ERROR, "pipeline must be in 0..64");
+    c->pipeline = value;
+  }
   else if (!strcmp(name, "parse_waves")) {
     if (value < 0 || value > 4 || value == 3) return fail(ZS_STREAM_ERROR, "parse_waves must be 0, 1, 2 or 4");
     c->parse_waves = value;
@@ -488,48 +495,53 @@ static uint32_t parse_seg_words(int w) {
                                : ZS_PARSE_SEG_WORDS;
 }
 
-// The deflate launch sequence of a batch (levels 1..9) on stream st.
-static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
-                          uint32_t max_len, uint32_t max_blk, const uint8_t* d_in, const uint64_t* d_in_off,
-                          const uint32_t* d_in_len, uint8_t* d_out, const uint64_t* d_out_off,
-                          const uint32_t* d_out_cap, const uint64_t* d_pos, const uint32_t* d_blk, zs_stream* d_st,
-                          uint32_t* syms, uint32_t* pscr, uint32_t* check, int32_t* d_status, uint32_t* d_out_len) {
-  zs_block* d_bk = c->blocks.as<zs_block>();
-  const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
-  MARK("start");
-  if (wrap) {
-    zs_k_checksum<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, check, wrap == 1 ? 1 : 2);
-    zs_k_copy_check<<<nblocks_s, nthreads_s, 0, st>>>(check, d_st, (int)n);
-    MARK("checksum");
-  }
-  if (level >= 4) {
-    const dim3 g((max_len + 8191) / 8192, n);
-    if (c->match_sweep) {
-      // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
-      // longer ones: chain links + per-tile chain walk (deflate_match.hip)
-      (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<n, 256, 0, st>>>(
-          d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
-      if (max_len > 65537u)
-        (c->lane_order ? zs_k_prev<true> : zs_k_prev<false>)<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos,
-                                                                               c->prevd.as<uint16_t>(), 65537u);
-      MARK("bucket");
-      zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
-                                     cfg.chain, cfg.nice, c->cur_pw == ZS_PARSEDW_WAVES ? 1 : 0);
-      MARK("sweep");
-      if (max_len > 65537u) {
-        zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
-                                       cfg.chain, cfg.nice, 65537u);
-        MARK("match");
-      }
-    } else {
-      // cross-check (option match_sweep = 0): the chain-walk kernels for every stream
+// The match finding of streams [0, n) of a batch (levels 4..9) on stream st:
+// every per-stream array already offset to the first stream.
+static int deflate_match(zs_ctx* c, hipStream_t st, const zs_level_cfg& cfg, uint32_t n, uint32_t max_len,
+                         const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                         const uint64_t* d_pos) {
+  const dim3 g((max_len + 8191) / 8192, n);
+  if (c->match_sweep) {
+    // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
+    // longer ones: chain links + per-tile chain walk (deflate_match.hip)
+    (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<n, 256, 0, st>>>(
+        d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
+    if (max_len > 65537u)
       (c->lane_order ? zs_k_prev<true> : zs_k_prev<false>)<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos,
-                                                                             c->prevd.as<uint16_t>(), 0u);
-      MARK("prev");
-      if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
-                                                   c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
+                                                                             c->prevd.as<uint16_t>(), 65537u);
+    MARK("bucket");
+    zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
+                                   cfg.chain, cfg.nice, c->cur_pw == ZS_PARSEDW_WAVES ? 1 : 0);
+    MARK("sweep");
+    if (max_len > 65537u) {
+      zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
+                                     cfg.chain, cfg.nice, 65537u);
       MARK("match");
     }
+  } else {
+    // cross-check (option match_sweep = 0): the chain-walk kernels for every stream
+    (c->lane_order ? zs_k_prev<true> : zs_k_prev<false>)<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos,
+                                                                           c->prevd.as<uint16_t>(), 0u);
+    MARK("prev");
+    if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
+                                                 c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
+    MARK("match");
+  }
+  return ZS_OK;
+}
+
+// The rest of the deflate sequence of streams [0, n) on stream st: the parse
+// (levels 4..9) or deflate_fast (1..3), trees, layout, emit, wrapper, statuses.
+// Per-stream arrays are offset to the first stream; syms and pscr too (kernels
+// index them by the launch-local stream index).
+static int deflate_tail(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
+                        uint32_t max_blk, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                        uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap, const uint64_t* d_pos,
+                        const uint32_t* d_blk, zs_stream* d_st, uint32_t* syms, uint32_t* pscr, int32_t* d_status,
+                        uint32_t* d_out_len) {
+  zs_block* d_bk = c->blocks.as<zs_block>();
+  const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
+  if (level >= 4) {
     const int pw = c->cur_pw;  // waves per stream of the lazy parse (deflate_parse.hip)
     if (pw == ZS_PARSEDW_WAVES) {
       zs_k_parse_dw<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), syms, d_bk,
@@ -563,6 +575,72 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
   if (wrap) zs_k_wrap<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_out, d_out_off, d_in_len, wrap, level, (int)n);
   zs_k_finish<<<nblocks_s, nthreads_s, 0, st>>>(d_st, d_status, d_out_len, (int)n);
   MARK("finish");
+  return ZS_OK;
+}
+
+// The deflate launch sequence of a batch (levels 1..9) on stream st.  Levels
+// 4..9 with the sweep run as a pipeline of chunks of streams (option pipeline):
+// chunk j's bucket + sweep on st, its parse .. emit on the side stream once its
+// sweep is done -- beside chunk j + 1's sweep, with which the parse, trees and
+// emit workgroups co-reside on a CU (LDS 141.6 + 19.5 KiB, VGPRs 4 x 80 + 184).
+static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
+                          const uint32_t* in_len, const uint8_t* d_in, const uint64_t* d_in_off,
+                          const uint32_t* d_in_len, uint8_t* d_out, const uint64_t* d_out_off,
+                          const uint32_t* d_out_cap, const uint64_t* d_pos, const uint32_t* d_blk, zs_stream* d_st,
+                          uint32_t* syms, uint32_t* pscr, uint32_t* check, int32_t* d_status, uint32_t* d_out_len) {
+  const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
+  MARK("start");
+  if (wrap) {
+    zs_k_checksum<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, check, wrap == 1 ? 1 : 2);
+    zs_k_copy_check<<<nblocks_s, nthreads_s, 0, st>>>(check, d_st, (int)n);
+    MARK("checksum");
+  }
+  uint32_t K = 1;
+  if (level >= 4 && c->match_sweep && c->cur_pw != ZS_PARSEDW_WAVES)
+    K = c->pipeline ? (uint32_t)c->pipeline : 1u;
+  K = std::max(1u, std::min(K, n));
+  const uint32_t pwords = parse_seg_words(c->cur_pw);
+  auto range = [&](uint32_t j, uint32_t& a, uint32_t& e, uint32_t& mlen, uint32_t& mblk) {
+    a = (uint32_t)((uint64_t)n * j / K);
+    e = (uint32_t)((uint64_t)n * (j + 1) / K);
+    mlen = 0;
+    mblk = 0;
+    for (uint32_t i = a; i < e; i++) {
+      mlen = std::max(mlen, in_len[i]);
+      mblk = std::max(mblk, in_len[i] / ZS_SYM_END + 2);
+    }
+  };
+  auto tail = [&](hipStream_t s2, uint32_t a, uint32_t e, uint32_t mblk) {
+    return deflate_tail(c, s2, level, wrap, cfg, e - a, mblk, d_in, d_in_off + a, d_in_len + a, d_out,
+                        d_out_off + a, d_out_cap + a, d_pos + a, d_blk + a, d_st + a, syms + a,
+                        pscr + (size_t)pwords * a, d_status + a, d_out_len + a);
+  };
+  if (K == 1) {
+    uint32_t a, e, mlen, mblk;
+    range(0, a, e, mlen, mblk);
+    if (level >= 4) {
+      const int r = deflate_match(c, st, cfg, n, mlen, d_in, d_in_off, d_in_len, d_pos);
+      if (r != ZS_OK) return r;
+    }
+    return tail(st, 0, n, mblk);
+  }
+  while (c->dev.size() < K) {
+    hipEvent_t ev;
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->dev.push_back(ev);
+  }
+  for (uint32_t j = 0; j < K; j++) {
+    uint32_t a, e, mlen, mblk;
+    range(j, a, e, mlen, mblk);
+    int r = deflate_match(c, st, cfg, e - a, mlen, d_in, d_in_off + a, d_in_len + a, d_pos + a);
+    if (r != ZS_OK) return r;
+    HIPCHK(hipEventRecord(c->dev[j], st));
+    HIPCHK(hipStreamWaitEvent(c->side, c->dev[j], 0));
+    if ((r = mark(c, c->side, "sweep_wait")) != ZS_OK) return r;  // (the side stream's phases start here)
+    if ((r = tail(c->side, a, e, mblk)) != ZS_OK) return r;
+  }
+  HIPCHK(hipEventRecord(c->join, c->side));
+  HIPCHK(hipStreamWaitEvent(st, c->join, 0));
   return ZS_OK;
 }
 
@@ -645,7 +723,9 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
   HIPCHK(c->check.ensure(4ull * n));
   HIPCHK(hipMemcpyAsync(c->meta.p, hm, ml.bytes, hipMemcpyHostToDevice, st));
   uint8_t* dm = c->meta.as<uint8_t>();
-  const int r = deflate_launch(c, st, level, wrap, kLevels[level], n, max_len, max_blk, d_in,
+  (void)max_len;
+  (void)max_blk;
+  const int r = deflate_launch(c, st, level, wrap, kLevels[level], n, in_len, d_in,
                                (const uint64_t*)(dm + ml.in_off), (const uint32_t*)(dm + ml.in_len), d_out,
                                (const uint64_t*)(dm + ml.out_off), (const uint32_t*)(dm + ml.out_cap),
                                (const uint64_t*)(dm + ml.pos_base), (const uint32_t*)(dm + ml.blk_base),
