@@ -1,7 +1,6 @@
-"""CPU check of the L4..L9 match finder's algorithm for streams of <= 65,537
-bytes (tools/emu/emu_bucket_sweep.c models zs_k_bucket + zs_k_sweep of
-deflate_sweep.hip): the counting sort by (hash, position), the lock-step
-sweep over bucket predecessors with 12-byte signatures, the liveness keys,
+"""CPU check of the L4..L9 match finder's algorithm (tools/emu/emu_bucket_sweep.c
+models zs_k_bucket + zs_k_sweep of deflate_sweep.hip over capi.cpp's windows):
+the counting sort by (hash, position), the lock-step sweep over bucket predecessors with 12-byte signatures, the liveness keys,
 the chain >> 2 snapshot and the deferred long candidates (with the re-walk
 after a fifth) reproduce a direct longest_match (deflate.ts:1053-1115) at
 every position, for both budgets and the slide-NIL flag, at the level
@@ -60,6 +59,33 @@ def test_sweep_model_matches_longest_match(emu, tmp_path, level):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout, r.stdout
     assert " 0 in 7-bit" not in r.stdout  # both signature forms were exercised
+
+
+def _long_streams():
+    specs = [("text", 65538), ("mixed", 100000), ("text", 262144), ("zeros", 131073), ("rand", 98317)]
+    out = [corpus.make({"kind": k, "n": n, "seed": 8100 + i}) for i, (k, n) in enumerate(specs)]
+    b = bytearray(corpus.rand(78, 200000))  # head candidates at exactly MAX_DIST around the window seams
+    for at in (65519, 65520, 98272, 150001):
+        b[at:at + 40] = b[at - 32506:at - 32506 + 40]
+    out.append(bytes(b))
+    out.append(bytes(x & 0x7F for x in corpus.rand(95, 150000)))
+    return out
+
+
+@pytest.mark.parametrize("level", [4, 7])
+def test_windowed_sweep_model_matches_longest_match(emu, tmp_path, level):
+    """Streams over 65,537 bytes: the sweep's windows (capi.cpp sweep_table -- a first window owning [0, 65520),
+    then 32,752 own positions after a 32,768-position look-back, u16 window-relative members) give every position
+    exactly once the result of a direct longest_match over the whole stream's chain."""
+    streams = _long_streams()
+    blob = struct.pack("<I", len(streams)) + struct.pack("<%dI" % len(streams), *map(len, streams)) + b"".join(streams)
+    f = tmp_path / "long.bin"
+    f.write_bytes(blob)
+    chain, nice = LEVELS[level]
+    r = subprocess.run([emu, str(f), str(chain), str(nice)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout, r.stdout
+    assert "checked %d positions" % sum(len(s) - 2 for s in streams) in r.stdout, r.stdout
 
 
 DEMAND_SRC = os.path.join(ROOT, "tools", "emu", "emu_demand.c")

@@ -65,10 +65,10 @@ def test_block_boundaries_and_stored_blocks(engine):
 
 @pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
 def test_sweep_match_table_equals_chain_walk(engine, level):
-    """zs_k_bucket + zs_k_sweep (deflate_sweep.hip) and zs_k_prev + zs_k_match
-    (deflate_match.hip, the kernels of streams over 65,537 B) compute the same
-    longest_match table -- both budgets and the slide-NIL flag -- at every
-    position, and the same output bytes (= the oracle's)."""
+    """zs_k_bucket + zs_k_sweep (deflate_sweep.hip; streams over 65,537 B in
+    windows) and zs_k_prev + zs_k_match (deflate_match.hip, the chain walk: option
+    match_sweep = 0) compute the same longest_match table -- both budgets and the
+    slide-NIL flag -- at every position, and the same output bytes (= the oracle's)."""
     rng = random.Random(500 + level)
     inputs = []
     for k in range(20):
@@ -84,6 +84,11 @@ def test_sweep_match_table_equals_chain_walk(engine, level):
     inputs.append(bytes(x & 0x7F for x in corpus.rand(91 + level, 65536)))
     inputs.append(bytes(0x41 + (x & 3) for x in corpus.rand(92 + level, 65536)))
     inputs.append(bytes(x & 0x7F for x in corpus.rand(93, 20000)) + corpus.text(94, 45537))
+    # streams over 65,537 bytes: the sweep in windows (a first one of 65,535 positions, then 32,767 own positions
+    # after a 32,768-position look-back each), at and around the window boundaries and up to 256 KiB
+    for n, kind in ((65538, "text"), (98302, "mixed"), (98303, "text"), (130836, "zeros"), (262144, "text"),
+                    (200001, "mixed"), (70000, "rand")):
+        inputs.append(corpus.make({"kind": kind, "n": n, "seed": rng.randrange(1 << 32)}))
     # (match_sweep, demand): the full sweep, the chain walk, and the demand-mode sweep (chain >> 2 steps; the
     # parse walks the rest where it asks for the full budget, zs_k_parse_dw)
     tables, outs = [], []

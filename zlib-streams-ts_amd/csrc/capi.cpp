@@ -98,6 +98,8 @@ struct zs_ctx {
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
   int pipeline = 1;          // L4..9 deflate batches: chunks pipelined over two streams (1: off; measured slower)
   std::vector<hipEvent_t> dev;  // the pipeline's sweep-done events
+  std::vector<uint32_t> hwin0;  // the sweep's windows: each stream's first (sweep_table)
+  std::vector<uint64_t> hpos;
   bool demand = false;       // L4..7: the sweep takes chain >> 2 steps, zs_k_parse_dw walks the rest where the parse needs them (exact; slower)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
   // the chain builders (zs_k_bucket, zs_k_prev, zs_k_fast) let same-address LDS atomics of
@@ -409,8 +411,8 @@ uint64_t zs_deflate_bound(uint64_t n, int wbits) {  // deflate.ts:615-674, memLe
 
 // Device metadata block: in_off | in_len | out_off | out_cap | pos_base | blk_base
 struct MetaLayout {
-  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, bytes;
-  explicit MetaLayout(uint32_t n) {
+  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, segs, bytes;
+  explicit MetaLayout(uint32_t n, uint32_t nwin = 0) {
     size_t o = 0;
     auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~size_t(255); return r; };
     in_off = take(8ull * n);
@@ -419,6 +421,7 @@ struct MetaLayout {
     out_cap = take(4ull * n);
     pos_base = take(8ull * n);
     blk_base = take(4ull * n);
+    segs = take(sizeof(zs_sweep_seg) * nwin);  // the sweep's windows (levels 4..9)
     bytes = o;
   }
 };
@@ -495,35 +498,59 @@ static uint32_t parse_seg_words(int w) {
                                : ZS_PARSE_SEG_WORDS;
 }
 
-// The match finding of streams [0, n) of a batch (levels 4..9) on stream st:
-// every per-stream array already offset to the first stream.
-static int deflate_match(zs_ctx* c, hipStream_t st, const zs_level_cfg& cfg, uint32_t n, uint32_t max_len,
-                         const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
-                         const uint64_t* d_pos) {
-  const dim3 g((max_len + 8191) / 8192, n);
-  if (c->match_sweep) {
-    // streams of <= 65537 bytes: counting sort by hash + lock-step sweep (deflate_sweep.hip);
-    // longer ones: chain links + per-tile chain walk (deflate_match.hip)
-    (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<n, 256, 0, st>>>(
-        d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
-    if (max_len > 65537u)
-      (c->lane_order ? zs_k_prev<true> : zs_k_prev<false>)<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos,
-                                                                             c->prevd.as<uint16_t>(), 65537u);
-    MARK("bucket");
-    zs_k_sweep<<<n, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
-                                   cfg.chain, cfg.nice, c->cur_pw == ZS_PARSEDW_WAVES ? 1 : 0);
-    MARK("sweep");
-    if (max_len > 65537u) {
-      zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(), c->mres.as<uint2>(),
-                                     cfg.chain, cfg.nice, 65537u);
-      MARK("match");
+// The sweep's window table of a batch (into `out`, batch stream indices) and each
+// stream's first window (win0[n] = the total).  Members: u16 per position for a
+// stream of one window (pos_base); 65,536 per window after them for longer ones.
+static void sweep_table(uint32_t n, const uint32_t* in_len, const uint64_t* pos, uint64_t P, zs_sweep_seg* out,
+                        std::vector<uint32_t>& win0, uint64_t& members) {
+  uint64_t mb = (P + 7) & ~7ull;
+  uint32_t w = 0;
+  win0.resize(n + 1);
+  for (uint32_t i = 0; i < n; i++) {
+    win0[i] = w;
+    const uint32_t len = in_len[i];
+    if (len <= 65537u) {
+      if (out) out[w] = {i, 0u, 0u, len, pos[i], 0};
+      w++;
+      continue;
     }
+    for (uint64_t lo = 0; lo < len; mb += 65536, w++) {
+      const uint32_t base = lo == 0 ? 0u : (uint32_t)lo - 32768u;
+      if (out) out[w] = {i, base, (uint32_t)lo - base, lo == 0 ? ZS_SEG_FIRST : 32768u + ZS_SEG_OWN, mb, 0};
+      lo += lo == 0 ? ZS_SEG_FIRST : ZS_SEG_OWN;
+    }
+  }
+  win0[n] = w;
+  members = mb;
+}
+
+// The match finding of streams [a, e) of a batch (levels 4..9) on stream st
+// (device arrays of the whole batch).  With the sweep, every stream is cut into
+// WINDOWS of at most 65,535 inserted positions (zs_sweep_seg, sweep_table): a
+// stream of up to 65,537 bytes is one; a longer one has a first window owning
+// positions [0, 65520) and then windows owning 32,752 positions each after a
+// 32,768-position look-back (more than MAX_DIST: every candidate of an own
+// position is in its window).
+static int deflate_match(zs_ctx* c, hipStream_t st, const zs_level_cfg& cfg, uint32_t a, uint32_t e,
+                         uint32_t max_len, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                         const uint64_t* d_pos, const zs_sweep_seg* d_segs) {
+  const uint32_t n = e - a;
+  if (c->match_sweep) {
+    const uint32_t w0 = c->hwin0[a], nw = c->hwin0[e] - w0;
+    // a window: counting sort by hash + lock-step sweep (deflate_sweep.hip)
+    (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<nw, 256, 0, st>>>(
+        d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
+    MARK("bucket");
+    zs_k_sweep<<<nw, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(),
+                                    c->mres.as<uint2>(), cfg.chain, cfg.nice, c->cur_pw == ZS_PARSEDW_WAVES ? 1 : 0);
+    MARK("sweep");
   } else {
     // cross-check (option match_sweep = 0): the chain-walk kernels for every stream
-    (c->lane_order ? zs_k_prev<true> : zs_k_prev<false>)<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos,
-                                                                           c->prevd.as<uint16_t>(), 0u);
+    const dim3 g((max_len + 8191) / 8192, n);
+    (c->lane_order ? zs_k_prev<true> : zs_k_prev<false>)<<<n, 64, 0, st>>>(d_in, d_in_off + a, d_in_len + a,
+                                                                           d_pos + a, c->prevd.as<uint16_t>(), 0u);
     MARK("prev");
-    if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, c->prevd.as<uint16_t>(),
+    if (max_len) zs_k_match<<<g, 1024, 0, st>>>(d_in, d_in_off + a, d_in_len + a, d_pos + a, c->prevd.as<uint16_t>(),
                                                  c->mres.as<uint2>(), cfg.chain, cfg.nice, 0u);
     MARK("match");
   }
@@ -584,7 +611,8 @@ static int deflate_tail(zs_ctx* c, hipStream_t st, int level, int wrap, const zs
 // sweep is done -- beside chunk j + 1's sweep, with which the parse, trees and
 // emit workgroups co-reside on a CU (LDS 141.6 + 19.5 KiB, VGPRs 4 x 80 + 184).
 static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
-                          const uint32_t* in_len, const uint8_t* d_in, const uint64_t* d_in_off,
+                          const uint32_t* in_len, const zs_sweep_seg* d_segs, const uint8_t* d_in,
+                          const uint64_t* d_in_off,
                           const uint32_t* d_in_len, uint8_t* d_out, const uint64_t* d_out_off,
                           const uint32_t* d_out_cap, const uint64_t* d_pos, const uint32_t* d_blk, zs_stream* d_st,
                           uint32_t* syms, uint32_t* pscr, uint32_t* check, int32_t* d_status, uint32_t* d_out_len) {
@@ -619,7 +647,7 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
     uint32_t a, e, mlen, mblk;
     range(0, a, e, mlen, mblk);
     if (level >= 4) {
-      const int r = deflate_match(c, st, cfg, n, mlen, d_in, d_in_off, d_in_len, d_pos);
+      const int r = deflate_match(c, st, cfg, 0, n, mlen, d_in, d_in_off, d_in_len, d_pos, d_segs);
       if (r != ZS_OK) return r;
     }
     return tail(st, 0, n, mblk);
@@ -632,7 +660,7 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
   for (uint32_t j = 0; j < K; j++) {
     uint32_t a, e, mlen, mblk;
     range(j, a, e, mlen, mblk);
-    int r = deflate_match(c, st, cfg, e - a, mlen, d_in, d_in_off + a, d_in_len + a, d_pos + a);
+    int r = deflate_match(c, st, cfg, a, e, mlen, d_in, d_in_off, d_in_len, d_pos, d_segs);
     if (r != ZS_OK) return r;
     HIPCHK(hipEventRecord(c->dev[j], st));
     HIPCHK(hipStreamWaitEvent(c->side, c->dev[j], 0));
@@ -686,8 +714,18 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
     }
     return r;
   }
-  // host-side layout: workspace bases
-  MetaLayout ml(n);
+  // host-side layout: workspace bases (and the sweep's windows, levels 4..9)
+  const bool sweep = level >= 4 && c->match_sweep;
+  uint64_t P = 0, members = 0;
+  uint32_t B = 0, max_len = 0, max_blk = 0;
+  c->hpos.resize(n);
+  for (uint32_t i = 0; i < n; i++) {
+    if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
+    c->hpos[i] = P;
+    P += ((uint64_t)in_len[i] + 7) & ~7ull;  // per-position tables start 8-aligned (16-B link loads in zs_k_match)
+  }
+  if (sweep) sweep_table(n, in_len, c->hpos.data(), P, nullptr, c->hwin0, members);
+  MetaLayout ml(n, sweep ? c->hwin0[n] : 0u);
   c->hmeta.resize(ml.bytes);
   c->last_n = n;
   uint8_t* hm = c->hmeta.data();
@@ -697,20 +735,17 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
   memcpy(hm + ml.out_cap, out_cap, 4ull * n);
   uint64_t* pos_base = (uint64_t*)(hm + ml.pos_base);
   uint32_t* blk_base = (uint32_t*)(hm + ml.blk_base);
-  uint64_t P = 0;
-  uint32_t B = 0, max_len = 0, max_blk = 0;
+  memcpy(pos_base, c->hpos.data(), 8ull * n);
+  if (sweep) sweep_table(n, in_len, pos_base, P, (zs_sweep_seg*)(hm + ml.segs), c->hwin0, members);
   for (uint32_t i = 0; i < n; i++) {
-    if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
-    pos_base[i] = P;
     blk_base[i] = B;
-    P += ((uint64_t)in_len[i] + 7) & ~7ull;  // per-position tables start 8-aligned (16-B link loads in zs_k_match)
     const uint32_t nb = in_len[i] / ZS_SYM_END + 2;
     B += nb;
     max_len = std::max(max_len, in_len[i]);
     max_blk = std::max(max_blk, nb);
   }
   HIPCHK(c->meta.ensure(ml.bytes));
-  HIPCHK(c->prevd.ensure(2 * P + 64));
+  HIPCHK(c->prevd.ensure(2 * std::max(members, P) + 64));
   HIPCHK(c->mres.ensure(8 * P + 64));
   HIPCHK(c->syms.ensure(4 * (P + n) + 64));
   c->cur_pw = level >= 4 ? parse_waves_for(c, n, level) : 1;
@@ -725,7 +760,7 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
   uint8_t* dm = c->meta.as<uint8_t>();
   (void)max_len;
   (void)max_blk;
-  const int r = deflate_launch(c, st, level, wrap, kLevels[level], n, in_len, d_in,
+  const int r = deflate_launch(c, st, level, wrap, kLevels[level], n, in_len, (const zs_sweep_seg*)(dm + ml.segs), d_in,
                                (const uint64_t*)(dm + ml.in_off), (const uint32_t*)(dm + ml.in_len), d_out,
                                (const uint64_t*)(dm + ml.out_off), (const uint32_t*)(dm + ml.out_cap),
                                (const uint64_t*)(dm + ml.pos_base), (const uint32_t*)(dm + ml.blk_base),

@@ -48,8 +48,9 @@
 #include "zs_kernels.h"
 #include <type_traits>
 
-#define ZS_SWEEP_MAX 65537u  // position + 1 <= 65535 for every inserted position: u16 members and offsets
-#define ZS_SW_WIN_WORDS ((ZS_SWEEP_MAX + 20u + 3u) / 4u + 2u)
+// the window in LDS: ZS_SEG_WPOS inserted positions, a longest match past the
+// last of them (258 bytes) and the 16-byte overreach of the word compares
+#define ZS_SW_WIN_WORDS ((ZS_SEG_WPOS + 258u + 20u + 3u) / 4u + 2u)
 #define ZS_SW_RING 128u  // records per wave (two blocks of 64 members), stored twice (mirror)
 #ifndef ZS_SW_EXP
 #define ZS_SW_EXP 0  // experiments (timing A/B only; 0 in the product)
@@ -98,20 +99,24 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
                                                             const uint64_t* __restrict__ in_off,
                                                             const uint32_t* __restrict__ in_len,
                                                             const uint64_t* __restrict__ pos_base,
+                                                            const zs_sweep_seg* __restrict__ segs,
                                                             uint16_t* __restrict__ members, uint2* __restrict__ mres) {
   __shared__ uint32_t cnt[16384];
   __shared__ uint32_t part[ZS_BK_THREADS];
   __shared__ uint32_t stg[ZS_BK_CHUNK / 4 + 2];
   __shared__ uint16_t q[2][ZS_BK_CHUNK];
-  const int s = blockIdx.x;
-  const uint32_t n = in_len[s];
-  if (n > ZS_SWEEP_MAX) return;  // zs_k_prev / zs_k_match's stream
+  const zs_sweep_seg G = segs[blockIdx.x];
+  const int s = (int)G.s;
+  const uint32_t nrel = in_len[s] - G.base;  // bytes from the window's start to the stream's end
   const uint32_t tid = threadIdx.x;
-  const uint8_t* src = in + in_off[s];
-  uint16_t* mem = members + pos_base[s];
-  uint2* out = mres + pos_base[s];
-  const uint32_t m = n > 2 ? n - 2 : 0u;  // inserted positions (deflate.ts:1367-1370)
-  for (uint32_t p = m + tid; p < n; p += ZS_BK_THREADS) out[p] = make_uint2(0, 0);
+  const uint8_t* src = in + in_off[s] + G.base;
+  uint16_t* mem = members + G.mb;
+  uint2* out = mres + pos_base[s] + G.base;
+  // inserted positions of the window (deflate.ts:1367-1370: p <= n - 3), and the bytes their hashes read
+  const uint32_t m = nrel > 2 ? min(nrel - 2, G.ohi) : 0u;
+  const uint32_t n = min(nrel, m + 2u);
+  if (nrel - m <= 2u)  // the window reaches the stream's end: its last positions are not inserted
+    for (uint32_t p = m + tid; p < nrel; p += ZS_BK_THREADS) out[p] = make_uint2(0, 0);
   if (m == 0) return;
   for (uint32_t i = tid; i < 16384 / 4; i += ZS_BK_THREADS) reinterpret_cast<uint4*>(cnt)[i] = make_uint4(0, 0, 0, 0);
   const bool aligned = ((uintptr_t)src & 3u) == 0;
@@ -281,10 +286,10 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
   }
   BK_MARK(2);
 }
-template __global__ void zs_k_bucket<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, uint16_t*,
-                                           uint2*);
-template __global__ void zs_k_bucket<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*, uint16_t*,
-                                            uint2*);
+template __global__ void zs_k_bucket<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*,
+                                           const zs_sweep_seg*, uint16_t*, uint2*);
+template __global__ void zs_k_bucket<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*,
+                                            const zs_sweep_seg*, uint16_t*, uint2*);
 
 // --------------------------------------------------------------- zs_k_sweep
 static __device__ __forceinline__ uint32_t sw_word(const uint32_t* win, uint32_t off) {
@@ -434,15 +439,21 @@ extern "C" int zs_sw_stats(unsigned long long* out) {
 
 template <bool A7, bool MW>
 static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, uint16_t* mw, uint32_t* next,
-                                               uint32_t n, const uint16_t* mem, uint2* out, int chain,
-                                               int nice_cfg, bool demand) {
+                                               uint32_t n, uint32_t m, uint32_t olo, uint32_t ohi,
+                                               const uint16_t* mem, uint2* out, int chain, int nice_cfg,
+                                               bool demand) {
+  // n: bytes from the window's start to the stream's end; m: the window's
+  // members (inserted positions); results for the own positions [olo, ohi)
   using Sig = SwSig<A7>;
-  const uint32_t m = n - 2;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t budget = (uint32_t)chain, budget_s = (uint32_t)chain >> 2;
   // the steps swept: the full chain, or (demand) the first chain >> 2 -- the rest
   // only where the parse asks for the full budget (zs_k_parse_dw)
+#if ZS_SW_EXP & 128
+  const uint32_t sbud = 4u;  // (timing: the per-chunk cost without chain steps past 4)
+#else
   const uint32_t sbud = demand ? budget_s : budget;
+#endif
   const uint32_t nchunks = (m + 63) / 64;
   auto put_rec = [&](int j, uint4 r) {
     const uint32_t i = (uint32_t)j & (ZS_SW_RING - 1);
@@ -491,7 +502,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     const uint32_t cn = claim();
     const int k0 = (int)(64 * c);
     const int k = k0 + (int)lane;
-    const bool own = (uint32_t)k < m;
+    const bool mem_ok = (uint32_t)k < m;
     SW_STAT(0, 1);
     const uint32_t p = pf_p, qb = pf_b;  // (0 past the members)
     if (cn < nchunks) {
@@ -499,6 +510,10 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
       pf_b = fetch((int)(64 * cn + lane) - 64);
     }
     c = cn;
+    // the lane's position is one of the window's own (a later window of a long
+    // stream: its first 32,768 positions are look-back, candidates only)
+    const bool own = mem_ok && p >= olo && p < ohi;
+    if (__builtin_amdgcn_ballot_w64(own) == 0) continue;
     mw0 = k0 - (int)sbud - (demand ? 1 : 0);  // (demand: member k - sbud - 1 for the probe below)
     if (MW) mw[k - mw0] = (uint16_t)p;
     Sig S;
@@ -515,8 +530,12 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     // ring: this chunk's block and the one before it
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    put_rec(k, own ? make_rec(p) : make_uint4(0, 0, 0, 0));
+    put_rec(k, mem_ok ? make_rec(p) : make_uint4(0, 0, 0, 0));
+#if ZS_SW_EXP & 256
+    put_rec(k - 64, make_uint4(qb, qb, qb, 0));  // (timing: the block before without its window reads)
+#else
     load_rec_q(k - 64, qb);
+#endif
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
 
@@ -615,7 +634,9 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     }
     // Steps [ta, tb] of block b (ta = 1 mod 4, tb = 0 mod 4, wave-uniform):
     // step t reads slot base - t, one address per group, immediate offsets inside.
-    auto group_fast = [&](uint32_t base, uint32_t t0, auto G) __attribute__((always_inline)) {
+    // (every lane runs it -- no divergent region, whose join costs register moves --
+    // and a lane whose chain has ended folds nothing)
+    auto group_fast = [&](uint32_t base, uint32_t t0, auto G, bool live) __attribute__((always_inline)) {
       constexpr uint32_t N = decltype(G)::value;
       // from the group's lowest slot up: one address, immediate offsets
       const uint32_t lo = base - t0 - (N - 1u);
@@ -632,7 +653,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         gm = max(max3(sc[0], sc[1], sc[2]), max3(sc[3], sc[4], max3(sc[5], sc[6], sc[7])));
       else
         gm = max3(sc[0], sc[1], max(sc[2], sc[3]));
-      fold(gm, t0, sc, N, base);
+      fold(live ? gm : 0u, t0, sc, N, base);
     };
     auto group_masked = [&](uint32_t base, uint32_t t0, uint32_t t1) __attribute__((always_inline)) {
       uint32_t sc[8];
@@ -670,10 +691,8 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
 #endif
           SW_STAT(1, 1);
           SW_STAT(4, t1 - t0 + 1u);
-          if (mine) {  // exec = the live lanes
-            if (t1 - t0 == 7u) group_fast(base, t0, G8{});
-            else group_fast(base, t0, G4{});
-          }
+          if (t1 - t0 == 7u) group_fast(base, t0, G8{}, mine);
+          else group_fast(base, t0, G4{}, mine);
         } else {
           SW_STAT(2, 1);
           SW_STAT(4, t1 - t0 + 1u);
@@ -768,7 +787,11 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
           if (((sw_hash(sw_word(win, q)) << 16) | q) > klim) rx = ZS_MORE | (uint32_t)k;
         }
       }
+#if ZS_SW_EXP & 512
+      if (rx == 0x12345678u) out[p] = make_uint2(rx, ry);  // (timing: without the result stores)
+#else
       out[p] = make_uint2(rx, ry);
+#endif
     }
   }
 }
@@ -776,18 +799,22 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
 __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                    const uint32_t* __restrict__ in_len,
                                                    const uint64_t* __restrict__ pos_base,
+                                                   const zs_sweep_seg* __restrict__ segs,
                                                    const uint16_t* __restrict__ members, uint2* __restrict__ mres,
                                                    int chain, int nice_cfg, int demand) {
   __shared__ __attribute__((aligned(16))) SwRing ring[16];
   __shared__ __attribute__((aligned(16))) uint32_t win[ZS_SW_WIN_WORDS];
   __shared__ uint16_t mwin[16][ZS_SW_MW];
   __shared__ uint32_t next;
-  const int s = blockIdx.x;
-  const uint32_t n = in_len[s];
-  if (n > ZS_SWEEP_MAX || n < 3) return;
-  const uint8_t* src = in + in_off[s];
-  // the whole stream in LDS, zero padded (reads run up to 16 bytes past n);
-  // the OR of its bytes' top bits picks the signature form
+  const zs_sweep_seg G = segs[blockIdx.x];
+  const int s = (int)G.s;
+  const uint32_t n = in_len[s] - G.base;  // bytes from the window's start to the stream's end
+  if (n < 3) return;
+  const uint32_t m = min(n - 2, G.ohi);
+  const uint8_t* src = in + in_off[s] + G.base;
+  // the window in LDS, zero padded past the stream's end (reads run up to 16
+  // bytes past a longest match); the OR of its bytes' top bits picks the
+  // signature form
   uint32_t hi = 0;
   if ((((uintptr_t)src) & 15u) == 0) {
     for (uint32_t i = threadIdx.x; 4 * i < ZS_SW_WIN_WORDS; i += 1024) {
@@ -816,15 +843,17 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
   if (threadIdx.x == 0) next = 0;
   const bool a7 = !__syncthreads_or((hi & 0x80808080u) != 0);
   SwRing* const R = &ring[threadIdx.x >> 6];
-  const uint16_t* mem = members + pos_base[s];
-  uint2* out = mres + pos_base[s];
+  const uint16_t* mem = members + G.mb;
+  uint2* out = mres + pos_base[s] + G.base;
   uint16_t* const mw = mwin[threadIdx.x >> 6];
-  const bool dm = demand != 0;
+  // (demand mode: the parse's walks read a whole stream's members and window -- streams of one window only)
+  const bool dm = demand != 0 && G.base == 0 && n <= 65537u;
+  const uint32_t olo = G.olo, ohi = G.ohi;
   if ((dm ? (chain >> 2) + 1 : chain) + 64 <= (int)ZS_SW_MW) {
-    if (a7) sw_body<true, true>(win, R, mw, &next, n, mem, out, chain, nice_cfg, dm);
-    else sw_body<false, true>(win, R, mw, &next, n, mem, out, chain, nice_cfg, dm);
+    if (a7) sw_body<true, true>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg, dm);
+    else sw_body<false, true>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg, dm);
   } else {  // levels 8, 9: positions from HBM
-    if (a7) sw_body<true, false>(win, R, mw, &next, n, mem, out, chain, nice_cfg, dm);
-    else sw_body<false, false>(win, R, mw, &next, n, mem, out, chain, nice_cfg, dm);
+    if (a7) sw_body<true, false>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg, dm);
+    else sw_body<false, false>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg, dm);
   }
 }

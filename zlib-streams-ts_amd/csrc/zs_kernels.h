@@ -36,13 +36,27 @@ __global__ void zs_k_prev(const uint8_t* in, const uint64_t* in_off, const uint3
                           uint16_t* prevd, uint32_t min_len);
 __global__ void zs_k_match(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const uint16_t* prevd, uint2* mres, int chain, int nice, uint32_t min_len);
-// levels 4..9, streams of at most 65,537 bytes (deflate_sweep.hip)
+// levels 4..9 (deflate_sweep.hip), one workgroup per WINDOW: the inserted
+// positions from `base` up to its own positions' end ohi (at most 65,535; a
+// stream of up to 65,537 bytes is one window, base 0); the window writes the
+// results of its own positions [olo, ohi) (window-relative), members at
+// members + mb (u16, window-relative)
+struct zs_sweep_seg {
+  uint32_t s, base, olo, ohi;
+  uint64_t mb;
+  uint64_t pad;
+};
+#define ZS_SEG_WPOS 65535u   // inserted positions per window at most (u16 members; bucket counts fit 16 bits)
+#define ZS_SEG_FIRST 65520u  // own positions of a long stream's first window ...
+#define ZS_SEG_OWN 32752u    // ... and of its later ones, after a 32,768-position look-back (> MAX_DIST);
+                             // multiples of 16: every window starts 16-byte aligned with its stream
 template <bool ORD>
 __global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                            uint16_t* members, uint2* mres);
+                            const zs_sweep_seg* segs, uint16_t* members, uint2* mres);
 // demand = 1: steps 1 .. chain >> 2 only; an entry the parse may need further is ZS_MORE | member (zs_k_parse_dw)
 __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                           const uint16_t* members, uint2* mres, int chain, int nice, int demand);
+                           const zs_sweep_seg* segs, const uint16_t* members, uint2* mres, int chain, int nice,
+                           int demand);
 // the lazy parse (deflate_parse.hip): pass A stages 32 match-table entries per lane in LDS
 #define ZS_PARSE_DECL(name)                                                                                        \
   __global__ void name(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base, \
