@@ -4,7 +4,8 @@ with its 16 extra bits (inflate/constants.ts:12,28: base 3, up to 65,538
 bytes) and the 32,769 / 49,153 distance codes 30/31 (constants.ts:34).
 
 A symbol list is [("lit", byte) | ("copy", length, distance) | ...]; expand()
-is the plain LZ77 meaning of the list (the expected output), build() the bits."""
+is the plain LZ77 meaning of the list (the expected output), build() the bits.
+blocks() strings stored blocks (RFC 1951 3.2.4) and fixed ones into one member."""
 
 
 class _Bits:
@@ -68,10 +69,8 @@ def _dist_code(d):
     raise ValueError(d)
 
 
-def build(symbols, d64=True):
-    """One final fixed-Huffman block holding the symbols."""
-    b = _Bits()
-    b.put(1, 1)  # BFINAL
+def _fixed_block(b, symbols, final, d64):
+    b.put(1 if final else 0, 1)  # BFINAL
     b.put(1, 2)  # BTYPE = 01 (fixed)
     for s in symbols:
         if s[0] == "lit":
@@ -85,7 +84,49 @@ def build(symbols, d64=True):
             b.code(j, 5)
             b.put(dv, dx)
     _fixed_lit(b, 256)
+
+
+def build(symbols, d64=True):
+    """One final fixed-Huffman block holding the symbols."""
+    b = _Bits()
+    _fixed_block(b, symbols, True, d64)
     return b.bytes()
+
+
+def blocks(parts, d64=False):
+    """A member of blocks in order, the last one final: ("stored", bytes) -- BTYPE 00, the bits to the byte
+    boundary, LEN, NLEN, the bytes (at most 65,535) -- ("fixed", symbols), or ("bits", block, nbits, expansion):
+    one block taken verbatim from an encoder's member (its first nbits, BFINAL rewritten).  Returns (member,
+    expansion)."""
+    b, out = _Bits(), bytearray()
+    for k, part in enumerate(parts):
+        final = k + 1 == len(parts)
+        if part[0] == "bits":
+            _, data, nbits, exp = part
+            b.put(1 if final else 0, 1)
+            for i in range(1, nbits):
+                b.put((data[i >> 3] >> (i & 7)) & 1, 1)
+            out += exp
+        elif part[0] == "stored":
+            data = part[1]
+            assert len(data) <= 65535
+            b.put(1 if final else 0, 1)
+            b.put(0, 2)
+            b.put(0, (8 - b.n) & 7)
+            b.put(len(data), 16)
+            b.put(len(data) ^ 0xFFFF, 16)
+            for x in data:
+                b.put(x, 8)
+            out += data
+        else:
+            _fixed_block(b, part[1], final, d64)
+            for s in part[1]:
+                if s[0] == "lit":
+                    out.append(s[1])
+                else:
+                    for _ in range(s[1]):
+                        out.append(out[-s[2]])
+    return b.bytes(), bytes(out)
 
 
 def expand(symbols):
@@ -111,3 +152,29 @@ def long_copies():
     cases.append(seed + [("copy", 65537, 299), ("copy", 1000, 50000)])
     cases.append([("lit", c) for c in b"xy"] + [("copy", 65538, 2), ("copy", 65538, 65536), ("copy", 300, 7)])
     return [(build(s, True), expand(s)) for s in cases]
+
+
+def stored_mix(rng, n, src, level0=False):
+    """A member of about n output bytes: stored blocks (0 .. 65,535 bytes of src, sizes not multiples of 4) and,
+    unless level0, fixed blocks between them whose copies reach back up to 32 KiB -- into the stored bytes too.
+    Returns (member, expansion)."""
+    parts, made, at = [], 0, 0
+    while made < n:
+        if level0 or rng.random() < 0.5:
+            k = min(rng.choice([0, 1, 7, 999, 5003, 20001, 65535]), n - made + 1)
+            parts.append(("stored", src[at % len(src):at % len(src) + k]))
+            at += k
+            made += len(parts[-1][1])
+        else:
+            syms = []
+            for _ in range(rng.choice([10, 300, 4000])):
+                if made < 1 or rng.random() < 0.6:
+                    syms.append(("lit", src[at % len(src)]))
+                    at += 1
+                    made += 1
+                else:  # (short copies: under 8 output bytes per input byte, as the segmented decode takes)
+                    ln = rng.choice([3, 4, 9, 17, 40])
+                    syms.append(("copy", ln, rng.randint(1, min(made, 32768))))
+                    made += ln
+            parts.append(("fixed", syms))
+    return blocks(parts)

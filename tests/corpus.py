@@ -81,3 +81,17 @@ def make(spec):
 
 def sha256(b):
     return hashlib.sha256(b).hexdigest()
+
+
+def patchwork(seed, n):
+    """Test-only (not in corpus.mjs): n bytes of M-, R- and T-corpus stretches of 3,000 .. 40,000 bytes, so that
+    an encoder's blocks alternate between coded and stored (the R stretches)."""
+    import random
+
+    rng = random.Random(seed)
+    parts, k = [], 0
+    while k < n:
+        kind, m = rng.choice(["mixed", "rand", "text"]), rng.choice([3000, 20000, 40000])
+        parts.append(make({"kind": kind, "n": m, "seed": stream_seed(rng.randrange(4096))}))
+        k += m
+    return b"".join(parts)[:n]

@@ -175,3 +175,82 @@ def test_scratch_budget_sends_the_rest_to_the_other_paths(engine):
     engine.set_option("seg_scratch_mb", 16384)
     assert 0 < nseg < N // 4
     assert got == src
+
+
+def _dyn_stored_member(rng, n, src, empty_at=None):
+    """A member of about n output bytes: stored blocks (0 .. 20,001 bytes) between dynamic blocks taken verbatim
+    from L6 members of src stretches (the encoder's own blocks, so lanes meet as in its members); with empty_at, an
+    empty stored block whose LEN / NLEN straddle input byte empty_at (a sub-chunk end) and a coded block after it."""
+    import sys
+
+    import bitbuild
+
+    sys.path.insert(0, os.path.join(ROOT, "tools", "emu"))
+    import emu_seg
+
+    parts, pos, made = [], 0, 0  # pos: the member's bits so far
+
+    def stored(k):
+        nonlocal pos, made
+        parts.append(("stored", src[made % len(src):made % len(src) + k]))
+        pos = ((pos + 3 + 7) & ~7) + 32 + 8 * len(parts[-1][1])
+        made += len(parts[-1][1])
+
+    def coded():
+        nonlocal pos, made
+        while True:
+            a = rng.randrange(len(src) - 40000)
+            chunk = src[a:a + rng.choice([3000, 12000, 30000])]
+            c = oracle.compress(chunk, 6, "deflate-raw")[1]
+            _, blks, end = emu_seg.decode(c)
+            if len(blks) == 1 and c[0] & 6 == 4:  # one dynamic block
+                break
+        parts.append(("bits", c, end, chunk))
+        pos += end
+        made += len(chunk)
+
+    while made < n:
+        if empty_at is not None and 0 < empty_at - pos // 8 < 60000:
+            q = (pos + 3 + 7) >> 3  # the filler's LEN
+            stored(empty_at - 3 - q - 4)
+            stored(0)  # header byte at empty_at - 3, LEN / NLEN over the boundary
+            assert (pos >> 3) == empty_at + 2
+            coded()
+            empty_at = None
+        elif rng.random() < 0.5:
+            stored(rng.choice([0, 1, 7, 999, 5003, 20001]))
+        else:
+            coded()
+    m, exp = bitbuild.blocks(parts)
+    assert oracle.decompress(m, "deflate-raw", cap=len(exp), reference_bugs=False)[1] == exp
+    return m
+
+
+def test_stored_blocks_in_the_segmented_decode(engine):
+    """Stored blocks (BTYPE 0, inflate.ts:631-672) walked and copied by the segmented decode: 256 KiB members of
+    R-corpus bytes at L6 and of M/R/T patchworks at L1 / L6 / L9 (the encoder's stored blocks among coded ones; one
+    has a window-wrap copy behind them), level-0 members (the engine's, and hand-built ones of stored blocks of 0 ..
+    65,535 bytes, not multiples of 4: the oracle does not restate level 0) and hand-built mixes of stored blocks and
+    an encoder's dynamic blocks (one with an empty stored block whose LEN / NLEN straddle a sub-chunk end, a coded
+    block after it) -- every member finished by the segmented decode, its outcome equal to the oracle's."""
+    import bitbuild
+
+    src = corpus.text(11, 150000) + corpus.rand(12, 100000) + corpus.make({"kind": "mixed", "n": 100000, "seed": 13})
+    raw = [bitbuild.stored_mix(random.Random(i), 262144, src, level0=True)[0] for i in range(3)]
+    raw += [_dyn_stored_member(random.Random(20 + i), 262144, src, 65536 if i == 0 else None) for i in range(3)]
+    raw += [oracle.compress(corpus.rand(8, 262144), 6, "deflate-raw")[1]]
+    raw += [oracle.compress(corpus.patchwork(seed, 262144), lv, "deflate-raw")[1]
+            for seed, lv in [(208, 6), (201, 1), (204, 9), (205, 6)]]
+    # the engine's level 0 (zs_k_stored, pinned to the reference's level-0 goldens): 32,768-byte stored blocks
+    lvl0 = [corpus.patchwork(209, 262144), corpus.text(14, 200000)]
+    raw += engine.compress_batch(lvl0, "deflate-raw", 0)
+    gz = [oracle.compress(corpus.patchwork(seed, 262144), 6, "gzip")[1] for seed in (208, 202)]
+    gz += engine.compress_batch(lvl0, "gzip", 0)
+    for fmt, comps in (("deflate-raw", raw), ("gzip", gz)):
+        want = [oracle.decompress(c, fmt, cap=1 << 20, reference_bugs=True) for c in comps]
+        got = engine.decompress_batch_detailed(comps, fmt, [len(w[1]) + 16 for w in want])
+        assert engine.last_seg_count() == len(comps), fmt  # every member finished by the segmented decode
+        for i, (g, (st, out, cons, ph, msg)) in enumerate(zip(got, want)):
+            assert st == 1 or fmt == "gzip", i
+            assert (g[0], g[1], g[2], g[4]) == (st, ph, msg, cons), (fmt, i, g[:3], g[4], st, ph, msg, cons)
+            assert st != 1 or g[3] == out, (fmt, i)

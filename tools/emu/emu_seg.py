@@ -13,7 +13,10 @@ at its start.  This model checks the plan that gives it:
     (output count, events, last symbol length) alone;
   * a piece that does not start within 144 bits before a sub-chunk end may
     start with any `fast` value: the flag only matters in the near zones, and
-    in the output zone (> B + 65020) no copy can reach before the call start.
+    in the output zone (> B + 65020) no copy can reach before the call start;
+  * a stored block is one piece: the reference's COPY state (inflate.ts:645-660)
+    ends calls inside it at sub-chunk ends and buffer fills, which the plan
+    replays from its input offset and length alone (zs_refcalls_t::stored).
 
 It decodes members serially (symbols with their bit fields), replays the
 reference's bookkeeping (a transcription of zs_refcalls.h) over the whole
@@ -44,10 +47,12 @@ BLO = [16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15]
 
 class Bits:
     def __init__(self, data):
-        self.v = int.from_bytes(data, "little")
+        self.d = bytes(data) + bytes(8)
 
     def get(self, pos, k):
-        return (self.v >> pos) & ((1 << k) - 1)
+        b = pos >> 3
+        v = int.from_bytes(self.d[b:b + (((pos & 7) + k + 7) >> 3)], "little")
+        return (v >> (pos & 7)) & ((1 << k) - 1)
 
 
 def table(lens):
@@ -79,7 +84,8 @@ def dec(br, pos, t):
 
 def decode(data):
     """Serial decode of a raw deflate member: symbols as dicts (sb, o, len, dist,
-    l1, e1, l2, e2, eob, blk) and the block starts (bit of the block header)."""
+    l1, e1, l2, e2, eob, blk; a stored block is one symbol with its bytes in raw)
+    and the block starts (bit of the block header)."""
     br = Bits(data)
     pos, o, syms, blocks = 0, 0, [], []
     while True:
@@ -88,7 +94,18 @@ def decode(data):
         typ = br.get(pos + 1, 2)
         pos += 3
         if typ == 0:
-            raise NotImplementedError("stored blocks: the segmented path bails them")
+            pos = (pos + 7) & ~7
+            n = br.get(pos, 16)
+            assert n == br.get(pos + 16, 16) ^ 0xFFFF
+            pos += 32
+            raw = data[pos >> 3:(pos >> 3) + n]
+            syms.append(dict(sb=pos, o=o, len=n, dist=0, l1=0, e1=0, l2=0, e2=0, eob=False, blk=len(blocks) - 1,
+                             stored=True, raw=raw))
+            o += n
+            pos += 8 * n
+            if last:
+                return syms, blocks, pos
+            continue
         if typ == 1:
             lens = [8] * 144 + [9] * 112 + [7] * 24 + [8] * 8
             lt, dt = table(lens), table([5] * 30)
@@ -215,12 +232,30 @@ class Calls:
         op3 = op2 - self.wn
         return n - op3 if (op3 < n and self.wn >= n - op3) else 0
 
+    def stored(self, at, o, n):
+        if o > self.B + 65536:
+            self.end_call(self.B + 65536)
+        while n == 0 and self.cend < at:  # (the plan's form: an empty block takes its header's crossings)
+            self.end_call(o)
+            self.next_chunk()
+        while n:
+            while at >= self.cend:
+                self.end_call(o)
+                self.next_chunk()
+            if o >= self.B + 65536:
+                self.end_call(self.B + 65536)
+            take = min(n, self.cend - at, self.B + 65536 - o)
+            at, o, n = at + take, o + take, n - take
+
 
 def replay(syms, C, lo, hi):
     """wrap tails of symbols lo..hi-1 from state C"""
     tails = {}
     for i in range(lo, hi):
         s = syms[i]
+        if s.get("stored"):
+            C.stored(s["sb"] >> 3, s["o"], s["len"])
+            continue
         run = C.symbol(s["sb"], s["o"], s["len"], s["l1"], s["e1"], s["l2"], s["e2"], s["eob"])
         if run and s["dist"]:
             t = C.wrap(s["o"], s["len"], s["dist"])
@@ -233,6 +268,9 @@ def expand(syms, tails):
     out = bytearray()
     for i, s in enumerate(syms):
         if s["eob"]:
+            continue
+        if s.get("stored"):
+            out += s["raw"]
             continue
         if not s["dist"]:
             out.append(s["lit"])
@@ -248,12 +286,14 @@ def expand(syms, tails):
 def events(syms):
     """crossing event k: the first symbol whose end bit is past 262144 k (blocks
     are contiguous in bits except for their headers: a symbol starting past the
-    boundary after a header is the event too)"""
+    boundary after a header is the event too); a stored block takes the
+    boundaries before its end itself (Calls.stored), no events"""
     ev, k = [], 1
     for i, s in enumerate(syms):
-        end = s["sb"] + s["l1"] + s["e1"] + s["l2"] + s["e2"]
+        end = s["sb"] + (8 * s["len"] if s.get("stored") else s["l1"] + s["e1"] + s["l2"] + s["e2"])
         while end > 262144 * k:
-            ev.append((k, i))
+            if not s.get("stored"):
+                ev.append((k, i))
             k += 1
     return ev
 
@@ -263,7 +303,8 @@ def plan(syms, blocks, starts):
     first one 0), from the pieces' events, output offsets and last lengths;
     unclean starts (within 144 bits before a sub-chunk end) merge into the piece
     before.  Returns [(start index, state, fast)]."""
-    ev = events(syms)
+    # the events and the stored blocks, in symbol order
+    acts = sorted([(i, k) for k, i in events(syms)] + [(i, 0) for i, s in enumerate(syms) if s.get("stored")])
     blkstart = {b[1] for b in blocks}
     C = Calls()
     out = [(0, (0, 0, 0, 32768), 0)]
@@ -272,16 +313,20 @@ def plan(syms, blocks, starts):
         a = starts[j]
         s = syms[a]
         O = s["o"]
-        # events of symbols before the piece, each with the fills before it
-        while ei < len(ev) and ev[ei][1] < a:
-            o_e = syms[ev[ei][1]]["o"]
-            while o_e >= C.B + 65536:
-                C.end_call(C.B + 65536)
-            C.end_call(o_e)
-            C.next_chunk()
+        # events of symbols before the piece, each with the fills before it, and stored blocks
+        while ei < len(acts) and acts[ei][0] < a:
+            i = acts[ei][0]
+            if acts[ei][1] == 0:
+                C.stored(syms[i]["sb"] >> 3, syms[i]["o"], syms[i]["len"])
+            else:
+                o_e = syms[i]["o"]
+                while o_e >= C.B + 65536:
+                    C.end_call(C.B + 65536)
+                C.end_call(o_e)
+                C.next_chunk()
             ei += 1
         prev = syms[a - 1]
-        o_prev = prev["o"]  # = O - last_len (0 after an end of block)
+        o_prev = O if prev.get("stored") else prev["o"]  # = O - last_len (0 after an end of block or stored block)
         while o_prev >= C.B + 65536:
             C.end_call(C.B + 65536)
         if a not in blkstart and s["sb"] + 144 > 8 * C.cend:

@@ -42,7 +42,8 @@
 //                   values (bytes or markers) with the window-wrap copy replayed
 //  zs_k_seg_resolve one workgroup per member: pieces in order, markers looked up
 //                   in the bytes already final (a 64 KiB LDS ring), bytes written
-// Any doubt -- no chain of blocks, a stored block, a lane that never
+// A stored block is one piece, its bytes copied from the input by the decode.
+// Any doubt -- no chain of blocks, a lane that never
 // synchronises, an invalid code or "too far back" in a piece, a marker further
 // back than a u16 says -- marks the member bad; the host then runs the
 // wave kernel over it (and that the exact kernel), so outcomes stay the reference's.
@@ -156,14 +157,24 @@ static __device__ __forceinline__ zs_sg_sym zs_sg_decode(zs_sg_reader& R, const 
 }
 
 // The block header at the wave reader's position (inflate.ts:600-836) into
-// zlib's tables (inflate_table) in LDS, as zs_k_inflate_wave; false for a
-// stored block or anything invalid (the member then takes the other paths).
+// zlib's tables (inflate_table) in LDS, as zs_k_inflate_wave; a stored block's
+// length (inflate.ts:631-672: LEN and NLEN at the next byte boundary, the reader
+// left at its first byte) in slen, else ZS_SEG_NONE; false for anything invalid
+// (the member then takes the other paths).
 static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* lens, uint16_t* work, bool d64,
                                     uint32_t& last, uint32_t& lbits, uint32_t& dbits, uint32_t& dofs,
-                                    uint32_t& ntab) {
+                                    uint32_t& ntab, uint32_t& slen) {
   last = zs_wr_take(R, 1);
   const uint32_t type = zs_wr_take(R, 2);
   uint32_t lused = 0, dused = 0;
+  slen = ZS_SEG_NONE;
+  if (type == 0) {
+    zs_wr_align(R);
+    const uint32_t len = zs_wr_take(R, 16), nlen = zs_wr_take(R, 16);
+    if (len != (nlen ^ 0xffffu) || zs_wr_over(R)) return false;  // "invalid stored block lengths", or past the input
+    slen = len;
+    return true;
+  }
   if (type == 1) {  // fixed tables (inflate.ts:218-280)
     uint32_t sym;
     for (sym = 0; sym < 144; sym++) lens[sym] = 8;
@@ -210,7 +221,7 @@ static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* l
     dbits = 6;
     if (zs_inflate_table(DISTS, lens + nlen, ndist, codes + lused, &dbits, work, d64, &dused)) return false;
   } else {
-    return false;  // stored (the other paths copy it) or "invalid block type"
+    return false;  // "invalid block type"
   }
   lbits = zs_u(lbits);
   dbits = zs_u(dbits);
@@ -659,15 +670,55 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
       zs_wr_seek(R, hdr >> 3);
       zs_wr_take(R, hdr & 7u);
     }
-    uint32_t last = 0, lbits = 0, dbits = 0, dofs = 0, ntab = 0;
-    good = zs_sg_header(R, L.codes, L.h.lens, L.h.work, D64, last, lbits, dbits, dofs, ntab);
+    uint32_t last = 0, lbits = 0, dbits = 0, dofs = 0, ntab = 0, slen = ZS_SEG_NONE;
+    good = zs_sg_header(R, L.codes, L.h.lens, L.h.work, D64, last, lbits, dbits, dofs, ntab, slen);
     const uint32_t sym0 = (uint32_t)zs_wr_bitpos(R);
     if (good && sym0 > nbits) good = false;
+    if (good && slen != ZS_SEG_NONE && (uint64_t)sym0 + 8ull * slen > nbits) good = false;  // (the exact path reports it)
     if (!good) break;
     __syncthreads();
     uint32_t tab = ZS_SEG_NONE, cur = sym0;
     bool first = true;
-    for (;;) {
+    if (slen != ZS_SEG_NONE) {
+      // ---- a stored block: one span of one piece (lane 0), the bytes at sym0 / 8
+      uint32_t b = 0;
+      if (lane == 0) b = atomicAdd(&M.nalloc, 1u);
+      b = zs_u(__shfl(b, 0));
+      if (b >= cap) {
+        good = false;
+        break;
+      }
+      b += sb0;
+      cur = sym0 + 8u * slen;
+      zs_seg_lane& P = lanes[(size_t)b * ZS_SEG_LANES + lane];
+      P.act = 0;
+      P.start = lane == 0 ? sym0 : ZS_SEG_NONE;
+      if (lane == 0) {
+        spans[atomicAdd(nspan, 1u)] = b;
+        P.end = cur;
+        P.cnt = slen;
+        P.last_len = 0;
+        P.nev = 0;  // (crossings inside it: the plan replays the COPY state, zs_sg_calls::stored)
+        P.ev_k0 = 0;
+        zs_seg_blk& Bk = blk[b];
+        Bk.m = m;
+        Bk.e = e;
+        Bk.hdr = hdr;
+        Bk.sym0 = sym0;
+        Bk.end = cur;
+        Bk.lbits = Bk.dbits = Bk.dofs = 0;
+        Bk.tab = ZS_SEG_NONE;
+        Bk.nl = 1;
+        Bk.S = 0;
+        Bk.next = ZS_SEG_NONE;
+        Bk.flags = ZS_SEG_B_OK | ZS_SEG_B_FIRST | ZS_SEG_B_EOB | ZS_SEG_B_STORED | (last ? ZS_SEG_B_FINAL : 0u);
+        if (prevb == ZS_SEG_NONE) E.first = b;
+        else blk[prevb].next = b;
+      }
+      prevb = b;
+      pe0 = cur;
+    }
+    while (slen == ZS_SEG_NONE) {  // (a coded block's spans; left by break)
       // ---- a span
       uint32_t b = 0;
       if (lane == 0) b = atomicAdd(&M.nalloc, 1u);
@@ -722,7 +773,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
     }
     if (!good) break;
     // ---- the block ended at cur: the final one, or at a later entry's start
-    S = min(ZS_SEG_SMAX, max(W, (cur - hdr) / 60u));
+    if (slen == ZS_SEG_NONE) S = min(ZS_SEG_SMAX, max(W, (cur - hdr) / 60u));
     hdr = cur;
     if (last) {
       flags_e = 3u;
@@ -770,6 +821,26 @@ struct zs_sg_calls {
   }
   __device__ void fills(uint32_t o) {  // the buffer fills a symbol at output position o has triggered
     while (o >= B + 65536u) end_call(B + 65536u);
+  }
+  // zs_refcalls_t::stored (the COPY state); the calls ending before its end -- sub-chunk ends below in + len,
+  // the header's ones too: no piece has them as events (the next piece's start at in + len)
+  __device__ void stored(uint32_t in, uint32_t o, uint32_t len) {
+    if (o > B + 65536u) end_call(B + 65536u);
+    while (len == 0 && cend < in) {  // (an empty block: the sub-chunks its header read past)
+      end_call(o);
+      cend += 32768u;
+    }
+    while (len) {
+      while (in >= cend) {
+        end_call(o);
+        cend += 32768u;
+      }
+      if (o >= B + 65536u) end_call(B + 65536u);
+      const uint32_t take = min(len, min(cend - in, B + 65536u - o));
+      in += take;
+      o += take;
+      len -= take;
+    }
   }
 };
 
@@ -825,7 +896,27 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
         uint32_t O = s_O, k = s_k, prevg = s_prevg, plen = s_plen;
         bool first = s_first != 0, bad = false;
         const bool newblk = (Bk.flags & ZS_SEG_B_FIRST) != 0;
-        for (uint32_t l = 0; l < ZS_SEG_LANES && !bad; l++) {
+        if (Bk.flags & ZS_SEG_B_STORED) {  // one piece; the reference's COPY state ends calls inside it
+          zs_seg_lane& p = P[0];
+          if (refw) C.stored(p.start >> 3, O, p.cnt);
+          p.O = O;
+          p.off = ((O + 7u) & ~7u) + ZS_SEG_PAD * k;
+          p.dend = p.end;
+          p.dcnt = p.cnt;
+          p.B = C.B;
+          p.wn = C.wn;
+          p.wh = C.wh;
+          p.cend = C.cend;
+          p.act = 1u;
+          if (k >= pmax) bad = true;
+          else ptab[pb + k] = make_uint4(O, p.cnt, p.off, 0u);
+          k++;
+          prevg = b * ZS_SEG_LANES;
+          O += p.cnt;
+          plen = 0;
+          first = false;
+        }
+        for (uint32_t l = 0; l < ZS_SEG_LANES && !bad && !(Bk.flags & ZS_SEG_B_STORED); l++) {
           zs_seg_lane& p = P[l];
           if (p.start == ZS_SEG_NONE) continue;
           bool merge = false;
@@ -1085,6 +1176,18 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
   const zs_seg_blk& Bk = blk[b];
   const uint32_t m = zs_u(Bk.m);
   if (m == ZS_SEG_NONE || !(Bk.flags & ZS_SEG_B_OK) || mem[m].bad) continue;
+  if (Bk.flags & ZS_SEG_B_STORED) {  // the input's bytes as values, 8 per lane and round
+    const zs_seg_lane& p = lanes[(size_t)b * ZS_SEG_LANES];
+    const uint8_t* sp = in + in_off[list[m]] + (p.start >> 3);
+    uint4* dst = reinterpret_cast<uint4*>(scratch + sbase[m] + p.off);  // (16-byte aligned, padded)
+    for (uint32_t i = 8u * lane; i < p.cnt; i += 8u * ZS_SEG_LANES) {
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) v[j] = i + j < p.cnt ? sp[i + j] : 0u;
+      dst[i >> 3] = make_uint4(v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16);
+    }
+    continue;
+  }
   const uint32_t ntab = ZS_SEG_TAB, tab = zs_u(Bk.tab);
   __syncthreads();  // (the previous span's tables are no longer read)
   for (uint32_t i = lane; i < ntab; i += 64) codes[i] = tcache[(size_t)tab * ZS_SEG_TAB + i];

@@ -26,6 +26,7 @@
 #define ZS_SEG_B_FINAL 2u  // ends the member's final block
 #define ZS_SEG_B_FIRST 4u  // starts a block (its header at hdr)
 #define ZS_SEG_B_EOB 8u    // ends its block (else the entry's next span continues it)
+#define ZS_SEG_B_STORED 16u  // a stored block (BTYPE 0): one piece, lane 0, its bytes copied from the input
 
 // One span: a stretch of one block whose symbols a wave's lanes decode from
 // sym0 + j S (zs_k_seg_walk); its lanes' pieces in zs_seg_lane[span * 64 + j].
