@@ -51,3 +51,30 @@ def test_group_parse_matches_serial_deflate_fast(emu, level):
     out = r.stdout.decode()
     assert r.returncode == 0, out + r.stderr.decode()
     assert "MISMATCH" not in out, out
+
+
+REC_SRC = os.path.join(ROOT, "tools", "emu", "emu_fast_rec.c")
+
+
+@pytest.fixture(scope="module")
+def emu_rec(tmp_path_factory):
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    exe = str(tmp_path_factory.mktemp("emu") / "emu_fast_rec")
+    subprocess.run(["gcc", "-O2", "-o", exe, REC_SRC], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("level", sorted(LEVELS))
+def test_member_run_walks_match_serial_deflate_fast(emu_rec, level):
+    """zs_k_fast_mr's construction (option fast_mr, deflate_fast_mr.hip): chains read as runs of the superset in
+    which every position is inserted (the bucket sort's members, 32 entries per lane walk), filtered by a bitmap of
+    the truly inserted positions before the group and speculative inside it, the walks that run out of entries
+    left to the replay's slow step -- the symbols and block cuts of the serial deflate_fast with the reference's
+    head[] / prev[] tables and slide schedule."""
+    chain, lazy, nice = LEVELS[level]
+    blob = b"".join(struct.pack("<5I", chain, lazy, nice, len(s), 32) + s for s in _streams())
+    r = subprocess.run([emu_rec], input=blob, capture_output=True, timeout=600)
+    out = r.stdout.decode()
+    assert r.returncode == 0, out + r.stderr.decode()
+    assert "MISMATCH" not in out and out.count("ok n=") == len(_streams()), out

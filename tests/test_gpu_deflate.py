@@ -178,6 +178,42 @@ def test_group_fast_parser_equals_serial_replay(engine, level):
             assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1]
 
 
+@pytest.mark.parametrize("level", [1, 2, 3])
+def test_member_run_fast_parser_equals_serial_replay(engine, level):
+    """zs_k_fast_mr (option fast_mr: chains from the bucket sort's member runs filtered by an inserted-position
+    bitmap, no head[] / prev[]) against zs_k_fast_serial: same bytes on the group test's streams (slides, zeros,
+    random, group and window edges, a candidate at exactly MAX_DIST) and on 256 KiB T-corpus streams with their
+    reference goldens at L1 (C4-L1's first 64)."""
+    import zsamd
+
+    specs = [("text", 262144), ("mixed", 200000), ("rand", 40000), ("zeros", 100000), ("ramp", 70000),
+             ("text", 0), ("text", 1), ("text", 3), ("text", 4), ("text", 59), ("text", 64), ("text", 259),
+             ("text", 32769), ("text", 65535), ("text", 65536), ("text", 65537), ("zeros", 65537),
+             ("text", 98304 + 300), ("mixed", 131072 + 17), ("zeros", 262144)]
+    inputs = [corpus.make({"kind": k, "n": n, "seed": 9300 + i}) for i, (k, n) in enumerate(specs)]
+    b = bytearray(corpus.rand(78, 90000))  # a candidate at exactly MAX_DIST
+    b[40000:40020] = b[40000 - 32506:40000 - 32506 + 20]
+    inputs.append(bytes(b))
+    c4 = bytes(zsamd.corpus("text", 0, 64, 262144))
+    inputs += [c4[i * 262144:(i + 1) * 262144] for i in range(64)]
+    try:
+        engine.set_option("fast_group", 0)
+        ref = engine.compress_batch_raw(inputs, "deflate-raw", level)
+        engine.set_option("fast_group", 1)
+        engine.set_option("fast_mr", 1)
+        res = engine.compress_batch_raw(inputs, "deflate-raw", level)
+    finally:
+        engine.set_option("fast_group", 1)
+        engine.set_option("fast_mr", 0)
+    bad = [i for i in range(len(inputs)) if res[i] != ref[i]]
+    assert not bad, [(specs[i] if i < len(specs) else i, len(res[i][1]), len(ref[i][1])) for i in bad]
+    if level == 1:
+        recs = golden_io.batch("t256_l1_raw")
+        k0 = len(inputs) - 64
+        assert all(res[k0 + i][0] == 1 and (len(res[k0 + i][1]), hashlib.sha256(res[k0 + i][1]).digest()[:16]) == recs[i]
+                   for i in range(64))
+
+
 @pytest.mark.parametrize("level", [4, 6, 9])
 def test_two_wave_parse_equals_one_wave_parse(engine, level):
     """zs_k_parse_2w / _4w (two / four waves per stream, 512 / 256-position segments; two waves are the default

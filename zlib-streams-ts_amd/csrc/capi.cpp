@@ -102,6 +102,7 @@ struct zs_ctx {
   std::vector<uint64_t> hpos;
   bool demand = false;       // L4..7: the sweep takes chain >> 2 steps, zs_k_parse_dw walks the rest where the parse needs them (exact; slower)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
+  bool fast_mr = false;      // L1..3: zs_k_fast_mr (chains from the bucket sort's member runs, 37 KiB of LDS)
   // the chain builders (zs_k_bucket, zs_k_prev, zs_k_fast) let same-address LDS atomics of
   // one instruction apply in lane order (1) or rank equal hashes by ballots (0); 0 when the
   // self-test finds the order violated on this device
@@ -334,6 +335,7 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "fast_group")) c->fast_group = value != 0;
+  else if (!strcmp(name, "fast_mr")) c->fast_mr = value != 0;
   else if (!strcmp(name, "lane_order")) {
     if (value && !c->lane_order_ok)
       return fail(ZS_STREAM_ERROR, "lane_order: this device does not apply LDS atomics in lane order");
@@ -411,7 +413,7 @@ uint64_t zs_deflate_bound(uint64_t n, int wbits) {  // deflate.ts:615-674, memLe
 
 // Device metadata block: in_off | in_len | out_off | out_cap | pos_base | blk_base
 struct MetaLayout {
-  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, segs, bytes;
+  size_t in_off, in_len, out_off, out_cap, pos_base, blk_base, segs, win0, bytes;
   explicit MetaLayout(uint32_t n, uint32_t nwin = 0) {
     size_t o = 0;
     auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~size_t(255); return r; };
@@ -421,7 +423,8 @@ struct MetaLayout {
     out_cap = take(4ull * n);
     pos_base = take(8ull * n);
     blk_base = take(4ull * n);
-    segs = take(sizeof(zs_sweep_seg) * nwin);  // the sweep's windows (levels 4..9)
+    segs = take(sizeof(zs_sweep_seg) * nwin);  // the sweep's windows (levels 4..9; 1..3 with fast_mr)
+    win0 = take(nwin ? 4ull * n : 0);          // each stream's first window
     bytes = o;
   }
 };
@@ -539,7 +542,7 @@ static int deflate_match(zs_ctx* c, hipStream_t st, const zs_level_cfg& cfg, uin
     const uint32_t w0 = c->hwin0[a], nw = c->hwin0[e] - w0;
     // a window: counting sort by hash + lock-step sweep (deflate_sweep.hip)
     (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<nw, 256, 0, st>>>(
-        d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
+        d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(), c->mres.as<uint2>(), 0);
     MARK("bucket");
     zs_k_sweep<<<nw, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(),
                                     c->mres.as<uint2>(), cfg.chain, cfg.nice, c->cur_pw == ZS_PARSEDW_WAVES ? 1 : 0);
@@ -565,7 +568,7 @@ static int deflate_tail(zs_ctx* c, hipStream_t st, int level, int wrap, const zs
                         uint32_t max_blk, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
                         uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap, const uint64_t* d_pos,
                         const uint32_t* d_blk, zs_stream* d_st, uint32_t* syms, uint32_t* pscr, int32_t* d_status,
-                        uint32_t* d_out_len) {
+                        uint32_t* d_out_len, const zs_sweep_seg* d_segs, const uint32_t* d_win0) {
   zs_block* d_bk = c->blocks.as<zs_block>();
   const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
   if (level >= 4) {
@@ -580,6 +583,18 @@ static int deflate_tail(zs_ctx* c, hipStream_t st, int level, int wrap, const zs
                                    pscr, cfg.good, cfg.lazy);
     }
     MARK("parse");
+  } else if (c->fast_group && c->fast_mr) {
+    // levels 1..3 from member runs: the bucket sort of the stream's windows (member index and rank per
+    // position), then the parse with 37 KiB of LDS (deflate_fast_mr.hip)
+    uint16_t* mem = c->prevd.as<uint16_t>() + 32;  // (32 members of padding below: a run's load starts at k - 32)
+    const uint32_t w0 = c->hwin0[0], nw = c->hwin0[n] - w0;
+    (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<nw, 256, 0, st>>>(
+        d_in, d_in_off, d_in_len, d_pos, d_segs + w0, mem, c->mres.as<uint2>(), 1);
+    MARK("bucket");
+    auto fast = cfg.nice <= 8 ? zs_k_fast_mr<2> : cfg.nice <= 16 ? zs_k_fast_mr<4> : zs_k_fast_mr<8>;
+    fast<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, syms, d_bk, d_st, cfg.chain, cfg.lazy, cfg.nice,
+                           mem, c->mres.as<uint2>(), d_segs, d_win0);
+    MARK("fast");
   } else {
     const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
     // levels 1..3: the group-speculative replay (default) or the step-by-step one (fast_group = 0)
@@ -611,7 +626,8 @@ static int deflate_tail(zs_ctx* c, hipStream_t st, int level, int wrap, const zs
 // sweep is done -- beside chunk j + 1's sweep, with which the parse, trees and
 // emit workgroups co-reside on a CU (LDS 141.6 + 19.5 KiB, VGPRs 4 x 80 + 184).
 static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
-                          const uint32_t* in_len, const zs_sweep_seg* d_segs, const uint8_t* d_in,
+                          const uint32_t* in_len, const zs_sweep_seg* d_segs, const uint32_t* d_win0,
+                          const uint8_t* d_in,
                           const uint64_t* d_in_off,
                           const uint32_t* d_in_len, uint8_t* d_out, const uint64_t* d_out_off,
                           const uint32_t* d_out_cap, const uint64_t* d_pos, const uint32_t* d_blk, zs_stream* d_st,
@@ -641,7 +657,7 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
   auto tail = [&](hipStream_t s2, uint32_t a, uint32_t e, uint32_t mblk) {
     return deflate_tail(c, s2, level, wrap, cfg, e - a, mblk, d_in, d_in_off + a, d_in_len + a, d_out,
                         d_out_off + a, d_out_cap + a, d_pos + a, d_blk + a, d_st + a, syms + a,
-                        pscr + (size_t)pwords * a, d_status + a, d_out_len + a);
+                        pscr + (size_t)pwords * a, d_status + a, d_out_len + a, d_segs, d_win0 + a);
   };
   if (K == 1) {
     uint32_t a, e, mlen, mblk;
@@ -715,7 +731,7 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
     return r;
   }
   // host-side layout: workspace bases (and the sweep's windows, levels 4..9)
-  const bool sweep = level >= 4 && c->match_sweep;
+  const bool sweep = (level >= 4 && c->match_sweep) || (level <= 3 && c->fast_group && c->fast_mr);
   uint64_t P = 0, members = 0;
   uint32_t B = 0, max_len = 0, max_blk = 0;
   c->hpos.resize(n);
@@ -736,7 +752,10 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
   uint64_t* pos_base = (uint64_t*)(hm + ml.pos_base);
   uint32_t* blk_base = (uint32_t*)(hm + ml.blk_base);
   memcpy(pos_base, c->hpos.data(), 8ull * n);
-  if (sweep) sweep_table(n, in_len, pos_base, P, (zs_sweep_seg*)(hm + ml.segs), c->hwin0, members);
+  if (sweep) {
+    sweep_table(n, in_len, pos_base, P, (zs_sweep_seg*)(hm + ml.segs), c->hwin0, members);
+    memcpy(hm + ml.win0, c->hwin0.data(), 4ull * n);
+  }
   for (uint32_t i = 0; i < n; i++) {
     blk_base[i] = B;
     const uint32_t nb = in_len[i] / ZS_SYM_END + 2;
@@ -745,7 +764,7 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
     max_blk = std::max(max_blk, nb);
   }
   HIPCHK(c->meta.ensure(ml.bytes));
-  HIPCHK(c->prevd.ensure(2 * std::max(members, P) + 64));
+  HIPCHK(c->prevd.ensure(2 * std::max(members, P) + 128));  // (+ the padding zs_k_fast_mr reads below its runs)
   HIPCHK(c->mres.ensure(8 * P + 64));
   HIPCHK(c->syms.ensure(4 * (P + n) + 64));
   c->cur_pw = level >= 4 ? parse_waves_for(c, n, level) : 1;
@@ -760,7 +779,8 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
   uint8_t* dm = c->meta.as<uint8_t>();
   (void)max_len;
   (void)max_blk;
-  const int r = deflate_launch(c, st, level, wrap, kLevels[level], n, in_len, (const zs_sweep_seg*)(dm + ml.segs), d_in,
+  const int r = deflate_launch(c, st, level, wrap, kLevels[level], n, in_len, (const zs_sweep_seg*)(dm + ml.segs),
+                               (const uint32_t*)(dm + ml.win0), d_in,
                                (const uint64_t*)(dm + ml.in_off), (const uint32_t*)(dm + ml.in_len), d_out,
                                (const uint64_t*)(dm + ml.out_off), (const uint32_t*)(dm + ml.out_cap),
                                (const uint64_t*)(dm + ml.pos_base), (const uint32_t*)(dm + ml.blk_base),

@@ -100,7 +100,8 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
                                                             const uint32_t* __restrict__ in_len,
                                                             const uint64_t* __restrict__ pos_base,
                                                             const zs_sweep_seg* __restrict__ segs,
-                                                            uint16_t* __restrict__ members, uint2* __restrict__ mres) {
+                                                            uint16_t* __restrict__ members, uint2* __restrict__ mres,
+                                                            int ranks) {
   __shared__ uint32_t cnt[16384];
   __shared__ uint32_t part[ZS_BK_THREADS];
   __shared__ uint32_t stg[ZS_BK_CHUNK / 4 + 2];
@@ -285,11 +286,39 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
     __syncthreads();
   }
   BK_MARK(2);
+  if (ranks) {
+    // levels 1..3 (zs_k_fast_mr): each own position's member index k and its rank in its bucket (the members
+    // before it there: its superset chain, deflate_fast_mr.hip) in mres[p].x = k | rank << 16.  After pass 2 the
+    // packed offsets hold each bucket's end, i.e. the next one's start.
+    // Thread t takes buckets [128 t, 128 t + 128): their members are one contiguous run, walked in order with
+    // the bucket boundaries from the offsets (no input reads), 8 members per load.
+    const uint32_t h0 = 128u * tid;
+    auto bend = [&](uint32_t h) -> uint32_t { return (cnt[h >> 1] >> (16u * (h & 1u))) & 0xffffu; };
+    uint32_t k = h0 ? bend(h0 - 1u) : 0u;
+    const uint32_t kend = bend(h0 + 127u);
+    uint32_t h = h0, st = k, e = bend(h0);
+    while (k < kend) {
+      const uint32_t ka = k & ~7u;  // an aligned group of 8 members (16-byte aligned: window arrays start 8-aligned)
+      const uint4 v = *reinterpret_cast<const uint4*>(mem + ka);
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) {
+        const uint32_t kk = ka + j;
+        if (kk < k || kk >= kend) continue;
+        while (kk >= e) {
+          st = e;
+          e = bend(++h);
+        }
+        const uint32_t p = ((&v.x)[j >> 1] >> (16u * (j & 1u))) & 0xffffu;
+        if (p >= G.olo && p < G.ohi) out[p] = make_uint2(kk | ((kk - st) << 16), 0u);
+      }
+      k = ka + 8u;
+    }
+  }
 }
 template __global__ void zs_k_bucket<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*,
-                                           const zs_sweep_seg*, uint16_t*, uint2*);
+                                           const zs_sweep_seg*, uint16_t*, uint2*, int);
 template __global__ void zs_k_bucket<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*,
-                                            const zs_sweep_seg*, uint16_t*, uint2*);
+                                            const zs_sweep_seg*, uint16_t*, uint2*, int);
 
 // --------------------------------------------------------------- zs_k_sweep
 static __device__ __forceinline__ uint32_t sw_word(const uint32_t* win, uint32_t off) {

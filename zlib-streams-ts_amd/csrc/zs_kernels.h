@@ -52,7 +52,7 @@ struct zs_sweep_seg {
                              // multiples of 16: every window starts 16-byte aligned with its stream
 template <bool ORD>
 __global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                            const zs_sweep_seg* segs, uint16_t* members, uint2* mres);
+                            const zs_sweep_seg* segs, uint16_t* members, uint2* mres, int ranks);
 // demand = 1: steps 1 .. chain >> 2 only; an entry the parse may need further is ZS_MORE | member (zs_k_parse_dw)
 __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                            const zs_sweep_seg* segs, const uint16_t* members, uint2* mres, int chain, int nice,
@@ -84,6 +84,12 @@ template <int NW, bool ORD>
 __global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,
                           int lazy, int nice);
+// levels 1..3 without head[] / prev[]: chains from zs_k_bucket's member runs (ranks = 1), deflate_fast_mr.hip
+template <int NW>
+__global__ void zs_k_fast_mr(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                             const uint64_t* pos_base, const uint32_t* blk_base, uint32_t* syms, zs_block* blocks,
+                             zs_stream* streams, int chain, int lazy, int nice, const uint16_t* members,
+                             const uint2* mres, const zs_sweep_seg* segs, const uint32_t* win0);
 __global__ void zs_k_fast_serial(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                  const uint64_t* pos_base, const uint32_t* blk_base, uint32_t* syms, zs_block* blocks,
                                  zs_stream* streams, int chain, int lazy, int nice);
