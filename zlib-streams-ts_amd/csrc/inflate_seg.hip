@@ -55,6 +55,21 @@
 #include "zs_refcalls.h"
 #include "zs_seg.h"
 
+#ifndef ZS_SEG_EXP
+#define ZS_SEG_EXP 0  // instrumentation (timing experiments only; 0 in the product): 1 per-span decode clocks,
+                      // 2 per-entry walk clocks (tools/dbg/seg_walk_clock.py)
+#endif
+#if ZS_SEG_EXP & 2
+#define ZS_SEG_WDBG_N 65536u
+// per entry: header cycles, span phase-1 cycles (lanes decoding alone), span sync + record cycles, blocks,
+// spans, phase-1 symbols of the busiest lane (summed over spans), all cycles, bad-code reseeks
+__device__ unsigned long long zs_seg_wdbg[ZS_SEG_WDBG_N][8];
+extern "C" int zs_seg_wdbg_fetch(void* out, unsigned long long bytes) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_seg_wdbg),
+                                  bytes < sizeof(zs_seg_wdbg) ? bytes : sizeof(zs_seg_wdbg));
+}
+#endif
+
 // ------------------------------------------------------------- lane reader
 // One lane's bit reader (the lane kernel's scheme: clamped aligned words, one
 // refill ahead, zero past the end), started at any bit; member bit positions
@@ -68,6 +83,9 @@ struct zs_sg_reader {
   uint32_t pf;
 };
 static __device__ __forceinline__ uint32_t zs_sg_load4(const zs_sg_reader& R, uint32_t at) {
+#if ZS_SEG_EXP & 4  // (timing: input words made up in registers instead of loaded -- garbage decodes)
+  return at * 2654435761u;
+#endif
   const uint32_t q = (at + R.sh) >> 2;
   const uint32_t lo = R.w4[min(q, R.last)], hi = R.w4[min(q + 1u, R.last)];
   const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, R.sh);
@@ -262,6 +280,9 @@ struct zs_sg_walk_lds {
       uint32_t tck[ZS_SEG_LANES][W / ZS_SEG_CKB];
     } s;
   };
+#if ZS_SEG_EXP & 2
+  unsigned long long dbg[4];  // phase-1 cycles, rest cycles, busiest lane's symbols, reseeks (this span)
+#endif
   uint32_t sync[ZS_SEG_LANES];  // lane j's start on the true stream: the first start it shares with lane j - 1
   uint32_t odone[ZS_SEG_LANES];  // words of own[j] complete (lane j has moved past them)
   uint32_t send;
@@ -293,6 +314,10 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
                                       uint32_t nl, uint32_t S, uint32_t lbits, uint32_t dbits, uint32_t dofs,
                                       zs_seg_lane* __restrict__ recs, uint32_t& send, bool& bad_out) {
   const uint32_t lane = threadIdx.x;
+#if ZS_SEG_EXP & 2
+  const unsigned long long dbg_t0 = __builtin_readcyclecounter();
+  uint32_t dbg_sym = 0, dbg_seek = 0;
+#endif
   const uint32_t nbits = 8u * n;
   const uint32_t nend = sym0 + nl * S;  // the nominal end
   const bool cont_ok = nend < nbits;    // (else the block must end in this span)
@@ -382,6 +407,10 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
     }
     const uint32_t sb = pos;
     const zs_sg_sym y = zs_sg_decode(G, lt, lmask, dt, dmask, emask);
+#if ZS_SEG_EXP & 2
+    dbg_sym++;
+    dbg_seek += y.kind == ZS_SG_BAD ? 1u : 0u;
+#endif
     if (y.kind == ZS_SG_BAD) {
       if (sb - q < W) {
 #pragma unroll
@@ -437,6 +466,17 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
   }
   put_word();
   __syncthreads();
+#if ZS_SEG_EXP & 2
+  const unsigned long long dbg_t1 = __builtin_readcyclecounter();
+  if (lane == 0) {
+    L.dbg[0] = dbg_t1 - dbg_t0;
+    L.dbg[2] = 0;
+    L.dbg[3] = 0;
+  }
+  __syncthreads();
+  atomicMax(&L.dbg[2], (unsigned long long)dbg_sym);
+  atomicAdd(&L.dbg[3], (unsigned long long)dbg_seek);
+#endif
   // ---- 2. each lane's true start: the first start in its window lane - 1 shares
   uint32_t sp = lane == 0 ? sym0 : ZS_SEG_NONE;
   if (on && lane) {
@@ -576,6 +616,10 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
   }
   bad_out = __syncthreads_or(bad);
   send = L.send;
+#if ZS_SEG_EXP & 2
+  if (lane == 0) L.dbg[1] = __builtin_readcyclecounter() - dbg_t1;
+  __syncthreads();
+#endif
   return kind;
 }
 
@@ -663,6 +707,10 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
   // block before (a zlib stream's blocks are alike): the block in one span of
   // about 60 lanes, S >= ZS_SEG_W (a lane's window ends before the next lane's start)
   uint32_t S = sbits;
+#if ZS_SEG_EXP & 2
+  unsigned long long wd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long wd_start = __builtin_readcyclecounter();
+#endif
   while (good) {
     // ---- a block: its header (wave-uniform) and tables
     if (prevb != ZS_SEG_NONE || hdr != (uint32_t)zs_wr_bitpos(R)) {  // (a span has reused the staging LDS)
@@ -671,7 +719,14 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
       zs_wr_take(R, hdr & 7u);
     }
     uint32_t last = 0, lbits = 0, dbits = 0, dofs = 0, ntab = 0, slen = ZS_SEG_NONE;
+#if ZS_SEG_EXP & 2
+    const unsigned long long wd_h = __builtin_readcyclecounter();
+#endif
     good = zs_sg_header(R, L.codes, L.h.lens, L.h.work, D64, last, lbits, dbits, dofs, ntab, slen);
+#if ZS_SEG_EXP & 2
+    wd[0] += __builtin_readcyclecounter() - wd_h;
+    wd[3]++;
+#endif
     const uint32_t sym0 = (uint32_t)zs_wr_bitpos(R);
     if (good && sym0 > nbits) good = false;
     if (good && slen != ZS_SEG_NONE && (uint64_t)sym0 + 8ull * slen > nbits) good = false;  // (the exact path reports it)
@@ -742,6 +797,13 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
       bool sbad = false;
       const uint32_t k = zs_sg_span<D64, W>(L, src, n, cur, pe0, nl, S, lbits, dbits, dofs,
                                          lanes + (size_t)b * ZS_SEG_LANES, send, sbad);
+#if ZS_SEG_EXP & 2
+      wd[1] += L.dbg[0];
+      wd[2] += L.dbg[1];
+      wd[4]++;
+      wd[5] += L.dbg[2];
+      wd[7] += L.dbg[3];
+#endif
       if (lane == 0) {
         zs_seg_blk& Bk = blk[b];
         Bk.m = m;
@@ -792,6 +854,11 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
     E.end = hdr;
     E.flags = good ? flags_e : 0u;
   }
+#if ZS_SEG_EXP & 2
+  wd[6] = __builtin_readcyclecounter() - wd_start;
+  if (lane == 0 && blockIdx.x < ZS_SEG_WDBG_N)
+    for (int i = 0; i < 8; i++) zs_seg_wdbg[blockIdx.x][i] = wd[i];
+#endif
 }
 
 // ------------------------------------------------------------------- plan
@@ -1145,9 +1212,6 @@ static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint
   return true;  // (x0 >= 0 here: one of the two paths above)
 }
 
-#ifndef ZS_SEG_EXP
-#define ZS_SEG_EXP 0  // instrumentation (timing experiments only; 0 in the product): 1 per-span decode clocks
-#endif
 #if ZS_SEG_EXP & 1
 #define ZS_SEG_DBG_N 65536u
 __device__ unsigned long long zs_seg_dbg[ZS_SEG_DBG_N][4];  // per span slot: start, end (max), symbols (max lane), far reads (max lane)
