@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--mode", default="deflate", choices=["deflate", "inflate"],
                     help="deflate: the headline (configs[1]); inflate: decode of pre-built members (configs[2], C5)")
     ap.add_argument("--replicas", type=int, default=16, help="inflate: members = streams x replicas (C3: 4096 x 16)")
+    ap.add_argument("--no-fixtures", action="store_true", help="deflate64-raw: without the reference's fixtures (A/B only)")
+    ap.add_argument("--fixtures", default="", help="deflate64-raw: only the fixtures whose names contain one of these "
+                    "comma-separated strings (A/B only)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="engine option (zs_set_option), e.g. lane_block=16; repeatable")
     return ap.parse_args()
@@ -504,12 +507,15 @@ def main():
     D.close()
 
 
-def d64_fixtures():
+def d64_fixtures(only=""):
     """The reference's test/data deflate64 fixtures (tests/golden/d64) with their
-    decoded sizes / digests from inflate_small.json."""
+    decoded sizes / digests from inflate_small.json (only: comma-separated name parts to keep)."""
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "inflate_small.json")))
+    keep = [k for k in only.split(",") if k]
     out = []
     for c in g["cases"]:
+        if keep and not any(k in c["name"] for k in keep):
+            continue
         if c["name"].startswith("d64_") and c.get("ok"):
             out.append((open(os.path.join(ROOT, "tests", "golden", "d64", c["name"][4:]), "rb").read(),
                         c["out_len"], c["out_sha256"]))
@@ -542,7 +548,7 @@ def main_inflate(args):
     N_glob = S * R
     # the global member list: the corpus members, with (C5-ii) the reference's deflate64 fixtures
     # interleaved at fixed places -- sharded as one list, so each fixture is decoded by exactly one rank
-    fx = d64_fixtures() if dec_fmt == "deflate64-raw" else []
+    fx = d64_fixtures(args.fixtures) if dec_fmt == "deflate64-raw" and not args.no_fixtures else []
     gstep = max(1, N_glob // max(1, len(fx)))
     entries = []
     for i in range(N_glob):

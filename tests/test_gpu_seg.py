@@ -118,7 +118,47 @@ def test_deflate64_fixtures_in_a_small_batch(engine):
         nseg = engine.last_seg_count()
     for (d, n, h), r in zip(small, got):
         assert r[0] == 1 and len(r[3]) == n and hashlib.sha256(r[3]).hexdigest() == h and r[4] == len(d)
-    assert nseg >= 1
+    # all five finished there: payload_63k / repeat_63k end with a 1-bit end-of-block code, whose
+    # zeros past the input end the walk must not take for the block's end
+    assert nseg == len(small) == 5
+
+
+def _runs_member(seed, n):
+    """T-corpus stretches between runs of period 1 .. 7 (1 .. 3,000 values): long copies of distance 1 .. 7,
+    at every alignment to the pieces' 8-value units, and far repeats of 64 .. 258 bytes.  (Stretches of
+    random bytes are not used: their near-uniform 8-bit literal codes keep a lane started at the wrong bit
+    offset from synchronising, and such members leave the segmented decode for the wave kernel.)"""
+    rng = random.Random(seed)
+    text = corpus.make({"kind": "text", "n": 1 << 16, "seed": corpus.stream_seed(seed)})
+    out = bytearray()
+    while len(out) < n:
+        at = rng.randrange(0, len(text) - 1200)
+        out += text[at:at + rng.randrange(200, 1200)]
+        p = rng.randrange(1, 8)
+        pat = bytes(rng.randrange(256) for _ in range(p))
+        k = rng.choice([rng.randrange(1, 64), rng.randrange(64, 400), rng.randrange(400, 3000)])
+        out += (pat * (k // p + 1))[:k]
+        if len(out) > 31000 and rng.random() < 0.5:  # a far repeat: long copies from before most pieces
+            at = len(out) - rng.randrange(300, 30000)
+            out += out[at:at + rng.randrange(64, 259)]
+    return bytes(out[:n])
+
+
+def test_long_runs_and_far_markers_in_the_segmented_decode(engine):
+    """Copies of 64 values and more leave a piece as whole 16-byte units (zs_sg_out::run): distance-1/2/4
+    runs, runs of the other periods, and markers for history far before a piece start -- the bytes equal the oracle's,
+    every member finished by the segmented decode."""
+    ms = []
+    for i in range(12):
+        s = _runs_member(500 + i, 150000 + 7919 * i)
+        ms.append((s, oracle.compress(s, [1, 6, 9][i % 3], "deflate-raw")[1]))
+    with _opts(engine, seg_bits=1024):
+        got = engine.decompress_batch_raw([c for _, c in ms], "deflate-raw", [len(s) for s, _ in ms])
+        nseg = engine.last_seg_count()
+    # (the oracle with the reference's window-wrap copy decides the bytes)
+    want = [oracle.decompress(c, "deflate-raw", cap=len(s), reference_bugs=True)[1] for s, c in ms]
+    assert nseg == len(ms)
+    assert [g[3] for g in got] == want
 
 
 def test_damaged_members_take_the_other_paths(engine):

@@ -26,22 +26,34 @@ def main():
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "inflate_small.json")))
     fx = [(c["name"], open(os.path.join(ROOT, "tests", "golden", "d64", c["name"][4:]), "rb").read(), c["out_len"])
           for c in g["cases"] if c["name"].startswith("d64_") and c.get("ok")]
+    keep = sys.argv[1:]
     for name, d, n in fx:
+        if keep and not any(k in name for k in keep):
+            continue
         r = eng.decompress_batch_raw([d], "deflate64-raw", [n])[0]
         ok = eng.last_seg_count()
-        cnt = struct.unpack("<2I", fetch(eng, 16, 8))
+        cb = fetch(eng, 16, 8)
+        if len(cb) < 8:
+            print("%-28s in %7d out %8d st %d (not in the segmented decode)" % (name, len(d), n, r[0]), flush=True)
+            continue
+        cnt = struct.unpack("<2I", cb)
         line = "%-28s in %7d out %8d seg %d st %d blocks %d" % (name, len(d), n, ok, r[0], cnt[0])
         print(line, flush=True)
         if ok:
             continue
         M = struct.unpack_from("<5I", fetch(eng, 19, 32))
         print("   mem", M)
-        B = fetch(eng, 17, 48 * cnt[0])
-        for b in range(cnt[0]):
-            v = struct.unpack_from("<12I", B, 48 * b)
+        B = fetch(eng, 17, 64 * 64)
+        nb = len(B) // 64
+        for b in range(nb):
+            if struct.unpack_from("<I", B, 64 * b)[0] == 0xffffffff:
+                continue
+            v = struct.unpack_from("<16I", B, 64 * b)
             print("   blk", b, "m r hdr sym0 end flags lb db dofs nl S", v[:11])
-        Lr = fetch(eng, 18, 76 * 64 * cnt[0])
-        for b in range(cnt[0]):
+        Lr = fetch(eng, 18, 76 * 64 * nb)
+        for b in range(len(Lr) // (76 * 64)):
+            if struct.unpack_from("<I", B, 64 * b)[0] == 0xffffffff:
+                continue
             for l in range(64):
                 v = struct.unpack_from("<19I", Lr, 76 * (64 * b + l))
                 if v[0] != 0xffffffff:
