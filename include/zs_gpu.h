@@ -257,6 +257,8 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * input byte) take the split / wave decoders instead; "seg_bits" (1024..8192,
  * default 2048): input bits per lane of an entry's first block; "seg_wide"
  * (default 1): the 2048-bit sync window for a batch of few large members;
+ * "seg_big_bits" (>= 65536, default 2^21): members with more input bits also
+ * walk from the block starts a finder kernel proposes (more walks per member);
  * "seg_scratch_mb" (default 16384): the segmented decode's u16 scratch per
  * batch (2 bytes per byte of capacity); members past it take the other paths.
  * These options never change output bytes.  "inflate_ref_wrap" (default 1)

@@ -125,6 +125,7 @@ struct zs_ctx {
   uint32_t seg_small_batch = 16384; // batches of at most this many members ...
   uint32_t seg_small_min = 4096;    // ... send members with more input bytes than this to it too
   bool seg_wide = true;             // the 2048-bit sync window for a batch of few large members
+  uint32_t seg_big_bits = ZS_SEG_BIG_BITS;  // members with more input bits also walk from the finder's block starts
   uint64_t seg_scratch_max = 16ull << 30;  // bytes of u16 piece scratch the segmented decode may take per batch
   uint32_t ncu = 256;               // compute units of the device
   Buf glist, gfound, gbig, gbigs, gspb, gspl, gflist, gent, gblk, glanes, gtab, gmem, gpbase, gplist, gsbase, gscr, gcnt;
@@ -344,6 +345,10 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "inflate_split")) c->inflate_split = value != 0;
   else if (!strcmp(name, "inflate_seg")) c->inflate_seg = value != 0;
   else if (!strcmp(name, "seg_wide")) c->seg_wide = value != 0;
+  else if (!strcmp(name, "seg_big_bits")) {
+    if (value < 65536) return fail(ZS_STREAM_ERROR, "seg_big_bits must be >= 65536");
+    c->seg_big_bits = (uint32_t)value;
+  }
   else if (!strcmp(name, "seg_scratch_mb")) {
     if (value < 0) return fail(ZS_STREAM_ERROR, "seg_scratch_mb must be >= 0");
     c->seg_scratch_max = (uint64_t)value << 20;
@@ -1273,7 +1278,7 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   const bool refw = c->inflate_ref_wrap && !d64;
   // per member: span slots (one per ZS_SEG_BLOCK_BITS input bits for the blocks, twice the
   // spans of the narrowest lanes, 8 more), the pieces' bound and their u16
-  // scratch (each piece 16-byte aligned and padded); members over ZS_SEG_BIG_BITS
+  // scratch (each piece 16-byte aligned and padded); members over seg_big_bits
   // input bits also walk from the finder's block starts
   c->hgpbase.assign(ng + 1, 0);
   c->hgsbase.assign(ng + 1, 0);
@@ -1286,7 +1291,7 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
     c->hgspb[k + 1] = c->hgspb[k] + (uint32_t)spans;
     c->hgpbase[k + 1] = c->hgpbase[k] + seg_pmax(in_len[i]);
     c->hgsbase[k + 1] = c->hgsbase[k] + seg_scratch_elems(in_len[i], out_cap[i]);
-    if (nbits > ZS_SEG_BIG_BITS) c->hgbig.push_back(k);
+    if (nbits > c->seg_big_bits) c->hgbig.push_back(k);
   }
   const uint32_t nb = c->hgspb[ng], nbig = (uint32_t)c->hgbig.size();
   HIPCHK(c->glist.ensure(4ull * ng));
