@@ -255,7 +255,8 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * across 64 lanes, the reference's calls tracked per piece); large deflate64
  * members and high-expansion members (cap > 64 KiB, >= 8 output bytes per
  * input byte) take the split / wave decoders instead; "seg_bits" (1024..8192,
- * default 2048): input bits per lane of an entry's first block; "seg_wide"
+ * default 0 = 4096 for members of >= 64 KiB of input on average, else 2048):
+ * input bits per lane of an entry's first block; "seg_wide"
  * (default 1): the 2048-bit sync window for a batch of few large members;
  * "seg_big_bits" (>= 65536, default 2^21): members with more input bits also
  * walk from the block starts a finder kernel proposes (more walks per member);

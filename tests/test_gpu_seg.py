@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 class _opts:
-    DEFAULTS = {"inflate_seg": 1, "seg_bits": 2048, "seg_small_batch": 16384, "seg_small_min": 4096,
+    DEFAULTS = {"inflate_seg": 1, "seg_bits": 0, "seg_small_batch": 16384, "seg_small_min": 4096,
                 "inflate_fast": 1, "inflate_ref_wrap": 1, "inflate_wave_min": 32768, "seg_scratch_mb": 16384}
 
     def __init__(self, engine, **kw):

@@ -121,7 +121,8 @@ struct zs_ctx {
   std::vector<uint32_t> hslist;
   // segmented decode (inflate_seg.hip): a member's blocks cut into lane-sized pieces that synchronise
   bool inflate_seg = true;
-  uint32_t seg_bits = 2048;         // input bits per lane of an entry's first block (later ones: from the block before)
+  uint32_t seg_bits = 0;            // input bits per lane of an entry's first block (later ones: from the block before);
+                                    // 0: 4096 for members of 64 KiB of input or more on average, else 2048
   uint32_t seg_small_batch = 16384; // batches of at most this many members ...
   uint32_t seg_small_min = 4096;    // ... send members with more input bytes than this to it too
   bool seg_wide = true;             // the 2048-bit sync window for a batch of few large members
@@ -354,7 +355,8 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
     c->seg_scratch_max = (uint64_t)value << 20;
   }
   else if (!strcmp(name, "seg_bits")) {
-    if (value < (int)ZS_SEG_W || value > (int)ZS_SEG_SMAX) return fail(ZS_STREAM_ERROR, "seg_bits must be 1024 .. 8192");
+    if (value != 0 && (value < (int)ZS_SEG_W || value > (int)ZS_SEG_SMAX))
+      return fail(ZS_STREAM_ERROR, "seg_bits must be 0 (auto) or 1024 .. 8192");
     c->seg_bits = (uint32_t)value;
   } else if (!strcmp(name, "seg_small_batch")) {
     if (value < 0) return fail(ZS_STREAM_ERROR, "seg_small_batch must be >= 0");
@@ -1356,8 +1358,12 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   const bool w2k = c->seg_wide && nwalk <= 3u * c->ncu && gbits >= 65536ull * 8 * ng;
   auto walk = d64 ? (w2k ? zs_k_seg_walk<true, 2048u> : zs_k_seg_walk<true, 1024u>)
                   : (w2k ? zs_k_seg_walk<false, 2048u> : zs_k_seg_walk<false, 1024u>);
+  // bits per lane: large members (4,096 x 256 KiB: 17.2 -> 15.9 ms, its 512-member shard 3.70 -> 3.57) walk fewer,
+  // wider spans; 64 KiB members keep 2048 (the 1,024-member gunzip shard: 2.11 vs 2.45 ms, the decode's pieces
+  // too few to fill the chip) -- tools/segbits_ab.sh
+  const uint32_t sbits = c->seg_bits ? c->seg_bits : gbits >= (1ull << 19) * ng ? 4096u : 2048u;
   walk<<<nwalk, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, ng, c->gbig.as<uint32_t>(), nbig, wbits, gf, gspb, gb, gln, gt,
-                             ge, gm, cnt + 2, c->gspl.as<uint32_t>(), std::max<uint32_t>(c->seg_bits, w2k ? 2048u : 0u));
+                             ge, gm, cnt + 2, c->gspl.as<uint32_t>(), std::max<uint32_t>(sbits, w2k ? 2048u : 0u));
   if (int r = mark(c, sd, "seg_walk")) return r;
   zs_k_seg_plan<<<ng, 64, 0, sd>>>(d_in, d_ioff, d_ilen, d_ocap, gl, ng, wbits, refw ? 1 : 0, gb, gln, ge, gm,
                                    c->gpbase.as<uint32_t>(), c->gplist.as<uint4>());
