@@ -434,6 +434,53 @@ def test_device_inflate_rejects_unaligned_capacities(engine):
 
 
 @pytest.mark.gpu
+def test_host_inflate_takes_exact_unaligned_capacities(engine):
+    """zs_inflate_batch (the C host entry, called directly through ctypes, no Python rounding) takes any capacity
+    and any output offset: a 17-byte member fits a capacity of 17 at offset 0, an 18-byte member with a capacity of
+    17 is Z_BUF_ERROR "output capacity exceeded" (the exact cap, not one rounded up to a word), and a member at the
+    unaligned offset 34 decodes in place (capi.cpp inflate_device's caller_regions)."""
+    L = engine._L
+    a, b = b"hello hello hello", b"hello hello hello!"
+    comps = [oracle.compress(x, 6, "deflate-raw")[1] for x in (a, b, a)]
+    blob = b"".join(comps)
+    n = len(comps)
+    in_off = (ctypes.c_uint64 * n)(0, len(comps[0]), len(comps[0]) + len(comps[1]))
+    in_len = (ctypes.c_uint32 * n)(*map(len, comps))
+    out_off = (ctypes.c_uint64 * n)(0, 17, 34)
+    out_cap = (ctypes.c_uint32 * n)(17, 17, 17)
+    out = ctypes.create_string_buffer(51)
+    st, ph, msg = [(ctypes.c_int32 * n)() for _ in range(3)]
+    olen, cons = [(ctypes.c_uint32 * n)() for _ in range(2)]
+    r = L.zs_inflate_batch(engine._ctx, -15, n, blob, in_off, in_len, out, out_off, out_cap, st, ph, msg, olen, cons)
+    assert r == 0
+    assert list(st) == [1, -5, 1]
+    assert L.zs_inflate_message(msg[1]).decode() == "output capacity exceeded"
+    assert out.raw[0:17] == a and out.raw[34:51] == a and list(olen)[0::2] == [17, 17]
+    # the same through the Python mirror: exact caps, not rounded
+    res = engine.decompress_batch_raw([comps[0], comps[1]], "deflate-raw", out_caps=[17, 17])
+    assert [x[0] for x in res] == [1, -5] and res[0][3] == a
+    # zs_deflate_batch likewise: a capacity of exactly the output's length (unaligned) fits, one byte less is
+    # Z_BUF_ERROR, and the streams land at unaligned offsets
+    src = [b"abcabcabcabcabcabcabc xyz", b"the quick brown fox jumps"]
+    want = [oracle.compress(x, 6, "deflate-raw")[1] for x in src]
+    ln = [len(w) for w in want]
+    for caps, ok in (([ln[0], ln[1]], [1, 1]), ([ln[0] - 1, ln[1]], [-5, 1])):
+        n = 2
+        blob2 = b"".join(src)
+        out2 = ctypes.create_string_buffer(sum(caps) + 1)
+        st2 = (ctypes.c_int32 * n)()
+        ol2 = (ctypes.c_uint32 * n)()
+        r = L.zs_deflate_batch(engine._ctx, 6, -15, n, blob2, (ctypes.c_uint64 * n)(0, len(src[0])),
+                               (ctypes.c_uint32 * n)(*map(len, src)), out2, (ctypes.c_uint64 * n)(1, 1 + caps[0]),
+                               (ctypes.c_uint32 * n)(*caps), st2, ol2)
+        assert r == 0 and list(st2) == ok
+        for i in range(n):
+            if ok[i] == 1:
+                o = 1 + sum(caps[:i])
+                assert ol2[i] == ln[i] and out2.raw[o:o + ln[i]] == want[i]
+
+
+@pytest.mark.gpu
 def test_host_batch_packs_produced_bytes_over_several_chunks(engine):
     """The host-buffer decode of a batch of >= 32 MB input runs as four chunks and packs each chunk's outputs by the
     bytes produced, not by capacity: a last chunk that expands far past 4x the batch input grows the pack buffers

@@ -68,7 +68,9 @@ def test_segmented_decode_equals_the_reference(engine, fmt):
             assert g[3] == out and cons == len(c), i
             if fmt != "deflate-raw":
                 assert (g[5] & 0xffffffff) == (oracle.crc32(out) if fmt == "gzip" else oracle.adler32(out)), i
-    assert ok >= 1
+    # the seeded corpus pinned: the members the reference itself decodes cleanly (the rest end in its
+    # "incorrect data check" through the window-wrap defect), so a generator change cannot hide a regression
+    assert ok == {"deflate-raw": 24, "deflate": 22, "gzip": 19}[fmt]
 
 
 @pytest.mark.parametrize("bits", [1024, 8192])

@@ -462,7 +462,6 @@ static int deflate_stored_batch(zs_ctx* c, int wrap, uint32_t n, const uint8_t* 
   memcpy(hm + ml.out_cap, out_cap, 4ull * n);
   uint64_t max_total = 0;
   for (uint32_t i = 0; i < n; i++) {
-    if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
     const uint64_t t = (wrap == 0 ? 0 : wrap == 1 ? 6 : 18) + 5ull * (in_len[i] / ZS_STORED_CHUNK + 1) + in_len[i];
     max_total = std::max(max_total, t);
   }
@@ -713,10 +712,29 @@ extern "C" int zs_deflate_batch_device(zs_ctx* c, int level, int wbits, uint32_t
                                     d_out_len, nullptr, hip_stream);
 }
 
+// The device compress.  out_cap[i] is the stream's capacity as the caller set
+// it (Z_BUF_ERROR past it, exactly); the kernels store whole dwords, so the
+// stream's region must reach out_off[i] + out_cap[i] rounded up to 4.
+// `caller_regions` (the public device entries): the regions are the caller's
+// buffers, so capacities must be multiples of 4; the host entries stage in
+// regions of the capacities rounded up and pass the exact capacities.
+static int deflate_device(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                          const uint32_t* in_len, uint8_t* d_out, const uint64_t* out_off, const uint32_t* out_cap,
+                          int32_t* d_status, uint32_t* d_out_len, uint32_t* d_check, void* hip_stream,
+                          bool caller_regions);
+
 extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* d_in,
                                           const uint64_t* in_off, const uint32_t* in_len, uint8_t* d_out,
                                           const uint64_t* out_off, const uint32_t* out_cap, int32_t* d_status,
                                           uint32_t* d_out_len, uint32_t* d_check, void* hip_stream) {
+  return deflate_device(c, level, wbits, n, d_in, in_off, in_len, d_out, out_off, out_cap, d_status, d_out_len,
+                        d_check, hip_stream, true);
+}
+
+static int deflate_device(zs_ctx* c, int level, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                          const uint32_t* in_len, uint8_t* d_out, const uint64_t* out_off, const uint32_t* out_cap,
+                          int32_t* d_status, uint32_t* d_out_len, uint32_t* d_check, void* hip_stream,
+                          bool caller_regions) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   if (level == -1) level = 6;  // Z_DEFAULT_COMPRESSION, deflate.ts:268-270
   int wrap;
@@ -728,6 +746,9 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
+  for (uint32_t i = 0; i < n; i++)
+    if ((out_off[i] & 3) || (caller_regions && (out_cap[i] & 3)))
+      return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
   if (level == 0) {
     const int r = deflate_stored_batch(c, wrap, n, d_in, in_off, in_len, d_out, out_off, out_cap, d_status,
                                        d_out_len, st);
@@ -743,7 +764,6 @@ extern "C" int zs_deflate_batch_device_ex(zs_ctx* c, int level, int wbits, uint3
   uint32_t B = 0, max_len = 0, max_blk = 0;
   c->hpos.resize(n);
   for (uint32_t i = 0; i < n; i++) {
-    if ((out_off[i] & 3) || (out_cap[i] & 3)) return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
     c->hpos[i] = P;
     P += ((uint64_t)in_len[i] + 7) & ~7ull;  // per-position tables start 8-aligned (16-B link loads in zs_k_match)
   }
@@ -1002,15 +1022,17 @@ extern "C" int zs_deflate_batch_ex(zs_ctx* c, int level, int wbits, uint32_t n, 
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
+  // device regions: the caller's capacity rounded up to whole words (the kernels store dwords);
+  // the caller's exact capacities are the Z_BUF_ERROR limits
   std::vector<uint32_t> ocap(n);
-  for (uint32_t i = 0; i < n; i++) ocap[i] = out_cap[i] & ~3u;
+  for (uint32_t i = 0; i < n; i++) ocap[i] = (uint32_t)std::min<uint64_t>(0xfffffffcull, ((uint64_t)out_cap[i] + 3) & ~3ull);
   uint32_t* res[3] = {(uint32_t*)status, out_len, check};
   return host_batch(c, n, in, in_off, in_len, ocap, 3, res, 1, out, out_off,
-                    [&](uint32_t a, uint32_t b, const uint64_t* doff, const uint64_t* ooff, const uint32_t* cap,
+                    [&](uint32_t a, uint32_t b, const uint64_t* doff, const uint64_t* ooff, const uint32_t*,
                         uint32_t** dr) {
-                      return zs_deflate_batch_device_ex(c, level, wbits, b - a, c->d_in.as<uint8_t>(), doff, in_len + a,
-                                                        c->d_out.as<uint8_t>(), ooff, cap, (int32_t*)dr[0], dr[1],
-                                                        check ? dr[2] : nullptr, c->stream);
+                      return deflate_device(c, level, wbits, b - a, c->d_in.as<uint8_t>(), doff, in_len + a,
+                                            c->d_out.as<uint8_t>(), ooff, out_cap + a, (int32_t*)dr[0], dr[1],
+                                            check ? dr[2] : nullptr, c->stream, false);
                     });  // out_len is 0 for failed streams
 }
 
@@ -1413,11 +1435,32 @@ extern "C" int zs_inflate_batch_device(zs_ctx* c, int wbits, uint32_t n, const u
                                     d_msg, d_out_len, d_consumed, nullptr, hip_stream);
 }
 
+// The device decode.  out_cap[i] is the member's capacity as the caller set it
+// (Z_BUF_ERROR past it, exactly); the decoders store whole dwords, so the
+// member's region must reach out_off[i] + out_cap[i] rounded up to 4.
+// `caller_regions`: the regions are the caller's own buffers (the public
+// device entries), so capacities must be multiples of 4 -- no store may pass
+// the last member's end.  The host entries decode into their own staging,
+// whose regions are the capacities rounded up, and pass their callers' exact
+// capacities with caller_regions = false.
+static int inflate_device(zs_ctx* c, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                          const uint32_t* in_len, uint8_t* d_out, const uint64_t* out_off, const uint32_t* out_cap,
+                          int32_t* d_status, int32_t* d_phase, int32_t* d_msg, uint32_t* d_out_len,
+                          uint32_t* d_consumed, uint32_t* d_check, void* hip_stream, bool caller_regions);
+
 extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, const uint8_t* d_in,
                                           const uint64_t* in_off, const uint32_t* in_len, uint8_t* d_out,
                                           const uint64_t* out_off, const uint32_t* out_cap, int32_t* d_status,
                                           int32_t* d_phase, int32_t* d_msg, uint32_t* d_out_len,
                                           uint32_t* d_consumed, uint32_t* d_check, void* hip_stream) {
+  return inflate_device(c, wbits, n, d_in, in_off, in_len, d_out, out_off, out_cap, d_status, d_phase, d_msg,
+                        d_out_len, d_consumed, d_check, hip_stream, true);
+}
+
+static int inflate_device(zs_ctx* c, int wbits, uint32_t n, const uint8_t* d_in, const uint64_t* in_off,
+                          const uint32_t* in_len, uint8_t* d_out, const uint64_t* out_off, const uint32_t* out_cap,
+                          int32_t* d_status, int32_t* d_phase, int32_t* d_msg, uint32_t* d_out_len,
+                          uint32_t* d_consumed, uint32_t* d_check, void* hip_stream, bool caller_regions) {
   if (!c) return fail(ZS_STREAM_ERROR, "null context");
   // inflateInit2_ / inflateReset2 validation (inflate.ts:138-192) for the stream-layer formats
   if (!(wbits == -15 || wbits == 15 || wbits == 31 || wbits == -16))
@@ -1426,11 +1469,10 @@ extern "C" int zs_inflate_batch_device_ex(zs_ctx* c, int wbits, uint32_t n, cons
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return ZS_OK;
   if (!c->keep_counts) c->seg_used = false;
-  // the decoders store whole dwords (up to 3 bytes past a member's end): offsets and
-  // capacities are multiples of 4 so that no store leaves the member's region (the
-  // host entries round the caller's capacities up inside their own staging)
+  // the decoders store whole dwords (up to 3 bytes past a member's end): offsets are
+  // multiples of 4, and so are the capacities of regions the caller owns
   for (uint32_t i = 0; i < n; i++)
-    if ((out_off[i] & 3) || (out_cap[i] & 3))
+    if ((out_off[i] & 3) || (caller_regions && (out_cap[i] & 3)))
       return fail(ZS_STREAM_ERROR, "output offsets/capacities must be multiples of 4");
   MetaLayout ml(n);
   c->hmeta.resize(ml.bytes);
@@ -1706,9 +1748,10 @@ extern "C" int zs_inflate_batch_ex(zs_ctx* c, int wbits, uint32_t n, const uint8
   return host_batch(c, n, in, in_off, in_len, ocap, 6, res, 3, out, out_off,
                     [&](uint32_t a, uint32_t b, const uint64_t* doff, const uint64_t* ooff, const uint32_t*,
                         uint32_t** dr) {
-                      return zs_inflate_batch_device_ex(c, wbits, b - a, c->d_in.as<uint8_t>(), doff, in_len + a,
-                                                        c->d_out.as<uint8_t>(), ooff, creq.data() + a,
-                                                        (int32_t*)dr[0], (int32_t*)dr[1], (int32_t*)dr[2], dr[3], dr[4],
-                                                        check ? dr[5] : nullptr, c->stream);
+                      // regions of ocap (rounded up) bytes; the caller's exact capacities as the limits
+                      return inflate_device(c, wbits, b - a, c->d_in.as<uint8_t>(), doff, in_len + a,
+                                            c->d_out.as<uint8_t>(), ooff, creq.data() + a, (int32_t*)dr[0],
+                                            (int32_t*)dr[1], (int32_t*)dr[2], dr[3], dr[4], check ? dr[5] : nullptr,
+                                            c->stream, false);
                     });
 }

@@ -434,7 +434,7 @@ static napi_value DecompressBatch(napi_env env, napi_callback_info info) {
       c = arg_cap(env, e, 1 << 16);
     }
     j->out_off[i] = tout;
-    j->cap[i] = (uint32_t)(((uint64_t)c + 3u) & 0xfffffffcull);
+    j->cap[i] = c;  /* exact: Z_BUF_ERROR past it (the host entry stages in word-aligned regions itself) */
     tout += j->cap[i];
   }
   j->out = j->unbounded ? NULL : (uint8_t *)malloc(tout ? tout : 1);  /* unbounded: the library allocates it */
