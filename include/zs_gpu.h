@@ -220,11 +220,7 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * "match_sweep" (default 1): levels 4..9 find matches by a counting sort by
  * hash + lock-step sweep, longer streams in windows of 65,535 positions with a
  * 32 KiB look-back (0: the chain-link + per-tile walk kernels, for every stream
- * -- a cross-check); "demand" (default 0): the sweep takes chain >> 2 steps and
- * the parse walks the rest where it asks for the full budget (measured slower);
- * "pipeline" (default 1 = off; K: the batch's streams in K chunks, each chunk's
- * parse .. emit on a side stream beside the next chunk's sweep -- measured
- * slower);
+ * -- a cross-check);
  * "lane_block" (default 0 = by batch size;
  * else 1..64, a power of two): members per workgroup of the inflate lane path;
  * "inflate_wave_min" (default 32768; 0 = never): members with more input bytes
@@ -242,9 +238,6 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * two rounds' speculative passes at once);
  * "fast_group" (default 1): levels 1..3 replay deflate_fast a group of 64
  * positions at a time from speculative per-lane chain walks (0: step by step);
- * "fast_mr" (default 0): those walks read the bucket sort's member runs
- * filtered by a bitmap instead of head[] / prev[] (37 instead of 160 KiB of
- * LDS per stream; measured slower);
  * "lane_order" (default 1 when the self-test passes, else 0 and 1 is refused):
  * the chain builders rank equal hashes by same-address LDS atomics applying in
  * lane order (1) or by ballots (0);

@@ -67,7 +67,8 @@ def emu_rec(tmp_path_factory):
 
 @pytest.mark.parametrize("level", sorted(LEVELS))
 def test_member_run_walks_match_serial_deflate_fast(emu_rec, level):
-    """zs_k_fast_mr's construction (option fast_mr, deflate_fast_mr.hip): chains read as runs of the superset in
+    """zs_k_fast_mr's construction (a variant, not in the product: tools/variants/deflate_fast_mr.hip, measured
+    slower): chains read as runs of the superset in
     which every position is inserted (the bucket sort's members, 32 entries per lane walk), filtered by a bitmap of
     the truly inserted positions before the group and speculative inside it, the walks that run out of entries
     left to the replay's slow step -- the symbols and block cuts of the serial deflate_fast with the reference's

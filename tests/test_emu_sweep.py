@@ -105,7 +105,8 @@ def emu_demand(tmp_path_factory):
 
 @pytest.mark.parametrize("level", sorted(LEVELS_DW))
 def test_demand_walk_model_matches_serial_parse(emu_demand, tmp_path, level):
-    """The demand mode (option demand: zs_k_sweep takes chain >> 2 steps, zs_k_parse_dw walks steps chain >> 2 + 1
+    """The demand-mode variant (tools/variants/r05_paths.patch, not in the product: zs_k_sweep takes chain >> 2
+    steps, zs_k_parse_dw walks steps chain >> 2 + 1
     .. chain where the parse asks for the full budget): its walk rule (stop at limit or where member positions stop
     falling) gives longest_match's full-budget result at every walked position, and the parse over it emits the
     serial deflate_slow's symbols."""

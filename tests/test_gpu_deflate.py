@@ -1,7 +1,6 @@
 """GPU parity: the HIP deflate engine against the reference's goldens and the oracle."""
 import hashlib
 import random
-import struct
 
 import pytest
 
@@ -84,35 +83,25 @@ def test_sweep_match_table_equals_chain_walk(engine, level):
     inputs.append(bytes(x & 0x7F for x in corpus.rand(91 + level, 65536)))
     inputs.append(bytes(0x41 + (x & 3) for x in corpus.rand(92 + level, 65536)))
     inputs.append(bytes(x & 0x7F for x in corpus.rand(93, 20000)) + corpus.text(94, 45537))
-    # streams over 65,537 bytes: the sweep in windows (a first one of 65,535 positions, then 32,767 own positions
-    # after a 32,768-position look-back each), at and around the window boundaries and up to 256 KiB
+    # streams over 65,537 bytes: the sweep in windows (a first one owning 65,520 positions, then 32,752 own positions
+    # after a 32,768-position look-back each, capi.cpp sweep_table), at and around the window boundaries and up to
+    # 256 KiB
     for n, kind in ((65538, "text"), (98302, "mixed"), (98303, "text"), (130836, "zeros"), (262144, "text"),
                     (200001, "mixed"), (70000, "rand")):
         inputs.append(corpus.make({"kind": kind, "n": n, "seed": rng.randrange(1 << 32)}))
-    # (match_sweep, demand): the full sweep, the chain walk, and the demand-mode sweep (chain >> 2 steps; the
-    # parse walks the rest where it asks for the full budget, zs_k_parse_dw)
+    # match_sweep: the sweep, and the chain walk (zs_k_prev + zs_k_match) as the cross-check
     tables, outs = [], []
     try:
-        for sweep, demand in ((1, 0), (0, 0), (1, 1)):
+        for sweep in (1, 0):
             engine.set_option("match_sweep", sweep)
-            engine.set_option("demand", demand)
             outs.append(engine.compress_batch_raw(inputs, "deflate-raw", level))
             tables.append([engine.debug_fetch(1, i, 8 * len(d)) for i, d in enumerate(inputs)])
     finally:
         engine.set_option("match_sweep", 1)
-        engine.set_option("demand", 0)
     for i, d in enumerate(inputs):
         assert tables[0][i] == tables[1][i], (i, len(d))
         want = oracle.compress(d, level, "deflate-raw")[1]
-        assert outs[0][i] == outs[1][i] == outs[2][i] and outs[0][i][1] == want, (i, len(d))
-        # demand mode: the chain >> 2 results are the full sweep's; a full-budget result is the full sweep's or
-        # left open (ZS_MORE | the position's member index) at levels 4..7
-        full = struct.unpack("<%dI" % (2 * len(d)), tables[0][i])
-        dem = struct.unpack("<%dI" % (2 * len(d)), tables[2][i])
-        assert full[1::2] == dem[1::2], (i, len(d))
-        opened = sum(1 for a, b in zip(full[0::2], dem[0::2]) if a != b)
-        assert all(a == b or (b >> 16) == 0xFFFF for a, b in zip(full[0::2], dem[0::2])), (i, len(d))
-        assert level <= 7 or opened == 0
+        assert outs[0][i] == outs[1][i] and outs[0][i][1] == want, (i, len(d))
 
 
 def test_output_capacity_too_small_reports_buf_error(engine):
@@ -176,42 +165,6 @@ def test_group_fast_parser_equals_serial_replay(engine, level):
     for d, (st, out) in zip(inputs, res):
         if len(d) <= 65536:
             assert st == 1 and out == oracle.compress(d, level, "deflate-raw")[1]
-
-
-@pytest.mark.parametrize("level", [1, 2, 3])
-def test_member_run_fast_parser_equals_serial_replay(engine, level):
-    """zs_k_fast_mr (option fast_mr: chains from the bucket sort's member runs filtered by an inserted-position
-    bitmap, no head[] / prev[]) against zs_k_fast_serial: same bytes on the group test's streams (slides, zeros,
-    random, group and window edges, a candidate at exactly MAX_DIST) and on 256 KiB T-corpus streams with their
-    reference goldens at L1 (C4-L1's first 64)."""
-    import zsamd
-
-    specs = [("text", 262144), ("mixed", 200000), ("rand", 40000), ("zeros", 100000), ("ramp", 70000),
-             ("text", 0), ("text", 1), ("text", 3), ("text", 4), ("text", 59), ("text", 64), ("text", 259),
-             ("text", 32769), ("text", 65535), ("text", 65536), ("text", 65537), ("zeros", 65537),
-             ("text", 98304 + 300), ("mixed", 131072 + 17), ("zeros", 262144)]
-    inputs = [corpus.make({"kind": k, "n": n, "seed": 9300 + i}) for i, (k, n) in enumerate(specs)]
-    b = bytearray(corpus.rand(78, 90000))  # a candidate at exactly MAX_DIST
-    b[40000:40020] = b[40000 - 32506:40000 - 32506 + 20]
-    inputs.append(bytes(b))
-    c4 = bytes(zsamd.corpus("text", 0, 64, 262144))
-    inputs += [c4[i * 262144:(i + 1) * 262144] for i in range(64)]
-    try:
-        engine.set_option("fast_group", 0)
-        ref = engine.compress_batch_raw(inputs, "deflate-raw", level)
-        engine.set_option("fast_group", 1)
-        engine.set_option("fast_mr", 1)
-        res = engine.compress_batch_raw(inputs, "deflate-raw", level)
-    finally:
-        engine.set_option("fast_group", 1)
-        engine.set_option("fast_mr", 0)
-    bad = [i for i in range(len(inputs)) if res[i] != ref[i]]
-    assert not bad, [(specs[i] if i < len(specs) else i, len(res[i][1]), len(ref[i][1])) for i in bad]
-    if level == 1:
-        recs = golden_io.batch("t256_l1_raw")
-        k0 = len(inputs) - 64
-        assert all(res[k0 + i][0] == 1 and (len(res[k0 + i][1]), hashlib.sha256(res[k0 + i][1]).digest()[:16]) == recs[i]
-                   for i in range(64))
 
 
 @pytest.mark.parametrize("level", [4, 6, 9])

@@ -22,7 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 class _opts:
     DEFAULTS = {"inflate_seg": 1, "seg_bits": 0, "seg_small_batch": 16384, "seg_small_min": 4096,
-                "inflate_fast": 1, "inflate_ref_wrap": 1, "inflate_wave_min": 32768, "seg_scratch_mb": 16384}
+                "inflate_fast": 1, "inflate_ref_wrap": 1, "inflate_wave_min": 32768, "seg_scratch_mb": 16384,
+                "seg_wide": 1, "seg_big_bits": 1 << 21, "timing": 0, "check_phases": 0}
 
     def __init__(self, engine, **kw):
         self.e, self.kw = engine, kw
@@ -71,6 +72,24 @@ def test_segmented_decode_equals_the_reference(engine, fmt):
     # the seeded corpus pinned: the members the reference itself decodes cleanly (the rest end in its
     # "incorrect data check" through the window-wrap defect), so a generator change cannot hide a regression
     assert ok == {"deflate-raw": 24, "deflate": 22, "gzip": 19}[fmt]
+
+
+@pytest.mark.parametrize("opt", [("seg_big_bits", 65536), ("seg_wide", 0), ("check_phases", 1), ("timing", 1)])
+def test_walk_options_do_not_change_bytes(engine, opt):
+    """seg_big_bits (members over it also walk from the block starts zs_k_split_find proposes), seg_wide (the
+    2,048-bit sync window), check_phases and timing only change how the decode runs: T- and M-corpus members of
+    100 .. 500 KB at L6 / L9, every one finished by the segmented decode, equal the oracle with the reference's
+    window-wrap copy, status and message included."""
+    rng = random.Random(sum(opt[0].encode()))
+    ms = _members(rng, "deflate-raw", ["text", "mixed"], [6, 9], [100000, 262144, 500000], 8)
+    comps = [c for _, c in ms]
+    caps = [len(s) + 16 for s, _ in ms]
+    with _opts(engine, **{opt[0]: opt[1]}):
+        got = engine.decompress_batch_detailed(comps, "deflate-raw", caps)
+        assert engine.last_seg_count() == len(ms)
+    for i, ((s, c), g) in enumerate(zip(ms, got)):
+        st, out, cons, ph, msg = oracle.decompress(c, "deflate-raw", cap=len(s) + 16, reference_bugs=True)
+        assert (g[0], g[1], g[2], g[4]) == (st, ph, msg, cons) and g[3] == out, (opt, i)
 
 
 @pytest.mark.parametrize("bits", [1024, 8192])

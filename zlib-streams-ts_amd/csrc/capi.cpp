@@ -96,13 +96,9 @@ struct zs_ctx {
   int lane_block = 0;        // members per workgroup of the inflate lane path (0: chosen from the batch size)
   int cur_pw = 1;            // waves per stream of the current deflate batch's parse (zs_k_parse / _2w / _4w)
   int parse_waves = 0;       // L4..9 one-wave parse: waves per stream (1, 2; 0: chosen from the batch size)
-  int pipeline = 1;          // L4..9 deflate batches: chunks pipelined over two streams (1: off; measured slower)
-  std::vector<hipEvent_t> dev;  // the pipeline's sweep-done events
   std::vector<uint32_t> hwin0;  // the sweep's windows: each stream's first (sweep_table)
   std::vector<uint64_t> hpos;
-  bool demand = false;       // L4..7: the sweep takes chain >> 2 steps, zs_k_parse_dw walks the rest where the parse needs them (exact; slower)
   bool fast_group = true;    // L1..3: zs_k_fast (group-speculative) instead of zs_k_fast_serial
-  bool fast_mr = false;      // L1..3: zs_k_fast_mr (chains from the bucket sort's member runs, 37 KiB of LDS)
   // the chain builders (zs_k_bucket, zs_k_prev, zs_k_fast) let same-address LDS atomics of
   // one instruction apply in lane order (1) or rank equal hashes by ballots (0); 0 when the
   // self-test finds the order violated on this device
@@ -306,7 +302,6 @@ void zs_ctx_destroy(zs_ctx* c) {
     if (b->p) (void)hipHostFree(b->p);
   if (c->d_offs.p) (void)hipFree(c->d_offs.p);
   for (hipEvent_t e : c->hev) (void)hipEventDestroy(e);
-  for (hipEvent_t e : c->dev) (void)hipEventDestroy(e);
   for (hipStream_t q : {c->h2d, c->d2h})
     if (q) {
       (void)hipStreamSynchronize(q);
@@ -337,7 +332,6 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "check_phases")) c->check_phases = value != 0;
   else if (!strcmp(name, "match_sweep")) c->match_sweep = value != 0;
   else if (!strcmp(name, "fast_group")) c->fast_group = value != 0;
-  else if (!strcmp(name, "fast_mr")) c->fast_mr = value != 0;
   else if (!strcmp(name, "lane_order")) {
     if (value && !c->lane_order_ok)
       return fail(ZS_STREAM_ERROR, "lane_order: this device does not apply LDS atomics in lane order");
@@ -364,11 +358,6 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   } else if (!strcmp(name, "seg_small_min")) {
     if (value < 0) return fail(ZS_STREAM_ERROR, "seg_small_min must be >= 0");
     c->seg_small_min = (uint32_t)value;
-  }
-  else if (!strcmp(name, "demand")) c->demand = value != 0;
-  else if (!strcmp(name, "pipeline")) {
-    if (value < 0 || value > 64) return fail(ZS_STREAM_ERROR, "pipeline must be in 0..64");
-    c->pipeline = value;
   }
   else if (!strcmp(name, "parse_waves")) {
     if (value < 0 || value > 4 || value == 3) return fail(ZS_STREAM_ERROR, "parse_waves must be 0, 1, 2 or 4");
@@ -430,7 +419,7 @@ struct MetaLayout {
     out_cap = take(4ull * n);
     pos_base = take(8ull * n);
     blk_base = take(4ull * n);
-    segs = take(sizeof(zs_sweep_seg) * nwin);  // the sweep's windows (levels 4..9; 1..3 with fast_mr)
+    segs = take(sizeof(zs_sweep_seg) * nwin);  // the sweep's windows (levels 4..9)
     win0 = take(nwin ? 4ull * n : 0);          // each stream's first window
     bytes = o;
   }
@@ -488,23 +477,16 @@ static int deflate_stored_batch(zs_ctx* c, int wrap, uint32_t n, const uint8_t* 
 // The L4..9 parse runs two waves per stream (zs_k_parse_2w: 512-position
 // segments, two rounds' speculative passes at once) for a batch of n streams?
 // The whole batch decides (chunks of one batch share the scratch layout).
-// Levels 4..7 with the sweep (option demand, default on): the sweep takes the
-// first chain >> 2 steps of every position and zs_k_parse_dw walks the rest
-// where the parse asks for the full budget (ZS_PARSEDW_WAVES waves per stream).
-// Levels 8, 9 sweep the whole chain (on text their chains end within chain >> 2).
 static int parse_waves_for(const zs_ctx* c, uint32_t n, int level) {
-  if (c->demand && c->match_sweep && level >= 4 && level <= 7) return ZS_PARSEDW_WAVES;
+  (void)level;
   if (c->parse_waves) return c->parse_waves;
   return n < ZS_PARSE2W_AUTO ? 2 : 1;
 }
 static uint32_t parse_seg(int w) {
-  return w == ZS_PARSEDW_WAVES ? ZS_PARSEDW_SEG : w == 4 ? ZS_PARSE4W_SEG : w == 2 ? ZS_PARSE2W_SEG : ZS_PARSE_SEG;
+  return w == 4 ? ZS_PARSE4W_SEG : w == 2 ? ZS_PARSE2W_SEG : ZS_PARSE_SEG;
 }
 static uint32_t parse_seg_words(int w) {
-  return w == ZS_PARSEDW_WAVES ? ZS_PARSEDW_SEG_WORDS
-         : w == 4              ? ZS_PARSE4W_SEG_WORDS
-         : w == 2              ? ZS_PARSE2W_SEG_WORDS
-                               : ZS_PARSE_SEG_WORDS;
+  return w == 4 ? ZS_PARSE4W_SEG_WORDS : w == 2 ? ZS_PARSE2W_SEG_WORDS : ZS_PARSE_SEG_WORDS;
 }
 
 // The sweep's window table of a batch (into `out`, batch stream indices) and each
@@ -548,10 +530,10 @@ static int deflate_match(zs_ctx* c, hipStream_t st, const zs_level_cfg& cfg, uin
     const uint32_t w0 = c->hwin0[a], nw = c->hwin0[e] - w0;
     // a window: counting sort by hash + lock-step sweep (deflate_sweep.hip)
     (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<nw, 256, 0, st>>>(
-        d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(), c->mres.as<uint2>(), 0);
+        d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
     MARK("bucket");
     zs_k_sweep<<<nw, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(),
-                                    c->mres.as<uint2>(), cfg.chain, cfg.nice, c->cur_pw == ZS_PARSEDW_WAVES ? 1 : 0);
+                                    c->mres.as<uint2>(), cfg.chain, cfg.nice);
     MARK("sweep");
   } else {
     // cross-check (option match_sweep = 0): the chain-walk kernels for every stream
@@ -574,33 +556,15 @@ static int deflate_tail(zs_ctx* c, hipStream_t st, int level, int wrap, const zs
                         uint32_t max_blk, const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
                         uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap, const uint64_t* d_pos,
                         const uint32_t* d_blk, zs_stream* d_st, uint32_t* syms, uint32_t* pscr, int32_t* d_status,
-                        uint32_t* d_out_len, const zs_sweep_seg* d_segs, const uint32_t* d_win0) {
+                        uint32_t* d_out_len) {
   zs_block* d_bk = c->blocks.as<zs_block>();
   const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
   if (level >= 4) {
     const int pw = c->cur_pw;  // waves per stream of the lazy parse (deflate_parse.hip)
-    if (pw == ZS_PARSEDW_WAVES) {
-      zs_k_parse_dw<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), syms, d_bk,
-                                           d_st, pscr, cfg.good, cfg.lazy, c->prevd.as<uint16_t>(), cfg.chain,
-                                           cfg.nice);
-    } else {
-      auto parse = pw == 4 ? zs_k_parse_4w : pw == 2 ? zs_k_parse_2w : zs_k_parse;
-      parse<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), syms, d_bk, d_st,
-                                   pscr, cfg.good, cfg.lazy);
-    }
+    auto parse = pw == 4 ? zs_k_parse_4w : pw == 2 ? zs_k_parse_2w : zs_k_parse;
+    parse<<<n, 64 * pw, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, c->mres.as<uint2>(), syms, d_bk, d_st,
+                                 pscr, cfg.good, cfg.lazy);
     MARK("parse");
-  } else if (c->fast_group && c->fast_mr) {
-    // levels 1..3 from member runs: the bucket sort of the stream's windows (member index and rank per
-    // position), then the parse with 37 KiB of LDS (deflate_fast_mr.hip)
-    uint16_t* mem = c->prevd.as<uint16_t>() + 32;  // (32 members of padding below: a run's load starts at k - 32)
-    const uint32_t w0 = c->hwin0[0], nw = c->hwin0[n] - w0;
-    (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<nw, 256, 0, st>>>(
-        d_in, d_in_off, d_in_len, d_pos, d_segs + w0, mem, c->mres.as<uint2>(), 1);
-    MARK("bucket");
-    auto fast = cfg.nice <= 8 ? zs_k_fast_mr<2> : cfg.nice <= 16 ? zs_k_fast_mr<4> : zs_k_fast_mr<8>;
-    fast<<<n, 64, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_blk, syms, d_bk, d_st, cfg.chain, cfg.lazy, cfg.nice,
-                           mem, c->mres.as<uint2>(), d_segs, d_win0);
-    MARK("fast");
   } else {
     const int fast_smem = 2 * 32768 * 2 + 32768;  // head[] + prev[] (u16 x 32 K each) + the 32 KiB input ring
     // levels 1..3: the group-speculative replay (default) or the step-by-step one (fast_group = 0)
@@ -626,18 +590,16 @@ static int deflate_tail(zs_ctx* c, hipStream_t st, int level, int wrap, const zs
   return ZS_OK;
 }
 
-// The deflate launch sequence of a batch (levels 1..9) on stream st.  Levels
-// 4..9 with the sweep run as a pipeline of chunks of streams (option pipeline):
-// chunk j's bucket + sweep on st, its parse .. emit on the side stream once its
-// sweep is done -- beside chunk j + 1's sweep, with which the parse, trees and
-// emit workgroups co-reside on a CU (LDS 141.6 + 19.5 KiB, VGPRs 4 x 80 + 184).
+// The deflate launch sequence of a batch (levels 1..9) on stream st.  (A
+// pipeline of chunks of streams -- chunk j's parse .. emit on a side stream
+// beside chunk j + 1's sweep -- measured slower twice: DESIGN 5,
+// tools/variants/r05_paths.patch.)
 static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const zs_level_cfg& cfg, uint32_t n,
                           const uint32_t* in_len, const zs_sweep_seg* d_segs, const uint32_t* d_win0,
-                          const uint8_t* d_in,
-                          const uint64_t* d_in_off,
-                          const uint32_t* d_in_len, uint8_t* d_out, const uint64_t* d_out_off,
-                          const uint32_t* d_out_cap, const uint64_t* d_pos, const uint32_t* d_blk, zs_stream* d_st,
-                          uint32_t* syms, uint32_t* pscr, uint32_t* check, int32_t* d_status, uint32_t* d_out_len) {
+                          const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len, uint8_t* d_out,
+                          const uint64_t* d_out_off, const uint32_t* d_out_cap, const uint64_t* d_pos,
+                          const uint32_t* d_blk, zs_stream* d_st, uint32_t* syms, uint32_t* pscr, uint32_t* check,
+                          int32_t* d_status, uint32_t* d_out_len) {
   const int nthreads_s = 256, nblocks_s = (int)((n + 255) / 256);
   MARK("start");
   if (wrap) {
@@ -645,53 +607,17 @@ static int deflate_launch(zs_ctx* c, hipStream_t st, int level, int wrap, const 
     zs_k_copy_check<<<nblocks_s, nthreads_s, 0, st>>>(check, d_st, (int)n);
     MARK("checksum");
   }
-  uint32_t K = 1;
-  if (level >= 4 && c->match_sweep && c->cur_pw != ZS_PARSEDW_WAVES)
-    K = c->pipeline ? (uint32_t)c->pipeline : 1u;
-  K = std::max(1u, std::min(K, n));
-  const uint32_t pwords = parse_seg_words(c->cur_pw);
-  auto range = [&](uint32_t j, uint32_t& a, uint32_t& e, uint32_t& mlen, uint32_t& mblk) {
-    a = (uint32_t)((uint64_t)n * j / K);
-    e = (uint32_t)((uint64_t)n * (j + 1) / K);
-    mlen = 0;
-    mblk = 0;
-    for (uint32_t i = a; i < e; i++) {
-      mlen = std::max(mlen, in_len[i]);
-      mblk = std::max(mblk, in_len[i] / ZS_SYM_END + 2);
-    }
-  };
-  auto tail = [&](hipStream_t s2, uint32_t a, uint32_t e, uint32_t mblk) {
-    return deflate_tail(c, s2, level, wrap, cfg, e - a, mblk, d_in, d_in_off + a, d_in_len + a, d_out,
-                        d_out_off + a, d_out_cap + a, d_pos + a, d_blk + a, d_st + a, syms + a,
-                        pscr + (size_t)pwords * a, d_status + a, d_out_len + a, d_segs, d_win0 + a);
-  };
-  if (K == 1) {
-    uint32_t a, e, mlen, mblk;
-    range(0, a, e, mlen, mblk);
-    if (level >= 4) {
-      const int r = deflate_match(c, st, cfg, 0, n, mlen, d_in, d_in_off, d_in_len, d_pos, d_segs);
-      if (r != ZS_OK) return r;
-    }
-    return tail(st, 0, n, mblk);
+  uint32_t mlen = 0, mblk = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    mlen = std::max(mlen, in_len[i]);
+    mblk = std::max(mblk, in_len[i] / ZS_SYM_END + 2);
   }
-  while (c->dev.size() < K) {
-    hipEvent_t ev;
-    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    c->dev.push_back(ev);
-  }
-  for (uint32_t j = 0; j < K; j++) {
-    uint32_t a, e, mlen, mblk;
-    range(j, a, e, mlen, mblk);
-    int r = deflate_match(c, st, cfg, a, e, mlen, d_in, d_in_off, d_in_len, d_pos, d_segs);
+  if (level >= 4) {
+    const int r = deflate_match(c, st, cfg, 0, n, mlen, d_in, d_in_off, d_in_len, d_pos, d_segs);
     if (r != ZS_OK) return r;
-    HIPCHK(hipEventRecord(c->dev[j], st));
-    HIPCHK(hipStreamWaitEvent(c->side, c->dev[j], 0));
-    if ((r = mark(c, c->side, "sweep_wait")) != ZS_OK) return r;  // (the side stream's phases start here)
-    if ((r = tail(c->side, a, e, mblk)) != ZS_OK) return r;
   }
-  HIPCHK(hipEventRecord(c->join, c->side));
-  HIPCHK(hipStreamWaitEvent(st, c->join, 0));
-  return ZS_OK;
+  return deflate_tail(c, st, level, wrap, cfg, n, mblk, d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_cap, d_pos,
+                      d_blk, d_st, syms, pscr, d_status, d_out_len);
 }
 
 // Per-stream check value (the reference's strm.adler after the stream,
@@ -759,7 +685,7 @@ static int deflate_device(zs_ctx* c, int level, int wbits, uint32_t n, const uin
     return r;
   }
   // host-side layout: workspace bases (and the sweep's windows, levels 4..9)
-  const bool sweep = (level >= 4 && c->match_sweep) || (level <= 3 && c->fast_group && c->fast_mr);
+  const bool sweep = level >= 4 && c->match_sweep;
   uint64_t P = 0, members = 0;
   uint32_t B = 0, max_len = 0, max_blk = 0;
   c->hpos.resize(n);
@@ -791,7 +717,7 @@ static int deflate_device(zs_ctx* c, int level, int wbits, uint32_t n, const uin
     max_blk = std::max(max_blk, nb);
   }
   HIPCHK(c->meta.ensure(ml.bytes));
-  HIPCHK(c->prevd.ensure(2 * std::max(members, P) + 128));  // (+ the padding zs_k_fast_mr reads below its runs)
+  HIPCHK(c->prevd.ensure(2 * std::max(members, P) + 128));
   HIPCHK(c->mres.ensure(8 * P + 64));
   HIPCHK(c->syms.ensure(4 * (P + n) + 64));
   c->cur_pw = level >= 4 ? parse_waves_for(c, n, level) : 1;

@@ -100,8 +100,7 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
                                                             const uint32_t* __restrict__ in_len,
                                                             const uint64_t* __restrict__ pos_base,
                                                             const zs_sweep_seg* __restrict__ segs,
-                                                            uint16_t* __restrict__ members, uint2* __restrict__ mres,
-                                                            int ranks) {
+                                                            uint16_t* __restrict__ members, uint2* __restrict__ mres) {
   __shared__ uint32_t cnt[16384];
   __shared__ uint32_t part[ZS_BK_THREADS];
   __shared__ uint32_t stg[ZS_BK_CHUNK / 4 + 2];
@@ -286,39 +285,11 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
     __syncthreads();
   }
   BK_MARK(2);
-  if (ranks) {
-    // levels 1..3 (zs_k_fast_mr): each own position's member index k and its rank in its bucket (the members
-    // before it there: its superset chain, deflate_fast_mr.hip) in mres[p].x = k | rank << 16.  After pass 2 the
-    // packed offsets hold each bucket's end, i.e. the next one's start.
-    // Thread t takes buckets [128 t, 128 t + 128): their members are one contiguous run, walked in order with
-    // the bucket boundaries from the offsets (no input reads), 8 members per load.
-    const uint32_t h0 = 128u * tid;
-    auto bend = [&](uint32_t h) -> uint32_t { return (cnt[h >> 1] >> (16u * (h & 1u))) & 0xffffu; };
-    uint32_t k = h0 ? bend(h0 - 1u) : 0u;
-    const uint32_t kend = bend(h0 + 127u);
-    uint32_t h = h0, st = k, e = bend(h0);
-    while (k < kend) {
-      const uint32_t ka = k & ~7u;  // an aligned group of 8 members (16-byte aligned: window arrays start 8-aligned)
-      const uint4 v = *reinterpret_cast<const uint4*>(mem + ka);
-#pragma unroll
-      for (uint32_t j = 0; j < 8; j++) {
-        const uint32_t kk = ka + j;
-        if (kk < k || kk >= kend) continue;
-        while (kk >= e) {
-          st = e;
-          e = bend(++h);
-        }
-        const uint32_t p = ((&v.x)[j >> 1] >> (16u * (j & 1u))) & 0xffffu;
-        if (p >= G.olo && p < G.ohi) out[p] = make_uint2(kk | ((kk - st) << 16), 0u);
-      }
-      k = ka + 8u;
-    }
-  }
 }
 template __global__ void zs_k_bucket<true>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*,
-                                           const zs_sweep_seg*, uint16_t*, uint2*, int);
+                                           const zs_sweep_seg*, uint16_t*, uint2*);
 template __global__ void zs_k_bucket<false>(const uint8_t*, const uint64_t*, const uint32_t*, const uint64_t*,
-                                            const zs_sweep_seg*, uint16_t*, uint2*, int);
+                                            const zs_sweep_seg*, uint16_t*, uint2*);
 
 // --------------------------------------------------------------- zs_k_sweep
 static __device__ __forceinline__ uint32_t sw_word(const uint32_t* win, uint32_t off) {
@@ -469,19 +440,18 @@ extern "C" int zs_sw_stats(unsigned long long* out) {
 template <bool A7, bool MW>
 static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, uint16_t* mw, uint32_t* next,
                                                uint32_t n, uint32_t m, uint32_t olo, uint32_t ohi,
-                                               const uint16_t* mem, uint2* out, int chain, int nice_cfg,
-                                               bool demand) {
+                                               const uint16_t* mem, uint2* out, int chain, int nice_cfg) {
   // n: bytes from the window's start to the stream's end; m: the window's
   // members (inserted positions); results for the own positions [olo, ohi)
   using Sig = SwSig<A7>;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t budget = (uint32_t)chain, budget_s = (uint32_t)chain >> 2;
-  // the steps swept: the full chain, or (demand) the first chain >> 2 -- the rest
-  // only where the parse asks for the full budget (zs_k_parse_dw)
+  // the steps swept: the full chain (a demand-driven variant that swept chain >> 2
+  // steps and left the rest to the parse lost: DESIGN 4.2, tools/variants/r05_paths.patch)
 #if ZS_SW_EXP & 128
   const uint32_t sbud = 4u;  // (timing: the per-chunk cost without chain steps past 4)
 #else
-  const uint32_t sbud = demand ? budget_s : budget;
+  const uint32_t sbud = budget;
 #endif
   const uint32_t nchunks = (m + 63) / 64;
   auto put_rec = [&](int j, uint4 r) {
@@ -543,7 +513,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     // stream: its first 32,768 positions are look-back, candidates only)
     const bool own = mem_ok && p >= olo && p < ohi;
     if (__builtin_amdgcn_ballot_w64(own) == 0) continue;
-    mw0 = k0 - (int)sbud - (demand ? 1 : 0);  // (demand: member k - sbud - 1 for the probe below)
+    mw0 = k0 - (int)sbud;
     if (MW) mw[k - mw0] = (uint16_t)p;
     Sig S;
     S.own(win, p);
@@ -806,15 +776,6 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         }
         rx = (L << 16) | (L > 2u ? D : 0u) | (head & 0x8000u);
         ry = (Ls << 16) | (Ls > 2u ? Ds : 0u);
-        // demand: the full-budget result is settled unless the chain is still
-        // live at step chain >> 2 + 1 below nice; then rx = ZS_MORE | k for the
-        // parse's continuation walk (a live step 2 means the head is not at
-        // MAX_DIST: no slide-NIL flag is lost)
-        if (demand && !tail && L < nice && (int)sbud < k) {
-          // (the ring loads filled the member window from k0 - 64 up: LDS unless sbud = 64)
-          const uint32_t q = MW && sbud < 64u ? member(k - (int)sbud - 1) : (uint32_t)mem[k - (int)sbud - 1];
-          if (((sw_hash(sw_word(win, q)) << 16) | q) > klim) rx = ZS_MORE | (uint32_t)k;
-        }
       }
 #if ZS_SW_EXP & 512
       if (rx == 0x12345678u) out[p] = make_uint2(rx, ry);  // (timing: without the result stores)
@@ -830,7 +791,7 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
                                                    const uint64_t* __restrict__ pos_base,
                                                    const zs_sweep_seg* __restrict__ segs,
                                                    const uint16_t* __restrict__ members, uint2* __restrict__ mres,
-                                                   int chain, int nice_cfg, int demand) {
+                                                   int chain, int nice_cfg) {
   __shared__ __attribute__((aligned(16))) SwRing ring[16];
   __shared__ __attribute__((aligned(16))) uint32_t win[ZS_SW_WIN_WORDS];
   __shared__ uint16_t mwin[16][ZS_SW_MW];
@@ -875,14 +836,12 @@ __global__ __launch_bounds__(1024) void zs_k_sweep(const uint8_t* __restrict__ i
   const uint16_t* mem = members + G.mb;
   uint2* out = mres + pos_base[s] + G.base;
   uint16_t* const mw = mwin[threadIdx.x >> 6];
-  // (demand mode: the parse's walks read a whole stream's members and window -- streams of one window only)
-  const bool dm = demand != 0 && G.base == 0 && n <= 65537u;
   const uint32_t olo = G.olo, ohi = G.ohi;
-  if ((dm ? (chain >> 2) + 1 : chain) + 64 <= (int)ZS_SW_MW) {
-    if (a7) sw_body<true, true>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg, dm);
-    else sw_body<false, true>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg, dm);
+  if (chain + 64 <= (int)ZS_SW_MW) {
+    if (a7) sw_body<true, true>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg);
+    else sw_body<false, true>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg);
   } else {  // levels 8, 9: positions from HBM
-    if (a7) sw_body<true, false>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg, dm);
-    else sw_body<false, false>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg, dm);
+    if (a7) sw_body<true, false>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg);
+    else sw_body<false, false>(win, R, mw, &next, n, m, olo, ohi, mem, out, chain, nice_cfg);
   }
 }

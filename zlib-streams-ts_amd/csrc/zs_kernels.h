@@ -52,11 +52,9 @@ struct zs_sweep_seg {
                              // multiples of 16: every window starts 16-byte aligned with its stream
 template <bool ORD>
 __global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                            const zs_sweep_seg* segs, uint16_t* members, uint2* mres, int ranks);
-// demand = 1: steps 1 .. chain >> 2 only; an entry the parse may need further is ZS_MORE | member (zs_k_parse_dw)
+                            const zs_sweep_seg* segs, uint16_t* members, uint2* mres);
 __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
-                           const zs_sweep_seg* segs, const uint16_t* members, uint2* mres, int chain, int nice,
-                           int demand);
+                           const zs_sweep_seg* segs, const uint16_t* members, uint2* mres, int chain, int nice);
 // the lazy parse (deflate_parse.hip): pass A stages 32 match-table entries per lane in LDS
 #define ZS_PARSE_DECL(name)                                                                                        \
   __global__ void name(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base, \
@@ -65,11 +63,6 @@ __global__ void zs_k_sweep(const uint8_t* in, const uint64_t* in_off, const uint
 ZS_PARSE_DECL(zs_k_parse)
 ZS_PARSE_DECL(zs_k_parse_2w)  // two waves per stream, ZS_PARSE2W_SEG-position segments
 ZS_PARSE_DECL(zs_k_parse_4w)  // four waves per stream, ZS_PARSE4W_SEG-position segments
-// the parse over a demand-mode match table: continues the open entries' chain walks (16 waves per stream)
-__global__ void zs_k_parse_dw(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                              const uint64_t* pos_base, const uint32_t* blk_base, const uint2* mres, uint32_t* syms,
-                              zs_block* blocks, zs_stream* streams, uint32_t* scratch, int good, int lazy,
-                              const uint16_t* members, int chain, int nice);
 // parse scratch words per 1024-position segment (deflate_parse.hip)
 #define ZS_PARSE_SEG 1024u
 #define ZS_PARSE_SEG_WORDS 3596u
@@ -77,19 +70,10 @@ __global__ void zs_k_parse_dw(const uint8_t* in, const uint64_t* in_off, const u
 #define ZS_PARSE2W_SEG_WORDS 2060u
 #define ZS_PARSE4W_SEG 256u
 #define ZS_PARSE4W_SEG_WORDS 1292u
-#define ZS_PARSEDW_SEG 64u
-#define ZS_PARSEDW_SEG_WORDS 716u
-#define ZS_PARSEDW_WAVES 16
 template <int NW, bool ORD>
 __global__ void zs_k_fast(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                           const uint32_t* blk_base, uint32_t* syms, zs_block* blocks, zs_stream* streams, int chain,
                           int lazy, int nice);
-// levels 1..3 without head[] / prev[]: chains from zs_k_bucket's member runs (ranks = 1), deflate_fast_mr.hip
-template <int NW>
-__global__ void zs_k_fast_mr(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
-                             const uint64_t* pos_base, const uint32_t* blk_base, uint32_t* syms, zs_block* blocks,
-                             zs_stream* streams, int chain, int lazy, int nice, const uint16_t* members,
-                             const uint2* mres, const zs_sweep_seg* segs, const uint32_t* win0);
 __global__ void zs_k_fast_serial(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                  const uint64_t* pos_base, const uint32_t* blk_base, uint32_t* syms, zs_block* blocks,
                                  zs_stream* streams, int chain, int lazy, int nice);
