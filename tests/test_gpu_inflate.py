@@ -334,3 +334,19 @@ def zlib_fixed(data, fmt):
     wb = {"deflate-raw": -15, "deflate": 15, "gzip": 31}[fmt]
     co = zlib.compressobj(6, zlib.DEFLATED, wb, 8, zlib.Z_FIXED)
     return co.compress(data) + co.flush()
+
+
+def test_wave_table_builder_equals_inflate_table(engine):
+    """zs_inflate_table_wave (zs_inftab.h: the decoding tables of a dynamic header built by the 64 lanes of a wave
+    -- ballot-sorted symbols, each root entry the canonical decode of its own bits, sub-tables sized and placed as
+    inflate_table allocates them, inftrees.ts:62-279) against the serial inflate_table on 8,192 random complete
+    code sets (literal/length, distance, code-length and deflate64 distance alphabets): same return value, root
+    bits, size and every entry."""
+    import ctypes
+
+    L = engine._L
+    L.zs_inftab_selfcheck.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.POINTER(ctypes.c_ulonglong)]
+    bad = ctypes.c_ulonglong(0)
+    assert L.zs_inftab_selfcheck(0, 12345, 256, 32, ctypes.byref(bad)) == 0
+    assert bad.value == 0

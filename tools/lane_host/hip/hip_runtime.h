@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <algorithm>
+#define ZS_HOST_BUILD 1  // (zs_inftab.h: the wave-parallel table builder needs a real wave)
 #define __global__
 #define __device__
 #define __host__

@@ -70,6 +70,19 @@ extern "C" int zs_seg_wdbg_fetch(void* out, unsigned long long bytes) {
 }
 #endif
 
+#if ZS_SEG_EXP & 16
+// header sub-phases, summed over all headers: code-length table, code-length decode, lit/len table, dist table, headers
+__device__ unsigned long long zs_seg_hdbg[8];
+extern "C" int zs_seg_hdbg_fetch(void* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_seg_hdbg), sizeof(zs_seg_hdbg));
+}
+#define HD_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define HD_ADD(i, a, b) do { if ((threadIdx.x & 63u) == 0) atomicAdd(&zs_seg_hdbg[i], (b) - (a)); } while (0)
+#else
+#define HD_T(v) do { } while (0)
+#define HD_ADD(i, a, b) do { } while (0)
+#endif
+
 // ------------------------------------------------------------- lane reader
 // One lane's bit reader (the lane kernel's scheme: clamped aligned words, one
 // refill ahead, zero past the end), started at any bit; member bit positions
@@ -200,10 +213,10 @@ static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* l
     for (; sym < 280; sym++) lens[sym] = 7;
     for (; sym < 288; sym++) lens[sym] = 8;
     lbits = 9;
-    zs_inflate_table(LENS, lens, 288, codes, &lbits, work, d64, &lused);
+    zs_inflate_table_wave<false>(LENS, lens, 288, codes, &lbits, work, d64, &lused);
     for (sym = 0; sym < 32; sym++) lens[sym] = 5;
     dbits = 5;
-    zs_inflate_table(DISTS, lens, 32, codes + lused, &dbits, work, d64, &dused);
+    zs_inflate_table_wave<false>(DISTS, lens, 32, codes + lused, &dbits, work, d64, &dused);
   } else if (type == 2) {  // dynamic (inflate.ts:662-836)
     const uint32_t nlen = zs_wr_take(R, 5) + 257, ndist = zs_wr_take(R, 5) + 1, ncode = zs_wr_take(R, 4) + 4;
     if (nlen > 286 || (!d64 && ndist > 30)) return false;
@@ -211,7 +224,9 @@ static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* l
     for (i = 0; i < ncode; i++) lens[ZS_BL_ORDER[i]] = (uint16_t)zs_wr_take(R, 3);
     for (; i < 19; i++) lens[ZS_BL_ORDER[i]] = 0;
     uint32_t cbits = 7, used;
-    if (zs_inflate_table(CODES, lens, 19, codes, &cbits, work, d64, &used)) return false;
+    HD_T(t0);
+    if (zs_inflate_table_wave<false>(CODES, lens, 19, codes, &cbits, work, d64, &used)) return false;
+    HD_T(t1);
     i = 0;
     while (i < nlen + ndist) {
       const zcode here = zs_wr_decode(R, codes, cbits);
@@ -234,10 +249,19 @@ static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* l
       while (rep--) lens[i++] = (uint16_t)val;
     }
     if (zs_wr_over(R) || zs_u(lens[256]) == 0) return false;
+    HD_T(t2);
     lbits = 9;
-    if (zs_inflate_table(LENS, lens, nlen, codes, &lbits, work, d64, &lused)) return false;
+    if (zs_inflate_table_wave<false>(LENS, lens, nlen, codes, &lbits, work, d64, &lused)) return false;
+    HD_T(t3);
     dbits = 6;
-    if (zs_inflate_table(DISTS, lens + nlen, ndist, codes + lused, &dbits, work, d64, &dused)) return false;
+    if (zs_inflate_table_wave<false>(DISTS, lens + nlen, ndist, codes + lused, &dbits, work, d64, &dused)) return false;
+    HD_T(t4);
+    HD_ADD(0, t0, t1);
+    HD_ADD(1, t1, t2);
+    HD_ADD(2, t2, t3);
+    HD_ADD(3, t3, t4);
+    HD_ADD(4, 0ull, 1ull);
+    HD_ADD(5, 0ull, (unsigned long long)(nlen + ndist));
   } else {
     return false;  // "invalid block type"
   }

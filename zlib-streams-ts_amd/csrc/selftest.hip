@@ -62,3 +62,111 @@ __global__ __launch_bounds__(64) void zs_k_selftest(uint32_t* __restrict__ bad, 
   }
   if (errs) atomicAdd(bad, errs);
 }
+
+// ---------------------------------------------------------------------------
+// zs_inflate_table_wave (zs_inftab.h) against zlib's serial inflate_table: one
+// wave per block builds random complete code sets (a leaf split at random until
+// the set has its symbol count; lengths <= 15, shuffled over the alphabet) with
+// both and compares the return value, root bits, table size and every entry.
+// Test infrastructure (tests/test_gpu_inflate.py); not used by the decoders.
+#include "zs_inftab.h"
+
+// the first failing set: type, d64, codes, returns, roots, sizes, lens[320], both tables
+__device__ uint32_t zs_inftab_dbg[16 + 320 + 2 * (ENOUGH_LENS + 8)];
+__device__ uint32_t zs_inftab_dbg_taken;
+extern "C" int zs_inftab_dbg_fetch(void* out, unsigned long long bytes) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_inftab_dbg), bytes < sizeof(zs_inftab_dbg) ? bytes : sizeof(zs_inftab_dbg));
+}
+__global__ __launch_bounds__(64) void zs_k_inftab_check(uint32_t seed, uint32_t sets, unsigned long long* bad) {
+  __shared__ uint16_t lens[320], work[320], work2[320];
+  __shared__ zcode ta[ENOUGH_LENS + 8], tb[ENOUGH_LENS + 8];
+  __shared__ uint8_t depth[320];
+  const uint32_t lane = threadIdx.x;
+  uint32_t x = seed * 0x9e3779b9u + blockIdx.x * 0x85ebca6bu + 1u;
+  auto rnd = [&]() {
+    x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+    return x;
+  };
+  __shared__ uint32_t s_kind, s_codes;
+  unsigned long long errs = 0;
+  for (uint32_t t = 0; t < sets; t++) {
+    if (lane == 0) {  // (lane 0 draws everything: the generator below draws a varying number of times)
+      s_kind = rnd() % 4u;  // LENS, DISTS, CODES, deflate64 DISTS
+      const uint32_t kd = s_kind;
+      s_codes = kd == 0 ? 257u + rnd() % 30u : kd == 2 ? 19u : kd == 3 ? 32u : 2u + rnd() % 29u;
+    }
+    __syncthreads();
+    const uint32_t kind = s_kind;
+    const int type = kind == 0 ? LENS : kind == 2 ? CODES : DISTS;
+    const bool d64 = kind == 3;
+    const uint32_t codes = s_codes;
+    const uint32_t maxd = type == CODES ? 7u : 15u;
+    if (lane == 0) {
+      uint32_t k = 2u + rnd() % (codes - 1u);  // symbols in the code (>= 2: a complete set)
+      // leaves of a random full binary tree: split a random leaf (depth < maxd) until there are k
+      uint32_t nl = 1;
+      depth[0] = 0;
+      while (nl < k && nl < codes) {
+        uint32_t j = rnd() % nl, tries = 0;
+        while (depth[j] >= maxd && tries++ < 400u) j = rnd() % nl;
+        if (depth[j] >= maxd) break;
+        depth[j]++;
+        depth[nl++] = depth[j];
+      }
+      k = nl;
+      for (uint32_t s = 0; s < codes; s++) lens[s] = 0;
+      for (uint32_t l = 0; l < k; l++) {  // a random free symbol for each leaf
+        uint32_t s = rnd() % codes;
+        while (lens[s]) s = (s + 1u) % codes;
+        lens[s] = depth[l];
+      }
+      if (type == LENS) {  // the end-of-block code present, as a valid header needs
+        if (!lens[256]) {
+          uint32_t s = 0;
+          while (!lens[s]) s++;
+          lens[256] = lens[s];
+          lens[s] = 0;
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t ba = type == LENS ? 9u : type == CODES ? 7u : 6u, bb = ba, ua = 0, ub = 0;
+    const int ra = zs_inflate_table(type, lens, codes, ta, &ba, work, d64, &ua);
+    __syncthreads();
+    const int rb = zs_inflate_table_wave<true>(type, lens, codes, tb, &bb, work2, d64, &ub);
+    __syncthreads();
+    unsigned long long e0 = 0;
+    if (ra != rb || ba != bb || (ra == 0 && ua != ub)) e0 = 1;
+    else if (ra == 0)
+      for (uint32_t i = lane; i < ua; i += 64) e0 += ta[i] != tb[i] ? 1u : 0u;
+    errs += e0;
+    const bool any = __syncthreads_or(e0 != 0);
+    if (any && lane == 0 && atomicExch(&zs_inftab_dbg_taken, 1u) == 0u) {
+      uint32_t* g = zs_inftab_dbg;
+      g[0] = (uint32_t)type; g[1] = d64; g[2] = codes; g[3] = (uint32_t)ra; g[4] = (uint32_t)rb;
+      g[5] = ba; g[6] = bb; g[7] = ua; g[8] = ub;
+      for (uint32_t i = 0; i < 320; i++) g[16 + i] = i < codes ? lens[i] : 0u;
+      for (uint32_t i = 0; i < ENOUGH_LENS + 8; i++) {
+        g[16 + 320 + i] = ta[i];
+        g[16 + 320 + ENOUGH_LENS + 8 + i] = tb[i];
+      }
+    }
+    __syncthreads();
+  }
+  if (errs) atomicAdd(bad, errs);
+}
+
+extern "C" int zs_inftab_selfcheck(int device, uint32_t seed, uint32_t blocks, uint32_t sets,
+                                   unsigned long long* mismatches) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  unsigned long long* d = nullptr;
+  if (hipMalloc(&d, sizeof(*d)) != hipSuccess) return -1;
+  int r = hipMemset(d, 0, sizeof(*d)) == hipSuccess ? 0 : -1;
+  if (r == 0) {
+    zs_k_inftab_check<<<blocks, 64>>>(seed, sets, d);
+    r = hipDeviceSynchronize() == hipSuccess && hipMemcpy(mismatches, d, sizeof(*d), hipMemcpyDeviceToHost) == hipSuccess
+            ? 0 : -1;
+  }
+  (void)hipFree(d);
+  return r;
+}
