@@ -379,8 +379,10 @@ struct SwSig<true> {
     a = sw_x7(sw_word(win, p)) | (sw_word(win, p + 3) << 8);
     b = sw_word(win, p + 6);
   }
+  // (the record's third word: the four bytes past the signature, which a long
+  // candidate's first extension step compares -- from the ring, not the window)
   static __device__ __forceinline__ uint4 rec(const uint32_t* win, uint32_t q, uint32_t w0) {
-    return make_uint4(sw_x7(w0) | (sw_word(win, q + 3) << 8), sw_word(win, q + 6), 0u, 0u);
+    return make_uint4(sw_x7(w0) | (sw_word(win, q + 3) << 8), sw_word(win, q + 6), sw_word(win, q + EXT), 0u);
   }
   __device__ __forceinline__ uint32_t mbits(uint32_t x, uint32_t y, uint32_t) const {
     uint32_t f0, f1;
@@ -458,10 +460,8 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     const uint32_t i = (uint32_t)j & (ZS_SW_RING - 1);
     R->ab[i] = make_uint2(r.x, r.y);
     R->ab[i + ZS_SW_RING] = make_uint2(r.x, r.y);
-    if (!A7) {
-      R->c[i] = r.z;
-      R->c[i + ZS_SW_RING] = r.z;
-    }
+    R->c[i] = r.z;  // (A7: the bytes past the signature)
+    R->c[i + ZS_SW_RING] = r.z;
     R->key[i] = r.w;
     R->key[i + ZS_SW_RING] = r.w;
   };
@@ -570,9 +570,11 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
 #pragma unroll
           for (uint32_t u = 0; u < 8; u++) {
             if (u < cnt && sc[u] >= long_m) {
-              const uint32_t q = R->key[base - t0 - u] & 0xffffu;
-              const uint32_t x = sw_word(win, q + Sig::EXT) ^ own_ext;
-              uint32_t len = x ? Sig::EXT + ((uint32_t)__builtin_ctz(x) >> 3) : sw_extend(win, p, q, maxc, Sig::EXT + 4u);
+              // the next four bytes: A7 records carry them (c), else from the window
+              const uint32_t x = (A7 ? R->c[base - t0 - u]
+                                     : sw_word(win, (R->key[base - t0 - u] & 0xffffu) + Sig::EXT)) ^ own_ext;
+              uint32_t len = x ? Sig::EXT + ((uint32_t)__builtin_ctz(x) >> 3)
+                               : sw_extend(win, p, R->key[base - t0 - u] & 0xffffu, maxc, Sig::EXT + 4u);
               len = min(min(len, maxc), nice);
               gl = max(gl, (len << 3) | (7u - u));
             }
