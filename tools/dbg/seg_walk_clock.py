@@ -2,7 +2,7 @@
 
   make -C zlib-streams-ts_amd/csrc BUILD=build_exp OUT=../../variants/segexp/libzsgpu.so \\
        HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -DZS_SEG_EXP=3"
-  ZS_LIB=variants/segexp/libzsgpu.so python3 tools/dbg/seg_walk_clock.py [n] [size] [fmt]
+  ZS_LIB=variants/segexp/libzsgpu.so python3 tools/dbg/seg_walk_clock.py [n] [size] [fmt] [OPTION=VALUE ...]
 
 For n T-corpus members of `size` bytes at L6: per entry the header cycles, the spans' phase 1 (lanes decoding
 alone) and the rest (sync, records), blocks, spans, the busiest lane's symbols, reseeks."""
@@ -21,6 +21,9 @@ def main():
     fmt = sys.argv[3] if len(sys.argv) > 3 else "deflate-raw"
     import zsamd
     eng = zsamd.Engine(0)
+    for kv in sys.argv[4:]:  # engine options NAME=VALUE
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     buf = bytes(zsamd.corpus("text", 0, n, size))
     srcs = [buf[i * size:(i + 1) * size] for i in range(n)]
     comps = eng.compress_batch(srcs, "deflate-raw" if fmt == "deflate64-raw" else fmt, 6)

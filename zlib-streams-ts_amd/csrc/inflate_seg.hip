@@ -227,27 +227,48 @@ static __device__ bool zs_sg_header(zs_wave_reader& R, zcode* codes, uint16_t* l
     HD_T(t0);
     if (zs_inflate_table_wave<false>(CODES, lens, 19, codes, &cbits, work, d64, &used)) return false;
     HD_T(t1);
+    // The code lengths (inflate.ts:702-778), one symbol at a time but with no
+    // memory round trip per symbol: the code-length code's table (<= 128
+    // entries of bits << 8 | symbol) sits in a VGPR, lane l holding entries l
+    // and l + 64, read with v_readlane at the input's next cbits bits; a repeat
+    // is stored by up to 138 lanes at once; the previous length stays in a
+    // register.  (Was an LDS lookup and readfirstlane per symbol and a store
+    // per repeated length: ~44k core cycles per header, profiles/r06/hdr/.)
+    const uint32_t lane = threadIdx.x & 63u, csz = 1u << cbits, cmask = csz - 1u, N = nlen + ndist;
+    const zcode c0 = lane < csz ? codes[lane] : 0u, c1 = lane + 64u < csz ? codes[lane + 64u] : 0u;
+    const uint32_t tv = ((C_BITS(c0) << 8) | C_VAL(c0)) | (((C_BITS(c1) << 8) | C_VAL(c1)) << 16);
+    uint32_t prev = 0;
     i = 0;
-    while (i < nlen + ndist) {
-      const zcode here = zs_wr_decode(R, codes, cbits);
-      const uint32_t v = C_VAL(here);
+    while (i < N) {
+      if (R.bits < 32) zs_wr_fill(R);
+      const uint32_t idx = (uint32_t)R.hold & cmask;
+      const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)(idx & 63u));
+      const uint32_t e = (idx & 64u) ? e2 >> 16 : e2 & 0xffffu;
+      const uint32_t nb = e >> 8, v = e & 0xffu;
+      R.hold >>= nb;
+      R.bits -= nb;
       if (v < 16) {
         lens[i++] = (uint16_t)v;
+        prev = v;
         continue;
       }
       uint32_t rep, val = 0;
       if (v == 16) {
         if (i == 0) return false;
-        val = zs_u(lens[i - 1]);
+        val = prev;
         rep = 3 + zs_wr_take(R, 2);
       } else if (v == 17) {
         rep = 3 + zs_wr_take(R, 3);
       } else {
         rep = 11 + zs_wr_take(R, 7);
       }
-      if (i + rep > nlen + ndist) return false;
-      while (rep--) lens[i++] = (uint16_t)val;
+      if (i + rep > N) return false;
+      for (uint32_t j = lane; j < rep; j += 64u) lens[i + j] = (uint16_t)val;
+      i += rep;
+      prev = val;
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // (the lengths visible to this wave's table builds)
+    __builtin_amdgcn_wave_barrier();
     if (zs_wr_over(R) || zs_u(lens[256]) == 0) return false;
     HD_T(t2);
     lbits = 9;
