@@ -251,6 +251,9 @@ void zs_set_timing(zs_ctx *ctx, int on);
  * default 0 = 4096 for members of >= 64 KiB of input on average, else 2048):
  * input bits per lane of an entry's first block; "seg_wide"
  * (default 1): the 2048-bit sync window for a batch of few large members;
+ * "seg_split" (0 off, 1 on, default 2 = batches of at most 2 large members per CU):
+ * each piece is cut in two at the first symbol start past its lane's middle, so
+ * the decode runs twice the pieces, each half as long;
  * "seg_big_bits" (>= 65536, default 2^21): members with more input bits also
  * walk from the block starts a finder kernel proposes (more walks per member);
  * "seg_scratch_mb" (default 16384): the segmented decode's u16 scratch per

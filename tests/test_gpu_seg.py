@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 class _opts:
     DEFAULTS = {"inflate_seg": 1, "seg_bits": 0, "seg_small_batch": 16384, "seg_small_min": 4096,
                 "inflate_fast": 1, "inflate_ref_wrap": 1, "inflate_wave_min": 32768, "seg_scratch_mb": 16384,
-                "seg_wide": 1, "seg_big_bits": 1 << 21, "timing": 0, "check_phases": 0}
+                "seg_wide": 1, "seg_big_bits": 1 << 21, "timing": 0, "check_phases": 0, "seg_split": 2}
 
     def __init__(self, engine, **kw):
         self.e, self.kw = engine, kw
@@ -74,10 +74,12 @@ def test_segmented_decode_equals_the_reference(engine, fmt):
     assert ok == {"deflate-raw": 24, "deflate": 22, "gzip": 19}[fmt]
 
 
-@pytest.mark.parametrize("opt", [("seg_big_bits", 65536), ("seg_wide", 0), ("check_phases", 1), ("timing", 1)])
+@pytest.mark.parametrize("opt", [("seg_big_bits", 65536), ("seg_wide", 0), ("check_phases", 1), ("timing", 1),
+                                 ("seg_split", 0), ("seg_split", 1)])
 def test_walk_options_do_not_change_bytes(engine, opt):
     """seg_big_bits (members over it also walk from the block starts zs_k_split_find proposes), seg_wide (the
-    2,048-bit sync window), check_phases and timing only change how the decode runs: T- and M-corpus members of
+    2,048-bit sync window), seg_split (pieces cut in two at the walk's mid points), check_phases and timing only
+    change how the decode runs: T- and M-corpus members of
     100 .. 500 KB at L6 / L9, every one finished by the segmented decode, equal the oracle with the reference's
     window-wrap copy, status and message included."""
     rng = random.Random(sum(opt[0].encode()))

@@ -1,0 +1,8 @@
+#!/bin/bash
+# round 6: split pieces (the plan cuts each piece at the walk's mid point) -- seg/inflate/boundary suites, decode shards
+set -o pipefail
+O=gpurun_out/r06j; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_gpu_seg.py tests/test_gpu_inflate.py tests/test_gpu_split.py -x -q --timeout 300 --timeout-method thread > $O/test.log 2>&1 || { tail -30 $O/test.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_boundary.py -x -q --timeout 600 --timeout-method thread -k "shard or large_member or c5 or gunzip" > $O/test_boundary.log 2>&1 || { tail -30 $O/test_boundary.log; exit 1; }
+TAG=r06j bash tools/dec_shards.sh > $O/dec_shards.txt 2>&1 || exit 1
+echo done

@@ -122,6 +122,7 @@ struct zs_ctx {
   uint32_t seg_small_batch = 16384; // batches of at most this many members ...
   uint32_t seg_small_min = 4096;    // ... send members with more input bytes than this to it too
   bool seg_wide = true;             // the 2048-bit sync window for a batch of few large members
+  int seg_split = 2;                // pieces cut in two at the walk's mid points (0 off, 1 on, 2 auto: small batches)
   uint32_t seg_big_bits = ZS_SEG_BIG_BITS;  // members with more input bits also walk from the finder's block starts
   uint64_t seg_scratch_max = 16ull << 30;  // bytes of u16 piece scratch the segmented decode may take per batch
   uint32_t ncu = 256;               // compute units of the device
@@ -340,6 +341,10 @@ int zs_set_option(zs_ctx* c, const char* name, int value) {
   else if (!strcmp(name, "inflate_split")) c->inflate_split = value != 0;
   else if (!strcmp(name, "inflate_seg")) c->inflate_seg = value != 0;
   else if (!strcmp(name, "seg_wide")) c->seg_wide = value != 0;
+  else if (!strcmp(name, "seg_split")) {
+    if (value < 0 || value > 2) return fail(ZS_STREAM_ERROR, "seg_split must be 0, 1 or 2 (auto)");
+    c->seg_split = value;
+  }
   else if (!strcmp(name, "seg_big_bits")) {
     if (value < 65536) return fail(ZS_STREAM_ERROR, "seg_big_bits must be >= 65536");
     c->seg_big_bits = (uint32_t)value;
@@ -1214,7 +1219,8 @@ __global__ void zs_k_inflate_check(const uint8_t* in, const uint64_t* in_off, co
 static uint32_t seg_pmax(uint32_t in_len) {
   const uint64_t nbits = 8ull * in_len;
   const uint64_t spans = nbits / ZS_SEG_BLOCK_BITS + 2 * nbits / (64ull * ZS_SEG_W) + 8;
-  return (uint32_t)std::min<uint64_t>(spans * ZS_SEG_LANES, nbits / ZS_SEG_W + spans + 1);
+  // (x 2: split mode cuts pieces in two)
+  return 2u * (uint32_t)std::min<uint64_t>(spans * ZS_SEG_LANES, nbits / ZS_SEG_W + spans + 1);
 }
 static uint64_t seg_scratch_elems(uint32_t in_len, uint32_t out_cap) {
   return (((uint64_t)out_cap + 7) & ~7ull) + ZS_SEG_PAD * (uint64_t)seg_pmax(in_len) + 16;
@@ -1237,7 +1243,7 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   for (uint32_t k = 0; k < ng; k++) {
     const uint32_t i = c->hglist[k];
     const uint64_t nbits = 8ull * in_len[i];
-    const uint64_t spans = nbits / ZS_SEG_BLOCK_BITS + 2 * nbits / (64ull * ZS_SEG_W) + 8;
+    const uint64_t spans = 2 * (nbits / ZS_SEG_BLOCK_BITS + 2 * nbits / (64ull * ZS_SEG_W) + 8);  // (x 2: split mode)
     c->hgspb[k + 1] = c->hgspb[k] + (uint32_t)spans;
     c->hgpbase[k + 1] = c->hgpbase[k] + seg_pmax(in_len[i]);
     c->hgsbase[k + 1] = c->hgsbase[k] + seg_scratch_elems(in_len[i], out_cap[i]);
@@ -1303,15 +1309,24 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   // (512 x 256 KiB: 5.3 -> 4.2 ms); otherwise 1024 (occupancy: 1,024 x 256 KiB 7.6 vs 6.6 ms)
   uint64_t gbits = 0;
   for (uint32_t k = 0; k < ng; k++) gbits += 8ull * in_len[c->hglist[k]];
-  const bool w2k = c->seg_wide && nwalk <= 3u * c->ncu && gbits >= 65536ull * 8 * ng;
+  const bool large = gbits >= 65536ull * 8 * ng;  // members of 64 KiB of input or more on average
+  const bool w2k = c->seg_wide && nwalk <= 3u * c->ncu && large;
   auto walk = d64 ? (w2k ? zs_k_seg_walk<true, 2048u> : zs_k_seg_walk<true, 1024u>)
                   : (w2k ? zs_k_seg_walk<false, 2048u> : zs_k_seg_walk<false, 1024u>);
   // bits per lane: large members (4,096 x 256 KiB: 17.2 -> 15.9 ms, its 512-member shard 3.70 -> 3.57) walk fewer,
   // wider spans; 64 KiB members keep 2048 (the 1,024-member gunzip shard: 2.11 vs 2.45 ms, the decode's pieces
   // too few to fill the chip) -- tools/segbits_ab.sh
   const uint32_t sbits = c->seg_bits ? c->seg_bits : gbits >= (1ull << 19) * ng ? 4096u : 2048u;
+  // Split mode: the plan cuts each piece in two at the first symbol start past its lane's middle (the walk
+  // records it), so the decode runs twice the pieces, each half as long.  The resolve then takes twice the
+  // rounds (one piece per round) and the plan twice the steps, so it pays only where the decode of few large
+  // members leaves SIMDs idle: a rank's 512 x 256 KiB shard 3.13 -> 2.93 ms (decode 1.36 -> 0.78, plan
+  // 0.08 -> 0.20, resolve 0.30 -> 0.50); 1,024 x 256 KiB 5.07 -> 5.52, C5-i's 1,024 x 64 KiB 1.93 -> 2.09
+  // (profiles/r06/seg/split_*)
+  const int split = c->seg_split == 2 ? (ng <= 2u * c->ncu && large ? 1 : 0) : c->seg_split;
   walk<<<nwalk, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, ng, c->gbig.as<uint32_t>(), nbig, wbits, gf, gspb, gb, gln, gt,
-                             ge, gm, cnt + 2, c->gspl.as<uint32_t>(), std::max<uint32_t>(sbits, w2k ? 2048u : 0u));
+                             ge, gm, cnt + 2, c->gspl.as<uint32_t>(), std::max<uint32_t>(sbits, w2k ? 2048u : 0u),
+                             split);
   if (int r = mark(c, sd, "seg_walk")) return r;
   zs_k_seg_plan<<<ng, 64, 0, sd>>>(d_in, d_ioff, d_ilen, d_ocap, gl, ng, wbits, refw ? 1 : 0, gb, gln, ge, gm,
                                    c->gpbase.as<uint32_t>(), c->gplist.as<uint4>());

@@ -357,7 +357,7 @@ struct zs_sg_walk_lds {
 template <bool D64, uint32_t W>
 static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, uint32_t n, uint32_t sym0, uint32_t pe0,
                                       uint32_t nl, uint32_t S, uint32_t lbits, uint32_t dbits, uint32_t dofs,
-                                      zs_seg_lane* __restrict__ recs, uint32_t& send, bool& bad_out) {
+                                      zs_seg_lane* __restrict__ recs, uint32_t& send, bool& bad_out, bool split) {
   const uint32_t lane = threadIdx.x;
 #if ZS_SEG_EXP & 2
   const unsigned long long dbg_t0 = __builtin_readcyclecounter();
@@ -403,6 +403,9 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
 #pragma unroll
   for (uint32_t e = 0; e < ZS_SEG_NEOB; e++) eob_sb[e] = eob_end[e] = eob_cum[e] = bad_sb[e] = 0;
   uint32_t ock = 0, tck = 0;  // checkpoint buckets filled
+  // split mode: the first symbol start at or past the lane's middle, the output count there, the symbol before's
+  const uint32_t qm = split ? q + S / 2u : ZS_SEG_NONE;
+  uint32_t mid_sb = ZS_SEG_NONE, mid_cum = 0, mid_ll = 0;
   // the bitmaps' current word (own words 0 .., tail words W / 32 ..) collects
   // in a register: positions only grow, so each word is stored once
   constexpr uint32_t NW = W / 32u;
@@ -425,6 +428,11 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
   };
   while (pos < lim) {
     const uint32_t off = pos - q, toff = pos - qn;
+    if (pos >= qm && mid_sb == ZS_SEG_NONE) {
+      mid_sb = pos;
+      mid_cum = cum;
+      mid_ll = last_len;
+    }
     if (off < W) {
       mark(off >> 5, off & 31u);
       if (off >= ock * ZS_SEG_CKB) {
@@ -655,6 +663,11 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
     P.end = end;
     P.cnt = ce - cc;
     P.last_len = ll;
+    // a split point strictly inside the piece, on the true stream (past its start)
+    const bool cut = mid_sb != ZS_SEG_NONE && mid_sb > start && mid_sb < end && mid_cum > cc && mid_cum < ce;
+    P.mb = cut ? mid_sb : ZS_SEG_NONE;
+    P.mc = cut ? mid_cum - cc : 0u;
+    P.mll = cut ? mid_ll : 0u;
     P.nev = ne;
     P.ev_k0 = k0;
 #pragma unroll
@@ -682,7 +695,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
                                                     zs_seg_lane* __restrict__ lanes, zcode* __restrict__ tcache,
                                                     zs_seg_ent* __restrict__ ents, zs_seg_mem* __restrict__ mem,
                                                     uint32_t* __restrict__ nspan, uint32_t* __restrict__ spans,
-                                                    uint32_t sbits) {
+                                                    uint32_t sbits, int split) {
   __shared__ zs_sg_walk_lds<W> L;
   const uint32_t lane = threadIdx.x;
   // the entry: blocks [0, n_list): entry 0 of list member blockIdx.x; then
@@ -824,15 +837,26 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
     }
     while (slen == ZS_SEG_NONE) {  // (a coded block's spans; left by break)
       // ---- a span
+      // (split mode: two slots, the second for the pieces' second halves, which the plan writes)
+      const uint32_t nsl = split ? 2u : 1u;
       uint32_t b = 0;
-      if (lane == 0) b = atomicAdd(&M.nalloc, 1u);
+      if (lane == 0) b = atomicAdd(&M.nalloc, nsl);
       b = zs_u(__shfl(b, 0));
-      if (b >= cap) {
+      if (b + nsl > cap) {
         good = false;
         break;
       }
       b += sb0;
-      if (lane == 0) spans[atomicAdd(nspan, 1u)] = b;  // (the decode's work list)
+      if (lane == 0) {  // (the decode's work list)
+        const uint32_t at = atomicAdd(nspan, nsl);
+        spans[at] = b;
+        if (split) spans[at + 1u] = b + 1u;
+      }
+      if (split) {
+        zs_seg_lane& P2 = lanes[(size_t)(b + 1u) * ZS_SEG_LANES + lane];
+        P2.act = 0;
+        P2.start = ZS_SEG_NONE;
+      }
       if (first) {
         tab = b;
         for (uint32_t i = lane; i < ntab; i += 64) tcache[(size_t)b * ZS_SEG_TAB + i] = L.codes[i];
@@ -845,7 +869,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
       uint32_t send = 0;
       bool sbad = false;
       const uint32_t k = zs_sg_span<D64, W>(L, src, n, cur, pe0, nl, S, lbits, dbits, dofs,
-                                         lanes + (size_t)b * ZS_SEG_LANES, send, sbad);
+                                         lanes + (size_t)b * ZS_SEG_LANES, send, sbad, split != 0);
 #if ZS_SEG_EXP & 2
       wd[1] += L.dbg[0];
       wd[2] += L.dbg[1];
@@ -868,9 +892,16 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
         Bk.S = S;
         Bk.next = ZS_SEG_NONE;
         Bk.flags = (k && !sbad ? ZS_SEG_B_OK : 0u) | (first ? ZS_SEG_B_FIRST : 0u) |
-                   (k == ZS_SG_K_BEND ? ZS_SEG_B_EOB : 0u) | (k == ZS_SG_K_BEND && last ? ZS_SEG_B_FINAL : 0u);
+                   (k == ZS_SG_K_BEND ? ZS_SEG_B_EOB : 0u) | (k == ZS_SG_K_BEND && last ? ZS_SEG_B_FINAL : 0u) |
+                   (split ? ZS_SEG_B_SPLIT : 0u);
         if (prevb == ZS_SEG_NONE) E.first = b;
         else blk[prevb].next = b;
+        if (split) {  // the second halves' slot: the same block and tables, off the entry's chain
+          zs_seg_blk& B2 = blk[b + 1u];
+          B2 = Bk;
+          B2.next = ZS_SEG_NONE;
+          B2.flags = Bk.flags & ZS_SEG_B_OK;
+        }
       }
       prevb = b;
       if (!k || sbad) {
@@ -969,6 +1000,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
                                                     zs_seg_mem* __restrict__ mem, const uint32_t* __restrict__ pbase,
                                                     uint4* __restrict__ ptab) {
   __shared__ zs_seg_lane P[ZS_SEG_LANES];
+  __shared__ zs_seg_lane Q[ZS_SEG_LANES];  // (split mode) the second halves, for the span's next slot
   __shared__ uint32_t s_bad, s_O, s_k, s_plen, s_first, s_prevg;
   __shared__ zs_sg_calls s_C;
   const uint32_t m = blockIdx.x, lane = threadIdx.x;
@@ -1006,6 +1038,11 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
         break;
       }
       P[lane] = lanes[(size_t)b * ZS_SEG_LANES + lane];
+      const bool split = (Bk.flags & ZS_SEG_B_SPLIT) != 0;
+      if (split) {
+        Q[lane].start = ZS_SEG_NONE;
+        Q[lane].act = 0;
+      }
       __syncthreads();
       if (lane == 0) {
         zs_sg_calls C = s_C;
@@ -1032,12 +1069,11 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
           plen = 0;
           first = false;
         }
-        for (uint32_t l = 0; l < ZS_SEG_LANES && !bad && !(Bk.flags & ZS_SEG_B_STORED); l++) {
-          zs_seg_lane& p = P[l];
-          if (p.start == ZS_SEG_NONE) continue;
+        // one piece (g: its record's global index; l0new: the first of a block)
+        auto piece = [&](zs_seg_lane& p, uint32_t g, bool l0new) {
           bool merge = false;
           if (!first && refw) {
-            if (l == 0 && newblk) {
+            if (l0new) {
               C.fills(O);  // the end-of-block code before it, at output O
             } else {
               C.fills(O - plen);  // the last symbol of the piece before
@@ -1046,9 +1082,10 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
             }
           }
           if (merge) {
-            // the piece before is in this block: in this span, or the entry's span before
-            const bool here = prevg / ZS_SEG_LANES == b;
-            zs_seg_lane& q = here ? P[prevg % ZS_SEG_LANES] : lanes[prevg];
+            // the piece before is in this block: in this span (or its second halves), or the entry's span before
+            const uint32_t ps = prevg / ZS_SEG_LANES;
+            zs_seg_lane& q = ps == b ? P[prevg % ZS_SEG_LANES]
+                             : (split && ps == b + 1u) ? Q[prevg % ZS_SEG_LANES] : lanes[prevg];
             q.dend = p.end;
             q.dcnt += p.cnt;
             p.act = 0;
@@ -1062,11 +1099,11 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
             p.wn = C.wn;
             p.wh = C.wh;
             p.cend = C.cend;
-            p.act = 1u | (l == 0 && newblk ? 0u : 2u);
+            p.act = 1u | (l0new ? 0u : 2u);
             if (k >= pmax) bad = true;
             else ptab[pb + k] = make_uint4(O, p.cnt, p.off, 0u);
             k++;
-            prevg = b * ZS_SEG_LANES + l;
+            prevg = g;
           }
           if (refw) {
             for (uint32_t x = 0; x < p.nev; x++) {
@@ -1080,6 +1117,31 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
           O += p.cnt;
           plen = p.last_len;
           first = false;
+        };
+        for (uint32_t l = 0; l < ZS_SEG_LANES && !bad && !(Bk.flags & ZS_SEG_B_STORED); l++) {
+          zs_seg_lane& p = P[l];
+          if (p.start == ZS_SEG_NONE) continue;
+          if (split && p.mb != ZS_SEG_NONE) {
+            // split mode: the piece as two, cut at its split point (the walk's first symbol start past the
+            // lane's middle): the second half into the next slot, with the events after the cut
+            zs_seg_lane& h = Q[l];
+            h = p;
+            h.start = p.mb;
+            h.cnt = p.cnt - p.mc;
+            uint32_t na = 0;
+            for (uint32_t x = 0; x < p.nev; x++) na += p.ev_o[x] < p.mc ? 1u : 0u;
+            h.nev = p.nev - na;
+            h.ev_k0 = p.ev_k0 + na;
+            for (uint32_t x = 0; x < h.nev; x++) h.ev_o[x] = p.ev_o[x + na] - p.mc;
+            p.end = p.mb;
+            p.cnt = p.mc;
+            p.last_len = p.mll;
+            p.nev = na;
+            piece(p, b * ZS_SEG_LANES + l, l == 0 && newblk);
+            if (!bad) piece(h, (b + 1u) * ZS_SEG_LANES + l, false);
+          } else {
+            piece(p, b * ZS_SEG_LANES + l, l == 0 && newblk);
+          }
         }
         s_C = C;
         s_O = O;
@@ -1092,6 +1154,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
       __syncthreads();
       // the pieces' plan back to HBM
       if (P[lane].start != ZS_SEG_NONE) lanes[(size_t)b * ZS_SEG_LANES + lane] = P[lane];
+      if (split) lanes[(size_t)(b + 1u) * ZS_SEG_LANES + lane] = Q[lane];
       __threadfence_block();
       __syncthreads();
       b = Bk.next;
@@ -1575,7 +1638,7 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
   template __global__ void zs_k_seg_walk<D, W>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,  \
                                                uint32_t, const uint32_t*, uint32_t, int, const uint64_t*,          \
                                                const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*, zs_seg_ent*,    \
-                                               zs_seg_mem*, uint32_t*, uint32_t*, uint32_t);
+                                               zs_seg_mem*, uint32_t*, uint32_t*, uint32_t, int);
 ZS_SEG_WALK_INST(false, 1024u)
 ZS_SEG_WALK_INST(true, 1024u)
 ZS_SEG_WALK_INST(false, 2048u)

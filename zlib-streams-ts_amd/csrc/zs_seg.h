@@ -27,6 +27,7 @@
 #define ZS_SEG_B_FIRST 4u  // starts a block (its header at hdr)
 #define ZS_SEG_B_EOB 8u    // ends its block (else the entry's next span continues it)
 #define ZS_SEG_B_STORED 16u  // a stored block (BTYPE 0): one piece, lane 0, its bytes copied from the input
+#define ZS_SEG_B_SPLIT 32u   // (split mode) the pieces' second halves are in the next slot, which the decode runs too
 
 // One span: a stretch of one block whose symbols a wave's lanes decode from
 // sym0 + j S (zs_k_seg_walk); its lanes' pieces in zs_seg_lane[span * 64 + j].
@@ -50,6 +51,9 @@ struct zs_seg_lane {
   uint32_t last_len;     // values of its last symbol (0: an end of block)
   uint32_t nev, ev_k0;   // sub-chunk crossing events: how many, the first sub-chunk index
   uint32_t ev_o[ZS_SEG_NEV];  // their symbols' output positions, relative to the piece start
+  // (split mode) where the plan may cut the piece in two: the first symbol start past
+  // the lane's middle (ZS_SEG_NONE: none), the values before it, the values of the symbol before it
+  uint32_t mb, mc, mll;
   // zs_k_seg_plan
   uint32_t O;            // member output position of the piece start
   uint32_t off;          // its scratch offset (u16 values; a multiple of 8)
@@ -74,7 +78,8 @@ template <bool D64, uint32_t W>  // W: the sync window (1024, or 2048 for a batc
 __global__ void zs_k_seg_walk(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* list,
                               uint32_t n_list, const uint32_t* big, uint32_t n_big, int wbits, const uint64_t* found,
                               const uint32_t* spb, zs_seg_blk* blk, zs_seg_lane* lanes, zcode* tcache,
-                              zs_seg_ent* ents, zs_seg_mem* mem, uint32_t* nspan, uint32_t* spans, uint32_t sbits);
+                              zs_seg_ent* ents, zs_seg_mem* mem, uint32_t* nspan, uint32_t* spans, uint32_t sbits,
+                              int split);
 __global__ void zs_k_seg_plan(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                               const uint32_t* out_cap, const uint32_t* list, uint32_t n_list, int wbits, int refw,
                               const zs_seg_blk* blk, zs_seg_lane* lanes, const zs_seg_ent* ents, zs_seg_mem* mem,
