@@ -1343,8 +1343,12 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   else
     zs_k_seg_decode<false, false><<<gdec, 64, 0, sd>>>(d_in, d_ioff, d_ilen, gl, cnt + 2, spl, gb, gln, gt, gm, sb, scr);
   if (int r = mark(c, sd, "seg_decode")) return r;
-  HIPCHK(hipFuncSetAttribute((const void*)zs_k_seg_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-  zs_k_seg_resolve<<<ng, 512, 65536, sd>>>(gl, gm, c->gpbase.as<uint32_t>(), c->gplist.as<uint4>(), sb, scr, d_out,
+  // the resolve: four members per CU (256 threads, a 32 KiB ring) unless the batch is too small to fill them
+  const bool rsmall = ng <= 2u * c->ncu;
+  const int rsm = rsmall ? 65536 : 32768;
+  auto resolve = rsmall ? zs_k_seg_resolve<512u, 65536u> : zs_k_seg_resolve<256u, 32768u>;
+  HIPCHK(hipFuncSetAttribute((const void*)resolve, hipFuncAttributeMaxDynamicSharedMemorySize, rsm));
+  resolve<<<ng, rsmall ? 512u : 256u, rsm, sd>>>(gl, gm, c->gpbase.as<uint32_t>(), c->gplist.as<uint4>(), sb, scr, d_out,
                                            d_ooff, lres, c->llen.as<uint32_t>(), cnt + 1, cnt + 3,
                                            c->gflist.as<uint32_t>());
   if (int r = mark(c, sd, "seg_resolve")) return r;

@@ -1518,11 +1518,17 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
 // covers up to 4,096 values of one piece; the next round's values are loaded
 // before this one's markers are looked up.  Bytes leave as whole words, 16 KiB
 // at a time.
-#define ZS_SG_RES_T 512u
+// T threads per member, an LDS ring of the last RING final bytes (a marker
+// further back reads the output already stored): <256, 32 KiB> -- four members per
+// CU -- for batches that fill the chip (4,096 x 256 KiB: resolve 2.27 -> ~1.8 ms),
+// <512, 64 KiB> for a few members (the 512-member shard: 0.50 vs 0.59 ms)
+#define ZS_SG_RES_T T
+#define ZS_SG_RES_RING RING
 #define ZS_SG_RES_E 8u                                  // values per thread per round
 #define ZS_SG_RES_R (ZS_SG_RES_T * ZS_SG_RES_E)        // values per round
-#define ZS_SG_RES_PT 512u                               // piece-table entries staged in LDS
-__global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restrict__ list,
+#define ZS_SG_RES_PT 256u                               // piece-table entries staged in LDS
+template <uint32_t T, uint32_t RING>
+__global__ __launch_bounds__(T) void zs_k_seg_resolve(const uint32_t* __restrict__ list,
                                                         const zs_seg_mem* __restrict__ mem,
                                                         const uint32_t* __restrict__ pbase,
                                                         const uint4* __restrict__ ptab,
@@ -1532,7 +1538,7 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
                                                         zs_lane_res* __restrict__ res, uint32_t* __restrict__ lens_out,
                                                         uint32_t* __restrict__ n_ok, uint32_t* __restrict__ n_left,
                                                         uint32_t* __restrict__ left) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t zs_rring[];  // 64 KiB of bytes
+  extern __shared__ __attribute__((aligned(16))) uint32_t zs_rring[];  // ZS_SG_RES_RING bytes
   __shared__ uint4 tab[ZS_SG_RES_PT];
   uint8_t* ring = reinterpret_cast<uint8_t*>(zs_rring);
   const uint32_t m = blockIdx.x, t = threadIdx.x;
@@ -1584,8 +1590,8 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
       const uint32_t x = cur[q];
       if (i < e.y && x >= 256u) {
         const uint32_t tg = O - (x - 255u);
-        if (O + i - tg < 65536u - ZS_SG_RES_R) {
-          cur[q] = ring[tg & 0xffffu];
+        if (O + i - tg < ZS_SG_RES_RING - ZS_SG_RES_R) {
+          cur[q] = ring[tg & (ZS_SG_RES_RING - 1u)];
         } else if ((tg >> 2) < wdone) {
           const uint32_t w = __hip_atomic_load(dst + (tg >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           cur[q] = (w >> (8u * (tg & 3u))) & 0xffu;
@@ -1598,13 +1604,13 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
 #pragma unroll
     for (uint32_t q = 0; q < ZS_SG_RES_E; q++) {
       const uint32_t i = i0 + q * ZS_SG_RES_T + t;
-      if (i < e.y) ring[(O + i) & 0xffffu] = (uint8_t)cur[q];
+      if (i < e.y) ring[(O + i) & (ZS_SG_RES_RING - 1u)] = (uint8_t)cur[q];
     }
     __syncthreads();
     // the complete words, 16 KiB at a time (and at the end)
     const uint32_t wend = k2 >= np ? (O + e.y) >> 2 : (k2 == k ? (O + j2) >> 2 : (O + e.y) >> 2);
     if (wend - wdone >= 4096u || k2 >= np) {
-      for (uint32_t w = wdone + t; w < wend; w += ZS_SG_RES_T) dst[w] = zs_rring[w & 0x3fffu];
+      for (uint32_t w = wdone + t; w < wend; w += ZS_SG_RES_T) dst[w] = zs_rring[w & (ZS_SG_RES_RING / 4u - 1u)];
       wdone = wend;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // (far markers read them back)
       __syncthreads();
@@ -1622,7 +1628,7 @@ __global__ __launch_bounds__(512) void zs_k_seg_resolve(const uint32_t* __restri
   }
   if (M.total & 3u) {  // the last bytes one by one: nothing is stored past the member's end
     uint8_t* db = out + out_off[s];
-    if (t < (M.total & 3u)) db[4u * wdone + t] = ring[(4u * wdone + t) & 0xffffu];
+    if (t < (M.total & 3u)) db[4u * wdone + t] = ring[(4u * wdone + t) & (ZS_SG_RES_RING - 1u)];
   }
   far = __syncthreads_or(far);
   if (t == 0) {
@@ -1651,3 +1657,12 @@ ZS_SEG_WALK_INST(true, 2048u)
 ZS_SEG_DEC_INST(false, false)
 ZS_SEG_DEC_INST(false, true)
 ZS_SEG_DEC_INST(true, false)
+
+template __global__ void zs_k_seg_resolve<256u, 32768u>(const uint32_t*, const zs_seg_mem*, const uint32_t*,
+                                                        const uint4*, const uint64_t*, const uint16_t*, uint8_t*,
+                                                        const uint64_t*, zs_lane_res*, uint32_t*, uint32_t*,
+                                                        uint32_t*, uint32_t*);
+template __global__ void zs_k_seg_resolve<512u, 65536u>(const uint32_t*, const zs_seg_mem*, const uint32_t*,
+                                                        const uint4*, const uint64_t*, const uint16_t*, uint8_t*,
+                                                        const uint64_t*, zs_lane_res*, uint32_t*, uint32_t*,
+                                                        uint32_t*, uint32_t*);

@@ -88,6 +88,7 @@ template <bool D64, bool REFW>
 __global__ void zs_k_seg_decode(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* list,
                                 const uint32_t* nspan, const uint32_t* spans, const zs_seg_blk* blk, const zs_seg_lane* lanes, const zcode* tcache,
                                 zs_seg_mem* mem, const uint64_t* sbase, uint16_t* scratch);
+template <uint32_t T, uint32_t RING>  // threads per member, its LDS ring of final bytes (dynamic LDS)
 __global__ void zs_k_seg_resolve(const uint32_t* list, const zs_seg_mem* mem, const uint32_t* pbase,
                                  const uint4* ptab, const uint64_t* sbase, const uint16_t* scratch, uint8_t* out,
                                  const uint64_t* out_off, zs_lane_res* res, uint32_t* lens_out, uint32_t* n_ok,
