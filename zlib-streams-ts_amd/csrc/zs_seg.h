@@ -10,7 +10,12 @@
 #define ZS_SEG_LANES 64u    // pieces per span (one lane each)
 #define ZS_SEG_W 1024u      // bits of a lane's start window whose symbol starts it records (the sync bitmaps; 2048 in
                             // the walk instance for batches of few large members: fewer chains that do not meet)
-#define ZS_SEG_CKB 128u     // spacing of a lane's (position, output count) checkpoints in its window
+#ifndef ZS_SEG_CKB
+// spacing of a lane's (position, output count) checkpoints in its window: 256 bits keeps the
+// 1,024-bit walk at 25 KB of LDS, six walks per CU instead of five (4,096 x 256 KiB decode 14.45 ->
+// 13.73 ms, C5-i 8.98 -> 8.47 ms; the re-decode from a checkpoint is at most 256 bits)
+#define ZS_SEG_CKB 256u
+#endif
 #define ZS_SEG_NEV 4u       // sub-chunk crossing events a lane records
 #define ZS_SEG_NEOB 4u      // end-of-block codes a lane logs
 #define ZS_SEG_PAD 16u      // u16 values of padding behind each piece's scratch
