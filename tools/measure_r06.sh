@@ -3,7 +3,7 @@
 # BASELINE config's bench line (inflate configs with their per-rank shard sweeps),
 # rocprofv3 kernel trace + FETCH/WRITE passes and SQ passes.  Logs under $1; copy
 # the summaries into profiles/r06/ with tools/collect_r06.sh.
-# usage: tools/measure_r06.sh OUTDIR [tests|benches|ibenches|dbenches|profiles[12]|sq[12]|all]...
+# usage: tools/measure_r06.sh OUTDIR [tests|benches|ibenches|dbenches|profiles[12]|sq[12]|rehearsal|all]...
 set -u
 OUT=$1; shift
 WHAT=${*:-all}
@@ -63,5 +63,10 @@ run sq_c5_d64 500 tools/pmc_sq.sh "$OUT/sq_c5_d64" $C5D
 run sq_c5_gzip_l6 500 tools/pmc_sq.sh "$OUT/sq_c5_gzip_l6" $C5G
 run sq_c4_l9 500 tools/pmc_sq.sh "$OUT/sq_c4_l9" $C4L9
 run sq_c4_l1 500 tools/pmc_sq.sh "$OUT/sq_c4_l1" $C4L1
+fi
+if want rehearsal; then
+run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+ZS_BENCH_BACKEND=gloo run bench_2ranks_gloo_1gpu 400 python3 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline
+ZS_BENCH_BACKEND=gloo run inflate_2ranks_gloo_1gpu 400 python3 bench.py --gpus 2 --mode inflate --steps 5 --warmup 2 --no-cpu-baseline
 fi
 echo measure-done

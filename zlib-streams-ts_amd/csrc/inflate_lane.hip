@@ -280,7 +280,9 @@ struct zs_lane_out {
   uint32_t P, F, w0, cw;
   __device__ __forceinline__ void init(uint8_t* dst, uint32_t* lds_ring) {
     const uintptr_t a = (uintptr_t)dst;
-    base = reinterpret_cast<uint32_t*>(a & ~(uintptr_t)15);
+    // (pointer arithmetic, not an integer round trip: the compiler then knows base is global memory
+    // and issues global loads / stores instead of flat ones, which also count against lgkmcnt)
+    base = reinterpret_cast<uint32_t*>(dst - (a & 15u));
     ring = lds_ring;
     P = (uint32_t)(a & 15u);
     w0 = P >> 2;

@@ -382,8 +382,11 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
     L.s.tck[lane][i] = ZS_SEG_NONE;
   }
   L.odone[lane] = 0;
-  volatile uint32_t* const vodone = L.odone;
-  volatile uint32_t* const vown_next = lane + 1u < nl ? L.s.own[lane + 1u] : L.s.own[lane];
+  // (LDS-typed: through a generic pointer a volatile access is a flat one, waited for with vmcnt(0) -- the
+  // input prefetch included)
+  typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
+  lds_vu32* const vodone = (lds_vu32*)L.odone;
+  lds_vu32* const vown_next = (lds_vu32*)(lane + 1u < nl ? L.s.own[lane + 1u] : L.s.own[lane]);
   bool left_own = false;
   // ---- 1. the lane's own decode
   zs_sg_reader G;
@@ -1219,9 +1222,17 @@ static_assert(ZS_SG_RING >= 16u + 7u && (ZS_SG_RING & (ZS_SG_RING - 1u)) == 0, "
 // One lane's u16 output (bytes, or markers 255 + k: the value k positions
 // before the piece): a ZS_SG_RING-value LDS ring, whole 16-byte units to HBM (the
 // piece's scratch is 16-byte aligned and padded, so no unit is shared).
+// (dst and ring typed by address space: with generic pointers the compiler folds get()'s two
+// loads into one flat load of a selected pointer, waited for on both counters)
+typedef __attribute__((address_space(1))) uint16_t zs_g_u16;
+typedef __attribute__((address_space(3))) uint16_t zs_l_u16;
+typedef uint32_t zs_v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) zs_v4u zs_g_u4;
+typedef __attribute__((address_space(3))) zs_v4u zs_l_u4;
+static __device__ __forceinline__ zs_v4u zs_v4(uint4 a) { return zs_v4u{a.x, a.y, a.z, a.w}; }
 struct zs_sg_out {
-  uint16_t* dst;
-  uint16_t* ring;
+  zs_g_u16* dst;
+  zs_l_u16* ring;
   uint32_t P, F;
   bool ovf;  // a reservation the ring could not hold (guarded statically; a run that sees it bails the member)
   __device__ __forceinline__ void put(uint32_t v) {
@@ -1230,7 +1241,7 @@ struct zs_sg_out {
   }
   __device__ __forceinline__ void flush() {
     while (F + 8u <= P) {
-      *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & (ZS_SG_RING - 1u)));
+      *reinterpret_cast<zs_g_u4*>(dst + F) = *reinterpret_cast<const zs_l_u4*>(ring + (F & (ZS_SG_RING - 1u)));
       F += 8u;
     }
   }
@@ -1254,7 +1265,7 @@ struct zs_sg_out {
 #endif
   __device__ __forceinline__ void finish() {
     flush();
-    if (F < P) *reinterpret_cast<uint4*>(dst + F) = *reinterpret_cast<const uint4*>(ring + (F & (ZS_SG_RING - 1u)));
+    if (F < P) *reinterpret_cast<zs_g_u4*>(dst + F) = *reinterpret_cast<const zs_l_u4*>(ring + (F & (ZS_SG_RING - 1u)));
   }
   // A long run of n >= ZS_SG_BULK values given by their 8-value units: one by one up to an
   // 8-aligned position, then whole 16-byte units straight to HBM from registers (no LDS
@@ -1270,11 +1281,11 @@ struct zs_sg_out {
     }
     flush();  // F = P
     const uint32_t e8 = end & ~7u;
-    for (; P < e8; P += 8u) *reinterpret_cast<uint4*>(dst + P) = unit(P);
+    for (; P < e8; P += 8u) *reinterpret_cast<zs_g_u4*>(dst + P) = zs_v4(unit(P));
     F = P;
 #pragma unroll
     for (uint32_t k = 0; k < ZS_SG_RING; k += 8u)
-      *reinterpret_cast<uint4*>(ring + ((P - ZS_SG_RING + k) & (ZS_SG_RING - 1u))) = unit(P - ZS_SG_RING + k);
+      *reinterpret_cast<zs_l_u4*>(ring + ((P - ZS_SG_RING + k) & (ZS_SG_RING - 1u))) = zs_v4(unit(P - ZS_SG_RING + k));
     while (P < end) {
       room(1);
       put(one(P));
@@ -1283,11 +1294,12 @@ struct zs_sg_out {
 };
 #define ZS_SG_BULK 64u  // (>= ZS_SG_RING + 15: the ring's values after the aligned units all belong to the run)
 static_assert(ZS_SG_BULK >= ZS_SG_RING + 15u, "bulk runs too short for the ring refill");
-static __device__ __forceinline__ uint32_t zs_sg_pick8(const uint32_t v[8], uint32_t i) {
-  uint32_t x = v[0];
-#pragma unroll
-  for (uint32_t t = 1; t < 8; t++) x = t == i ? v[t] : x;
-  return x;
+// value i (runtime, < 8) of eight u16 values packed two per word: bit selects, not an
+// indexed array (a select chain on i the compiler turns into a scratch-memory table)
+static __device__ __forceinline__ uint32_t zs_sg_pick8(const uint32_t (&w)[4], uint32_t i) {
+  const uint32_t a = (i & 2u) ? w[1] : w[0], b = (i & 2u) ? w[3] : w[2];
+  const uint32_t c = (i & 4u) ? b : a;
+  return (i & 1u) ? c >> 16 : c & 0xffffu;
 }
 
 // n values from piece position x0 (negative: markers for the history before
@@ -1345,21 +1357,24 @@ static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint
       // d = 1, 2, 4: every 8-aligned unit holds the same values (runs: the deflate64 fixtures'
       // 257-byte distance-1 copies)
       const uint32_t P0 = W.P, dm = (uint32_t)d - 1u, rb = (0u - P0) & dm;
+      const uint32_t pv[4] = {v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16};
       uint32_t u[8];
 #pragma unroll
-      for (uint32_t k = 0; k < 8; k++) u[k] = zs_sg_pick8(v, (rb + k) & dm);
+      for (uint32_t k = 0; k < 8; k++) u[k] = zs_sg_pick8(pv, (rb + k) & dm);
       const uint4 w = make_uint4(u[0] | u[1] << 16, u[2] | u[3] << 16, u[4] | u[5] << 16, u[6] | u[7] << 16);
       W.run(
-          n, [w](uint32_t) { return w; }, [&v, P0, dm](uint32_t x) { return zs_sg_pick8(v, (x - P0) & dm); });
+          n, [w](uint32_t) { return w; },
+          [v0 = v[0], v1 = v[1], v2 = v[2], v3 = v[3], P0, dm](uint32_t x) {  // (by value: v stays in registers)
+            const uint32_t i = (x - P0) & dm;  // d = 1, 2, 4: i < 4
+            return i == 0 ? v0 : i == 1 ? v1 : i == 2 ? v2 : v3;
+          });
       return true;
     }
     uint32_t j = 0;
     W.room(16);
+    const uint32_t pv[4] = {v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16};
     for (uint32_t i = 0; i < first; i++) {
-      uint32_t x = v[0];
-#pragma unroll
-      for (uint32_t t = 1; t < 8; t++) x = t == j ? v[t] : x;
-      W.put(x);
+      W.put(zs_sg_pick8(pv, j));
       j = j + 1 == (uint32_t)d ? 0u : j + 1;
     }
     const uint32_t rest = n - first;
@@ -1444,8 +1459,8 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
   zs_sg_init(G, in + in_off[s], in_len[s]);
   zs_sg_seek(G, p.start);
   zs_sg_out W;
-  W.dst = scratch + sbase[m] + p.off;
-  W.ring = ring[lane];
+  W.dst = (zs_g_u16*)(scratch + sbase[m] + p.off);
+  W.ring = (zs_l_u16*)ring[lane];
   W.P = 0;
   W.F = 0;
   W.ovf = false;

@@ -46,10 +46,14 @@
 // words holding it, sh: its offset in the first, last: the last word's index).
 // The candidate's bits: the aligned words holding the member (w4; sh: its
 // offset in the first, last: the last word's index, reads clamped to it).
+// (pointers typed by address space: generic ones let the compiler fold word()'s two loads into one
+// flat load of a selected pointer)
+typedef const __attribute__((address_space(1))) uint32_t zs_gc_u32;
+typedef const __attribute__((address_space(3))) uint32_t zs_lc_u32;
 struct zs_hdr_src {
-  const uint32_t* w4;
+  zs_gc_u32* w4;
   uint32_t sh, last;
-  const uint32_t* lw;  // a window of the aligned words staged in LDS: [lq0, lq0 + ln)
+  zs_lc_u32* lw;  // a window of the aligned words staged in LDS: [lq0, lq0 + ln)
   uint32_t lq0, ln;
   __device__ __forceinline__ uint32_t word(uint32_t q) const {
     return q - lq0 < ln ? lw[q - lq0] : w4[min(q, last)];
@@ -71,7 +75,7 @@ struct zs_hdr_src {
 // (kBlPos: each code-length symbol's place in the header's order, ZS_BL_ORDER inverted)
 static constexpr uint8_t kBlPos[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
 
-static __device__ bool zs_split_header_rest(const zs_hdr_src& S, uint64_t bit, uint64_t nbits, uint64_t a,
+static __device__ bool zs_split_header_rest(const zs_hdr_src S, uint64_t bit, uint64_t nbits, uint64_t a,
                                             uint64_t b) {
   const uint32_t nlen = (uint32_t)((a >> 3) & 31u) + 257, ndist = (uint32_t)((a >> 8) & 31u) + 1;
   const uint32_t ncode = (uint32_t)((a >> 13) & 15u) + 4u;
@@ -246,9 +250,9 @@ __global__ __launch_bounds__(256) void zs_k_split_find(const uint8_t* __restrict
   const bool d64 = wbits == -16;
   zs_hdr_src S;
   S.sh = (uint32_t)((uintptr_t)src & 3u);
-  S.w4 = reinterpret_cast<const uint32_t*>(src - S.sh);
+  S.w4 = (zs_gc_u32*)(src - S.sh);
   S.last = (S.sh + n - 1u) >> 2;
-  S.lw = stage;
+  S.lw = (zs_lc_u32*)stage;
   S.ln = 0;
   S.lq0 = 0;
   const uint64_t w_lo = lo >> 5, w_hi = (hi + 31u) >> 5;
