@@ -1311,8 +1311,11 @@ static int seg_launch(zs_ctx* c, hipStream_t st, int wbits, uint32_t n, const ui
   for (uint32_t k = 0; k < ng; k++) gbits += 8ull * in_len[c->hglist[k]];
   const bool large = gbits >= 65536ull * 8 * ng;  // members of 64 KiB of input or more on average
   const bool w2k = c->seg_wide && nwalk <= 3u * c->ncu && large;
-  auto walk = d64 ? (w2k ? zs_k_seg_walk<true, 2048u> : zs_k_seg_walk<true, 1024u>)
-                  : (w2k ? zs_k_seg_walk<false, 2048u> : zs_k_seg_walk<false, 1024u>);
+  // (large deflate members: the instance whose lanes decode the stretch between their sync windows
+  // without the windows' bookkeeping)
+  auto walk = d64 ? (w2k ? zs_k_seg_walk<true, 2048u, false> : zs_k_seg_walk<true, 1024u, false>)
+                  : (w2k ? zs_k_seg_walk<false, 2048u, true>
+                         : large ? zs_k_seg_walk<false, 1024u, true> : zs_k_seg_walk<false, 1024u, false>);
   // bits per lane: large members (4,096 x 256 KiB: 17.2 -> 15.9 ms, its 512-member shard 3.70 -> 3.57) walk fewer,
   // wider spans; 64 KiB members keep 2048 (the 1,024-member gunzip shard: 2.11 vs 2.45 ms, the decode's pieces
   // too few to fill the chip) -- tools/segbits_ab.sh

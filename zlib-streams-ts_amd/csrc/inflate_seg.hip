@@ -354,7 +354,7 @@ struct zs_sg_walk_lds {
 #define ZS_SG_K_NONE 0u
 #define ZS_SG_K_BEND 2u
 #define ZS_SG_K_CONT 4u
-template <bool D64, uint32_t W>
+template <bool D64, uint32_t W, bool ST>
 static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, uint32_t n, uint32_t sym0, uint32_t pe0,
                                       uint32_t nl, uint32_t S, uint32_t lbits, uint32_t dbits, uint32_t dofs,
                                       zs_seg_lane* __restrict__ recs, uint32_t& send, bool& bad_out, bool split) {
@@ -429,7 +429,68 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
     }
     acc |= 1u << bit;
   };
+  bool nofast = false;  // the stretch below stopped at this lane's end-of-block / invalid code
+  // (ST: the walk instance for large members -- the 4,096 x 256 KiB walk 5.96 -> 5.49 ms; C5-i's 64 KiB
+  // members, 2,048-bit spans, lose 4 % with this code in the loop at all: their instance has none)
+  constexpr bool stretches = ST;
   while (pos < lim) {
+#if !(ZS_SEG_EXP & 32)
+    // The stretch between a lane's two windows: no marks, no checkpoints and --
+    // 64 bits (more than a symbol) short of the tail window, the split point and
+    // the next sub-chunk boundary -- no events.  When EVERY running lane is in its
+    // stretch, the wave decodes literals and copies without that bookkeeping until
+    // one of them leaves it (an end-of-block or invalid code seeks back and leaves
+    // that symbol to the loop below).  The extra bits need no refill: >= 32 bits
+    // are held before a code of <= 15 bits and <= 16 extra bits.
+    if (stretches && __builtin_amdgcn_ballot_w64(left_own && !nofast) == __builtin_amdgcn_read_exec()) {
+      uint32_t bdn = (pos + 262143u) & ~262143u;
+      if (bdn == 0) bdn = 262144u;
+      uint32_t fe = min(min(qn, lim), bdn);
+      if (mid_sb == ZS_SEG_NONE) fe = min(fe, qm);
+      const bool in = fe > pos + 64u;
+      const uint64_t run = __builtin_amdgcn_read_exec();
+      if (__builtin_amdgcn_ballot_w64(in) == run) {
+        const uint32_t fend = fe - 64u;
+        bool stay;
+        do {
+          if (G.bits < 32) zs_sg_fill(G);
+          uint32_t nb;
+          zcode here = zs_sg_code(G, lt, lmask, nb);
+          uint32_t op = C_OP(here), len = 1u;
+          bool stop = false;
+          if (op) {
+            if (op & 96u) {  // end of block / invalid
+              stop = true;
+            } else {
+              const uint32_t e1 = op & emask;
+              len = C_VAL(here) + ((uint32_t)G.hold & ((1u << e1) - 1u));
+              zs_sg_drop(G, e1);
+              if (G.bits < 32) zs_sg_fill(G);
+              here = zs_sg_code(G, dt, dmask, nb);
+              op = C_OP(here);
+              stop = (op & 64u) != 0;  // invalid distance
+              zs_sg_drop(G, op & 15u);
+            }
+          }
+          if (stop) {
+            zs_sg_seek(G, pos);
+            nofast = true;
+          } else {
+#if ZS_SEG_EXP & 2
+            dbg_sym++;
+#endif
+            cum += len;
+            last_len = len;
+            pos = zs_sg_bitpos(G);
+          }
+          stay = !stop && pos < fend;
+        } while (__builtin_amdgcn_ballot_w64(stay) == run);
+        pe = pos;
+        continue;
+      }
+    }
+    nofast = false;
+#endif
     const uint32_t off = pos - q, toff = pos - qn;
     if (pos >= qm && mid_sb == ZS_SEG_NONE) {
       mid_sb = pos;
@@ -688,7 +749,7 @@ static __device__ uint32_t zs_sg_span(zs_sg_walk_lds<W>& L, const uint8_t* src, 
   return kind;
 }
 
-template <bool D64, uint32_t W>
+template <bool D64, uint32_t W, bool ST>
 __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                     const uint32_t* __restrict__ in_len,
                                                     const uint32_t* __restrict__ list, uint32_t n_list,
@@ -871,7 +932,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
       const uint32_t nl = max(1u, min(ZS_SEG_LANES, (nbits - cur + S - 1u) / S));
       uint32_t send = 0;
       bool sbad = false;
-      const uint32_t k = zs_sg_span<D64, W>(L, src, n, cur, pe0, nl, S, lbits, dbits, dofs,
+      const uint32_t k = zs_sg_span<D64, W, ST>(L, src, n, cur, pe0, nl, S, lbits, dbits, dofs,
                                          lanes + (size_t)b * ZS_SEG_LANES, send, sbad, split != 0);
 #if ZS_SEG_EXP & 2
       wd[1] += L.dbg[0];
@@ -1655,15 +1716,16 @@ __global__ __launch_bounds__(T) void zs_k_seg_resolve(const uint32_t* __restrict
   }
 }
 
-#define ZS_SEG_WALK_INST(D, W)                                                                                     \
-  template __global__ void zs_k_seg_walk<D, W>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,  \
+#define ZS_SEG_WALK_INST(D, W, ST)                                                                                 \
+  template __global__ void zs_k_seg_walk<D, W, ST>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*,  \
                                                uint32_t, const uint32_t*, uint32_t, int, const uint64_t*,          \
                                                const uint32_t*, zs_seg_blk*, zs_seg_lane*, zcode*, zs_seg_ent*,    \
                                                zs_seg_mem*, uint32_t*, uint32_t*, uint32_t, int);
-ZS_SEG_WALK_INST(false, 1024u)
-ZS_SEG_WALK_INST(true, 1024u)
-ZS_SEG_WALK_INST(false, 2048u)
-ZS_SEG_WALK_INST(true, 2048u)
+ZS_SEG_WALK_INST(false, 1024u, false)
+ZS_SEG_WALK_INST(false, 1024u, true)
+ZS_SEG_WALK_INST(true, 1024u, false)
+ZS_SEG_WALK_INST(false, 2048u, true)
+ZS_SEG_WALK_INST(true, 2048u, false)
 #define ZS_SEG_DEC_INST(D, W)                                                                                       \
   template __global__ void zs_k_seg_decode<D, W>(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, \
                                                  const uint32_t*, const uint32_t*, const zs_seg_blk*,              \

@@ -79,7 +79,8 @@ struct zs_seg_mem {
   uint32_t pad[2];
 };
 
-template <bool D64, uint32_t W>  // W: the sync window (1024, or 2048 for a batch of few large members)
+template <bool D64, uint32_t W, bool ST>  // W: the sync window (1024, or 2048 for a batch of few large members);
+                                          // ST: large members, the bookkeeping-free stretch (inflate_seg.hip)
 __global__ void zs_k_seg_walk(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint32_t* list,
                               uint32_t n_list, const uint32_t* big, uint32_t n_big, int wbits, const uint64_t* found,
                               const uint32_t* spb, zs_seg_blk* blk, zs_seg_lane* lanes, zcode* tcache,
