@@ -20,3 +20,7 @@ for d in "$SRC"/sq_*; do
   [ -f "$d/sq_summary.txt" ] && cp "$d/sq_summary.txt" "$DST/sq_summary_$t.txt"
 done
 ls "$DST"
+for f in smoke bench_2ranks_gloo_1gpu inflate_2ranks_gloo_1gpu; do
+  [ -f "$SRC/$f.log" ] && cp "$SRC/$f.log" "$DST/$f.log"
+done
+true
