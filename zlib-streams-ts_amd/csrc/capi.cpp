@@ -534,7 +534,7 @@ static int deflate_match(zs_ctx* c, hipStream_t st, const zs_level_cfg& cfg, uin
   if (c->match_sweep) {
     const uint32_t w0 = c->hwin0[a], nw = c->hwin0[e] - w0;
     // a window: counting sort by hash + lock-step sweep (deflate_sweep.hip)
-    (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<nw, 256, 0, st>>>(
+    (c->lane_order ? zs_k_bucket<true> : zs_k_bucket<false>)<<<nw, ZS_BK_THREADS, 0, st>>>(
         d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(), c->mres.as<uint2>());
     MARK("bucket");
     zs_k_sweep<<<nw, 1024, 0, st>>>(d_in, d_in_off, d_in_len, d_pos, d_segs + w0, c->prevd.as<uint16_t>(),

@@ -78,7 +78,8 @@ static __device__ __forceinline__ uint32_t sw_hash(uint32_t w) {  // SURVEY A1, 
 // equal hashes get slots in position order.  Pass 1 hashes input words held
 // in registers, pass 2 a 4 KiB LDS stage of the input.  Results of the
 // positions that are not inserted (the last two) are zeroed.
-#define ZS_BK_THREADS 256u
+#define ZS_BK_WPT (16384u / ZS_BK_THREADS)  // scan: count words per thread
+#define ZS_BK_PPL (ZS_BK_THREADS / 64u)     // scan: partial sums per lane of the wave-level scan
 #ifndef ZS_BK_PROF
 #define ZS_BK_PROF 0  // timing experiments: wall-clock per pass summed over workgroups (0 in the product)
 #endif
@@ -150,19 +151,19 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
   }
   __syncthreads();
   BK_MARK(0);
-  // exclusive scan: thread i owns words [64i, 64i + 64) (buckets 128i ...)
+  // exclusive scan: thread i owns words [WPT i, WPT i + WPT) (buckets 2 WPT i ...)
   {
     uint32_t sum = 0;
-    for (uint32_t j = 0; j < 64; j++) {
-      const uint32_t w = cnt[64 * tid + ((j + tid) & 63u)];  // rotated: threads hit different banks
+    for (uint32_t j = 0; j < ZS_BK_WPT; j++) {
+      const uint32_t w = cnt[ZS_BK_WPT * tid + ((j + tid) & (ZS_BK_WPT - 1u))];  // rotated: threads hit different banks
       sum += (w & 0xffffu) + (w >> 16);
     }
     part[tid] = sum;
     __syncthreads();
-    if (tid < 64) {  // scan of the 256 partial sums, one wave
-      uint32_t v[4], t = 0;
+    if (tid < 64) {  // scan of the partial sums, one wave
+      uint32_t v[ZS_BK_PPL], t = 0;
 #pragma unroll
-      for (int j = 0; j < 4; j++) { v[j] = part[4 * tid + j]; t += v[j]; }
+      for (uint32_t j = 0; j < ZS_BK_PPL; j++) { v[j] = part[ZS_BK_PPL * tid + j]; t += v[j]; }
       uint32_t x = t;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -171,16 +172,14 @@ __global__ __launch_bounds__(ZS_BK_THREADS) void zs_k_bucket(const uint8_t* __re
       }
       uint32_t run = x - t;
 #pragma unroll
-      for (int j = 0; j < 4; j++) { part[4 * tid + j] = run; run += v[j]; }
+      for (uint32_t j = 0; j < ZS_BK_PPL; j++) { part[ZS_BK_PPL * tid + j] = run; run += v[j]; }
     }
     __syncthreads();
     uint32_t run = part[tid];
-    for (uint32_t j = 0; j < 64; j++) {
-      const uint32_t i = 64 * tid + ((j + tid) & 63u);
-      (void)i;
-      const uint32_t w = cnt[64 * tid + j];
+    for (uint32_t j = 0; j < ZS_BK_WPT; j++) {
+      const uint32_t w = cnt[ZS_BK_WPT * tid + j];
       const uint32_t lo = w & 0xffffu;
-      cnt[64 * tid + j] = run | ((run + lo) << 16);
+      cnt[ZS_BK_WPT * tid + j] = run | ((run + lo) << 16);
       run += lo + (w >> 16);
     }
   }

@@ -50,6 +50,8 @@ struct zs_sweep_seg {
 #define ZS_SEG_FIRST 65520u  // own positions of a long stream's first window ...
 #define ZS_SEG_OWN 32752u    // ... and of its later ones, after a 32,768-position look-back (> MAX_DIST);
                              // multiples of 16: every window starts 16-byte aligned with its stream
+// zs_k_bucket's workgroup: wave 0 claims, the others scatter (a multiple of 64 dividing 16384: the scan's slices)
+#define ZS_BK_THREADS 512u
 template <bool ORD>
 __global__ void zs_k_bucket(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, const uint64_t* pos_base,
                             const zs_sweep_seg* segs, uint16_t* members, uint2* mres);
