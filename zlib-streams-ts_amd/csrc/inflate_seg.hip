@@ -137,7 +137,8 @@ static __device__ __forceinline__ void zs_sg_init(zs_sg_reader& R, const uint8_t
   R.last = (R.sh + n - 1u) >> 2;
 }
 // a code from a zlib table (second level included); nb: its bits
-static __device__ __forceinline__ zcode zs_sg_code(zs_sg_reader& R, const zcode* t, uint32_t mask, uint32_t& nb) {
+template <typename TT>
+static __device__ __forceinline__ zcode zs_sg_code(zs_sg_reader& R, const TT& t, uint32_t mask, uint32_t& nb) {
   zcode here = t[(uint32_t)R.hold & mask];
   uint32_t b = C_BITS(here);
   if (C_OP(here) && (C_OP(here) & 0xf0) == 0) {
@@ -158,8 +159,9 @@ struct zs_sg_sym {
   uint32_t kind, val, len;  // literal: val; copy: len, val = distance
   uint32_t l1, e1, l2, e2;  // the bit fields (zs_refcalls)
 };
+template <typename TD>
 static __device__ __forceinline__ zs_sg_sym zs_sg_decode(zs_sg_reader& R, const zcode* lt, uint32_t lmask,
-                                                        const zcode* dt, uint32_t dmask, uint32_t emask) {
+                                                        const TD& dt, uint32_t dmask, uint32_t emask) {
   zs_sg_sym y = {ZS_SG_BAD, 0u, 0u, 0u, 0u, 0u, 0u};
   if (R.bits < 32) zs_sg_fill(R);
   zcode here = zs_sg_code(R, lt, lmask, y.l1);
@@ -889,6 +891,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
         Bk.end = cur;
         Bk.lbits = Bk.dbits = Bk.dofs = 0;
         Bk.tab = ZS_SEG_NONE;
+        Bk.pad[0] = 0;
         Bk.nl = 1;
         Bk.S = 0;
         Bk.next = ZS_SEG_NONE;
@@ -952,6 +955,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_walk(const uint8_t* __restrict__ 
         Bk.dbits = dbits;
         Bk.dofs = dofs;
         Bk.tab = tab;
+        Bk.pad[0] = ntab;  // (the decode's table size)
         Bk.nl = nl;
         Bk.S = S;
         Bk.next = ZS_SEG_NONE;
@@ -1274,6 +1278,22 @@ __global__ __launch_bounds__(64) void zs_k_seg_plan(const uint8_t* __restrict__ 
 }
 
 // ----------------------------------------------------------------- decode
+// The decode's LDS table: the first ZS_SEG_TAB_DEC entries of a block's tables (inflate_table's
+// sizes; text blocks use 600-900), not the ENOUGH bound (1,444): 4 instead of 5.8 KB of LDS per wave,
+// 20 waves per CU instead of 16.  The literal/length table always fits (<= 852 entries); distance
+// entries past the bound are read from the walk's copy in HBM (zs_sg_dtab)
+#ifndef ZS_SEG_TAB_DEC
+#define ZS_SEG_TAB_DEC 1024u
+#endif
+static_assert(ZS_SEG_TAB_DEC > ENOUGH_LENS, "the literal/length table must fit the decode's LDS table");
+typedef const __attribute__((address_space(3))) zcode zs_l_zc;
+typedef const __attribute__((address_space(1))) zcode zs_g_zc;
+struct zs_sg_dtab {  // a distance table: entries below lim in LDS, the rest in HBM
+  zs_l_zc* l;
+  zs_g_zc* g;
+  uint32_t lim;
+  __device__ __forceinline__ zcode operator[](uint32_t i) const { return i < lim ? l[i] : g[i]; }
+};
 #ifndef ZS_SG_RING
 #define ZS_SG_RING 32u  // u16 values of a lane's LDS output ring (a power of two; 32 vs 64: 10 instead of 14 KB of
                         // LDS per wave, C5-i 11.0 -> 10.2 ms)
@@ -1474,7 +1494,7 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
                                                       const zcode* __restrict__ tcache, zs_seg_mem* __restrict__ mem,
                                                       const uint64_t* __restrict__ sbase,
                                                       uint16_t* __restrict__ scratch) {
-  __shared__ zcode codes[ZS_SEG_TAB];
+  __shared__ zcode codes[ZS_SEG_TAB_DEC];
   __shared__ __attribute__((aligned(16))) uint16_t ring[ZS_SEG_LANES][ZS_SG_RING];
   const uint32_t lane = threadIdx.x;
   const uint32_t ns = *nspan;
@@ -1495,9 +1515,9 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
     }
     continue;
   }
-  const uint32_t ntab = ZS_SEG_TAB, tab = zs_u(Bk.tab);
+  const uint32_t ntab = zs_u(Bk.pad[0]), tab = zs_u(Bk.tab);
   __syncthreads();  // (the previous span's tables are no longer read)
-  for (uint32_t i = lane; i < ntab; i += 64) codes[i] = tcache[(size_t)tab * ZS_SEG_TAB + i];
+  for (uint32_t i = lane; i < min(ntab, ZS_SEG_TAB_DEC); i += 64) codes[i] = tcache[(size_t)tab * ZS_SEG_TAB + i];
   __syncthreads();
   const zs_seg_lane& p = lanes[(size_t)b * ZS_SEG_LANES + lane];
 #if ZS_SEG_EXP & 1
@@ -1515,7 +1535,9 @@ __global__ __launch_bounds__(64) void zs_k_seg_decode(const uint8_t* __restrict_
   const uint32_t s = list[m];
   const uint32_t lmask = (1u << Bk.lbits) - 1u, dmask = (1u << Bk.dbits) - 1u, emask = D64 ? 31u : 15u;
   const zcode* lt = codes;
-  const zcode* dt = codes + Bk.dofs;
+  const uint32_t dofs = zs_u(Bk.dofs);
+  const zs_sg_dtab dt = {(const zs_l_zc*)(codes + dofs), (const zs_g_zc*)(tcache + (size_t)tab * ZS_SEG_TAB + dofs),
+                         ZS_SEG_TAB_DEC - dofs};
   zs_sg_reader G;
   zs_sg_init(G, in + in_off[s], in_len[s]);
   zs_sg_seek(G, p.start);
