@@ -1373,7 +1373,9 @@ struct zs_sg_out {
     }
   }
 };
+#ifndef ZS_SG_BULK
 #define ZS_SG_BULK 64u  // (>= ZS_SG_RING + 15: the ring's values after the aligned units all belong to the run)
+#endif
 static_assert(ZS_SG_BULK >= ZS_SG_RING + 15u, "bulk runs too short for the ring refill");
 // value i (runtime, < 8) of eight u16 values packed two per word: bit selects, not an
 // indexed array (a select chain on i the compiler turns into a scratch-memory table)
