@@ -566,9 +566,20 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         SW_STAT(3, 1);
         if (gm >= long_m && (lthr >> 3) < nice) {
           uint32_t gl = 0;
+#if ZS_SW_EXP & 1024
 #pragma unroll
           for (uint32_t u = 0; u < 8; u++) {
             if (u < cnt && sc[u] >= long_m) {
+#else
+          // the group's long steps as a mask, visited one by one (one to three per lane, typically)
+          uint32_t lm = 0;
+#pragma unroll
+          for (uint32_t u = 0; u < 8; u++) lm |= (u < cnt && sc[u] >= long_m) ? 1u << u : 0u;
+          while (lm) {
+            const uint32_t u = (uint32_t)__builtin_ctz(lm);
+            lm &= lm - 1u;
+            {
+#endif
               // the next four bytes: A7 records carry them (c), else from the window
               const uint32_t x = (A7 ? R->c[base - t0 - u]
                                      : sw_word(win, (R->key[base - t0 - u] & 0xffffu) + Sig::EXT)) ^ own_ext;
