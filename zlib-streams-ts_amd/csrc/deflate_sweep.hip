@@ -537,8 +537,10 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
 
+    // the best short candidate: its group's maximum score (matched bits, 7 - its place in the group) and the
+    // group's first step (0: none) -- the step itself, t0 + 7 - (score & 7), is formed once at the end
     uint32_t thr = Sig::THR0, thr_s = Sig::THR0;
-    uint32_t bt = 0, bt_s = 0;                  // step of the best short candidate (0: none)
+    uint32_t bt = 0, bt_s = 0;
     // best long candidate: its length (capped at nice) as lthr = len << 3 | 7, its step
     uint32_t lthr = 7u, lbt = 0, lthr_s = 7u, lbt_s = 0;
     const uint32_t own_ext = sw_word(win, p + Sig::EXT);  // the lane's bytes past a full signature
@@ -555,9 +557,15 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     // and ties with every later one, so it stays first.
     auto fold = [&](uint32_t gm, uint32_t t0, const uint32_t* sc, uint32_t cnt, uint32_t base)
         __attribute__((always_inline)) {
+#if ZS_SW_EXP & 4096  // (A/B: the step formed per group)
       const bool up = gm > thr;
       thr = max(thr, gm | 7u);
       bt = up ? t0 + 7u - (gm & 7u) : bt;
+#else
+      const bool up = gm > (thr | 7u);  // longer than the best so far
+      thr = up ? gm : thr;
+      bt = up ? t0 : bt;
+#endif
 #if ZS_SW_EXP & 32
       if (0) {
 #else
@@ -761,13 +769,18 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
           Ls = bs >> 16;
           Ds = Ls > 2u ? p - (uint32_t)mem[k - (int)(0xffffu - (bs & 0xffffu))] : 0u;
         } else {
+#if ZS_SW_EXP & 4096
+          const uint32_t tb = bt, tb_s = bt_s;
+#else
+          const uint32_t tb = bt + 7u - (thr & 7u), tb_s = bt_s + 7u - (thr_s & 7u);  // the steps
+#endif
           if (bt) {
             L = Sig::len(thr >> 3);
-            D = p - member(k - (int)bt);
+            D = p - member(k - (int)tb);
           }
           if (bt_s) {
             Ls = Sig::len(thr_s >> 3);
-            Ds = bt_s == bt ? D : p - member(k - (int)bt_s);
+            Ds = tb_s == tb ? D : p - member(k - (int)tb_s);
           }
           // long candidates beat every short one; a nice one's length was capped: measure it
           auto long_of = [&](uint32_t lt, uint32_t t, uint32_t& len, uint32_t& dist) {
