@@ -674,20 +674,50 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         gm = max3(sc[0], sc[1], max(sc[2], sc[3]));
       fold(live ? gm : 0u, t0, sc, N, base);
     };
-    auto group_masked = [&](uint32_t base, uint32_t t0, uint32_t t1) __attribute__((always_inline)) {
+    // (like group_fast: one address, immediate offsets, every load issued before the first is waited for)
+    auto group_masked = [&](uint32_t base, uint32_t t0, auto G) __attribute__((always_inline)) {
+      constexpr uint32_t N = decltype(G)::value;
+#if ZS_SW_EXP & 8192  // (A/B: step by step, an address and a wait each)
       uint32_t sc[8];
       uint64_t lm = 0, last = 0;
 #pragma unroll
       for (uint32_t u = 0; u < 8; u++) {
         sc[u] = 0u;
-        if (u <= t1 - t0) {
+        if (u < N) {
           sc[u] = mstep(base - t0 - u, u, lm);
           last = lm;
         }
       }
       alive_m = sw_uniform(last);  // the lanes live at the group's last step
-      fold(max(max3(sc[0], sc[1], sc[2]), max3(sc[3], sc[4], max3(sc[5], sc[6], sc[7]))), t0, sc, t1 - t0 + 1u,
-           base);
+      fold(max(max3(sc[0], sc[1], sc[2]), max3(sc[3], sc[4], max3(sc[5], sc[6], sc[7]))), t0, sc, N, base);
+#else
+      const uint32_t lo = base - t0 - (N - 1u);
+      const uint2* const A = R->ab + lo;
+      const uint32_t* const C = R->c + lo;
+      const uint32_t* const K = R->key + lo;
+      uint32_t sc[N], key[N];
+      uint2 ab[N];
+#pragma unroll
+      for (uint32_t u = 0; u < N; u++) {
+        key[u] = K[N - 1u - u];
+        ab[u] = A[N - 1u - u];
+      }
+      uint64_t lm = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < N; u++) {
+        asm("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(lm) : "v"(key[u]), "v"(klim));
+        lm &= alive_m;
+        const uint32_t v = score(S.mbits(ab[u].x, ab[u].y, A7 ? 0u : C[N - 1u - u]), u);
+        asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(sc[u]) : "v"(v), "s"(lm));
+      }
+      alive_m = sw_uniform(lm);  // the lanes live at the group's last step
+      uint32_t gm;
+      if constexpr (N == 8)
+        gm = max(max3(sc[0], sc[1], sc[2]), max3(sc[3], sc[4], max3(sc[5], sc[6], sc[7])));
+      else
+        gm = max3(sc[0], sc[1], max(sc[2], sc[3]));
+      fold(gm, t0, sc, N, base);
+#endif
     };
     using G8 = std::integral_constant<uint32_t, 8>;
     using G4 = std::integral_constant<uint32_t, 4>;
@@ -715,7 +745,8 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         } else {
           SW_STAT(2, 1);
           SW_STAT(4, t1 - t0 + 1u);
-          group_masked(base, t0, t1);
+          if (t1 - t0 == 7u) group_masked(base, t0, G8{});
+          else group_masked(base, t0, G4{});
         }
         snap(t1);  // (every lane: one whose chain ended has its final best already)
         t0 = t1 + 1u;
