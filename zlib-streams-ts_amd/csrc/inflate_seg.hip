@@ -1300,6 +1300,7 @@ struct zs_sg_dtab {  // a distance table: entries below lim in LDS, the rest in 
 #endif
 // room(k) flushes whole 8-value units: up to 7 values stay, so k + 7 must fit (the largest k is 16)
 static_assert(ZS_SG_RING >= 16u + 7u && (ZS_SG_RING & (ZS_SG_RING - 1u)) == 0, "decode ring too small");
+static_assert(ZS_SG_RING > 28u, "a short-period copy reads up to 2 x 14 values back from the ring (near)");
 // One lane's u16 output (bytes, or markers 255 + k: the value k positions
 // before the piece): a ZS_SG_RING-value LDS ring, whole 16-byte units to HBM (the
 // piece's scratch is 16-byte aligned and padded, so no unit is shared).
@@ -1344,6 +1345,28 @@ struct zs_sg_out {
     return x + ZS_SG_RING >= P ? ring[x & (ZS_SG_RING - 1u)] : dst[x];
   }
 #endif
+  // a value of the last ZS_SG_RING (x + ZS_SG_RING >= P), from the ring
+  __device__ __forceinline__ uint32_t near(uint32_t x) const { return ring[x & (ZS_SG_RING - 1u)]; }
+  // the eight values at x .. x + 7 (< P): all stored, all in the ring, or across the two.  (Element
+  // by element, each value's ring-or-HBM branch made the compiler wait for every load on its own: eight
+  // round trips to HBM for a far copy's round instead of one.)
+  __device__ __forceinline__ void get8(uint32_t x, uint32_t (&v)[8]) {
+#if !(ZS_SEG_EXP & 1)
+    if (x + 7u + ZS_SG_RING < P) {
+      const zs_g_u16* const d = dst + x;  // (one address, immediate offsets)
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) v[j] = d[j];
+      return;
+    }
+    if (x + ZS_SG_RING >= P) {
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) v[j] = ring[(x + j) & (ZS_SG_RING - 1u)];
+      return;
+    }
+#endif
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) v[j] = get(x + j);
+  }
   __device__ __forceinline__ void finish() {
     flush();
     if (F < P) *reinterpret_cast<zs_g_u4*>(dst + F) = *reinterpret_cast<const zs_l_u4*>(ring + (F & (ZS_SG_RING - 1u)));
@@ -1420,8 +1443,7 @@ static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint
     for (uint32_t i = 0; i < n; i += 8) {
       W.room(8);
       uint32_t v[8];
-#pragma unroll
-      for (uint32_t j = 0; j < 8; j++) v[j] = W.get((uint32_t)x0 + i + j);
+      W.get8((uint32_t)x0 + i, v);
       const uint32_t k = min(8u, n - i);
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++)
@@ -1435,7 +1457,7 @@ static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint
     const uint32_t first = min(n, dd);
     uint32_t v[8];
 #pragma unroll
-    for (uint32_t j = 0; j < 8; j++) v[j] = (int32_t)j < d ? W.get((uint32_t)x0 + j) : 0u;
+    for (uint32_t j = 0; j < 8; j++) v[j] = (int32_t)j < d ? W.near((uint32_t)x0 + j) : 0u;  // (d < 8 back)
     if ((d & (d - 1)) == 0 && n >= ZS_SG_BULK) {
       // d = 1, 2, 4: every 8-aligned unit holds the same values (runs: the deflate64 fixtures'
       // 257-byte distance-1 copies)
@@ -1466,7 +1488,7 @@ static __device__ __forceinline__ bool zs_sg_copy(zs_sg_out& W, int32_t x0, uint
       W.room(8);
       uint32_t u[8];
 #pragma unroll
-      for (uint32_t k = 0; k < 8; k++) u[k] = W.get(xs + i + k);
+      for (uint32_t k = 0; k < 8; k++) u[k] = W.near(xs + i + k);  // (at most 2 dd <= 28 back)
       const uint32_t k8 = min(8u, rest - i);
 #pragma unroll
       for (uint32_t k = 0; k < 8; k++)
