@@ -1703,6 +1703,12 @@ __global__ __launch_bounds__(T) void zs_k_seg_resolve(const uint32_t* __restrict
       j2 = 0;
     }
     const bool restage = k2 < np && k2 - tb >= ZS_SG_RES_PT;
+#if !(ZS_SEG_EXP & 64)
+    // this round's values first, then the next round's loads: they fly while the markers are looked up.
+    // (Issued first, the compiler waited for all of them before the first marker: vmcnt(0) on a value loaded
+    // a round earlier and copied across the loop.)
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+#endif
     if (k2 < np && !restage) load(tab[k2 - tb], j2, nxt);
     // this round's markers
     const uint32_t O = e.x;
