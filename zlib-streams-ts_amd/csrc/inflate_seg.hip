@@ -1687,7 +1687,7 @@ __global__ __launch_bounds__(T) void zs_k_seg_resolve(const uint32_t* __restrict
   // the current round (piece k from value i0) and its values
   uint32_t k = 0, i0 = 0;
   uint32_t cur[ZS_SG_RES_E], nxt[ZS_SG_RES_E];
-  auto load = [&](const uint4& e, uint32_t j0, uint32_t (&v)[ZS_SG_RES_E]) {
+  auto load = [&](const uint4 e, uint32_t j0, uint32_t (&v)[ZS_SG_RES_E]) {
 #pragma unroll
     for (uint32_t q = 0; q < ZS_SG_RES_E; q++) {
       const uint32_t i = j0 + q * ZS_SG_RES_T + t;
@@ -1710,8 +1710,10 @@ __global__ __launch_bounds__(T) void zs_k_seg_resolve(const uint32_t* __restrict
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
 #endif
     if (k2 < np && !restage) load(tab[k2 - tb], j2, nxt);
-    // this round's markers
     const uint32_t O = e.x;
+    // this round's markers.  (Read for all eight values together, a wave's stored words before any pick,
+    // the markers cost more except on 4,096 x 256 KiB: 12.90 -> 12.75 ms there, but C5-i 8.17 -> 8.32 ms and
+    // the 512-member shard 0.44 -> 0.58 ms; idle lanes' work and registers.)
 #pragma unroll
     for (uint32_t q = 0; q < ZS_SG_RES_E; q++) {
       const uint32_t i = i0 + q * ZS_SG_RES_T + t;
