@@ -726,6 +726,38 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
     // its last step runs unmasked with the exec mask of the live lanes;
     // otherwise masked.
     auto run = [&](uint32_t base, uint32_t ta, uint32_t tb) __attribute__((always_inline)) {
+#if !(ZS_SW_EXP & 16384)
+      // the next group's last key is read with this group's records: the fast-or-masked test waits on no load
+      auto last_of = [&](uint32_t t0) __attribute__((always_inline)) {
+        uint32_t t1 = t0 + 7u <= tb ? t0 + 7u : t0 + 3u;
+        if (t0 <= budget_s && t1 > budget_s) t1 = budget_s;
+        return t1;
+      };
+      if (ta > tb) return;
+      uint32_t t0 = ta, t1 = last_of(ta);
+      uint32_t kl = R->key[base - t1];
+      while (alive_m) {
+        const bool mine = ((alive_m >> lane) & 1u) != 0;
+        const uint64_t last_live = __builtin_amdgcn_ballot_w64(mine && kl > klim);
+        const uint32_t n0 = t1 + 1u, n1 = n0 <= tb ? last_of(n0) : t1;
+        kl = R->key[base - n1];
+        if (last_live == alive_m) {
+          SW_STAT(1, 1);
+          SW_STAT(4, t1 - t0 + 1u);
+          if (t1 - t0 == 7u) group_fast(base, t0, G8{}, mine);
+          else group_fast(base, t0, G4{}, mine);
+        } else {
+          SW_STAT(2, 1);
+          SW_STAT(4, t1 - t0 + 1u);
+          if (t1 - t0 == 7u) group_masked(base, t0, G8{});
+          else group_masked(base, t0, G4{});
+        }
+        snap(t1);
+        if (n0 > tb) break;
+        t0 = n0;
+        t1 = n1;
+      }
+#else
       for (uint32_t t0 = ta; t0 <= tb && alive_m;) {
         uint32_t t1 = t0 + 7u <= tb ? t0 + 7u : t0 + 3u;
         if (t0 <= budget_s && t1 > budget_s) t1 = budget_s;
@@ -751,6 +783,7 @@ static __device__ __forceinline__ void sw_body(const uint32_t* win, SwRing* R, u
         snap(t1);  // (every lane: one whose chain ended has its final best already)
         t0 = t1 + 1u;
       }
+#endif
     };
     for (uint32_t b = 0; sbud > 4u && alive_m; b++) {
       // block b = steps (64b, 64b + 64]: members k0 - 64b - 64 ... k0 - 64b + 62, i.e. the blocks b and b + 1 back
