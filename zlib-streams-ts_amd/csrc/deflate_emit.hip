@@ -618,11 +618,15 @@ __global__ void zs_k_layout(const uint32_t* __restrict__ blk_base, zs_block* __r
 
 // -------------------------------------------------------------------- emit
 #define ZS_EMIT_THREADS 256
-#define ZS_STAGE_WORDS 2048
-#define ZS_EMIT_PER_THREAD 4
+#define ZS_EMIT_PER_THREAD 8
+// the stage holds the block header, the dynamic tree header and one chunk's
+// bits (at most 15 + 5 + 15 + 13 = 48 per symbol) past the carried word
+#define ZS_STAGE_WORDS (ZS_HDR_WORDS + 2 + ZS_EMIT_THREADS * ZS_EMIT_PER_THREAD * 48 / 32)
+static_assert(ZS_EMIT_THREADS == 256, "zs_k_emit builds its 256-entry length table one entry per thread");
 
 static __device__ __forceinline__ uint32_t zs_block_scan(uint32_t v, uint32_t* tmp, uint32_t& total) {
-  // exclusive scan over the 256-thread workgroup
+  // exclusive scan over the 256-thread workgroup (one barrier: the caller's
+  // later barriers keep tmp from being rewritten while it is read)
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -635,7 +639,6 @@ static __device__ __forceinline__ uint32_t zs_block_scan(uint32_t v, uint32_t* t
   uint32_t pre = 0;
   for (uint32_t i = 0; i < wv; i++) pre += tmp[i];
   total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
-  __syncthreads();
   return pre + x - v;
 }
 
@@ -654,6 +657,9 @@ __global__ __launch_bounds__(ZS_EMIT_THREADS) void zs_k_emit(
     uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off, int wrap) {
   __shared__ uint32_t stage[ZS_STAGE_WORDS + 4];
   __shared__ uint32_t tbl[ZS_L_CODES + ZS_D_CODES];
+  __shared__ uint32_t ltab[256];
+  __shared__ uint2 dt[ZS_D_CODES];
+  __shared__ uint8_t dcode[512];
   __shared__ uint32_t scan_tmp[4];
   const int s = blockIdx.y;
   const uint32_t b = blockIdx.x;
@@ -697,14 +703,46 @@ __global__ __launch_bounds__(ZS_EMIT_THREADS) void zs_k_emit(
     return;
   }
 
-  // Huffman-coded block
+  // Huffman-coded block.  The thread's symbols of the first chunk are loaded
+  // before the tables are set up, and each chunk's loads are issued before the
+  // previous chunk is coded (PT consecutive symbols per thread).
+  constexpr uint32_t PT = ZS_EMIT_PER_THREAD, chunk = ZS_EMIT_THREADS * PT;
+  const uint32_t* sy = syms + pos_base[s] + s + blk.sym_start;
+  const uint32_t nsym = blk.sym_count;
+  uint32_t nx[PT];
+  auto fetch = [&](uint32_t c0) __attribute__((always_inline)) {
+#pragma unroll
+    for (uint32_t k = 0; k < PT; k++) {
+      const uint32_t i = c0 + threadIdx.x * PT + k;
+      nx[k] = i < nsym ? sy[i] : 0u;
+    }
+  };
+  fetch(0);
   const uint32_t* ctab = codes + (size_t)bi * (ZS_L_CODES + ZS_D_CODES);
   for (uint32_t i = threadIdx.x; i < ZS_L_CODES + ZS_D_CODES; i += ZS_EMIT_THREADS) {
     if (blk.type == 1) tbl[i] = i < ZS_L_CODES ? ZS_STATIC_LTREE[i] : ZS_STATIC_DTREE[i - ZS_L_CODES];
     else tbl[i] = ctab[i];
   }
+  for (uint32_t i = threadIdx.x; i < 512; i += ZS_EMIT_THREADS) dcode[i] = ZS_DIST_CODE[i];
   for (uint32_t i = threadIdx.x; i < ZS_STAGE_WORDS + 4; i += ZS_EMIT_THREADS) stage[i] = 0;
   __syncthreads();
+  // a match's codes from LDS: ltab[lc] = the length code's bits and its extra
+  // bits (<= 20) | their count << 24; dt[dc] = the distance code's bits | its
+  // length << 16 | extra bits << 24, and the code's base distance
+  {
+    const uint32_t lc = threadIdx.x;  // ZS_EMIT_THREADS == 256 lengths
+    const uint32_t code = ZS_LENGTH_CODE[lc];
+    const uint32_t e1 = tbl[code + 257];
+    const uint32_t xl = (uint32_t)ZS_EXTRA_LBITS[code];
+    // code 285 (length 258) has no extra bits: lc - base must not leak (trees.ts:495-499)
+    const uint32_t xv = (lc - (uint32_t)ZS_BASE_LENGTH[code]) & ((1u << xl) - 1u);
+    ltab[lc] = ((e1 & 0xffffu) | (xv << (e1 >> 16))) | (((e1 >> 16) + xl) << 24);
+    if (lc < ZS_D_CODES) {
+      const uint32_t e2 = tbl[ZS_L_CODES + lc];
+      dt[lc] = make_uint2((e2 & 0xffffu) | ((e2 >> 16) << 16) | ((uint32_t)ZS_EXTRA_DBITS[lc] << 24),
+                          (uint32_t)ZS_BASE_DIST[lc]);
+    }
+  }
   uint64_t wbase = first_w;  // global word index of stage[0]
   uint64_t pos = off0;
   if (threadIdx.x == 0) zs_stage_or(stage, pos - wbase * 32, hdr3, 3);
@@ -720,41 +758,35 @@ __global__ __launch_bounds__(ZS_EMIT_THREADS) void zs_k_emit(
     pos += blk.hdr_bits;
   }
   __syncthreads();
-  const uint32_t* sy = syms + pos_base[s] + s + blk.sym_start;
-  const uint32_t nsym = blk.sym_count;
-  const uint32_t chunk = ZS_EMIT_THREADS * ZS_EMIT_PER_THREAD;
   for (uint32_t c0 = 0;; c0 += chunk) {
     const bool final_chunk = c0 + chunk >= nsym;
-    uint64_t v[ZS_EMIT_PER_THREAD];
-    uint32_t n[ZS_EMIT_PER_THREAD];
+    uint32_t x[PT];
+#pragma unroll
+    for (uint32_t k = 0; k < PT; k++) x[k] = nx[k];
+    if (!final_chunk) fetch(c0 + chunk);
+    uint64_t v[PT];
+    uint32_t n[PT];
     uint32_t tot = 0;
 #pragma unroll
-    for (int k = 0; k < ZS_EMIT_PER_THREAD; k++) {
-      const uint32_t i = c0 + threadIdx.x * ZS_EMIT_PER_THREAD + k;
+    for (uint32_t k = 0; k < PT; k++) {
+      const uint32_t i = c0 + threadIdx.x * PT + k;
       v[k] = 0;
       n[k] = 0;
       if (i < nsym) {
-        const uint32_t x = sy[i];
-        if (x & 0x80000000u) {  // compress_block (trees.ts:476-520)
-          const uint32_t lc = (x >> 16) & 0xff, dist = (x & 0xffffu) - 1;
-          const uint32_t code = ZS_LENGTH_CODE[lc];
-          const uint32_t e1 = tbl[code + 257];
-          uint32_t nb = e1 >> 16;
-          uint64_t acc = e1 & 0xffffu;
-          const uint32_t xl = (uint32_t)ZS_EXTRA_LBITS[code];
-          // code 285 (length 258) has no extra bits: lc - base must not leak (trees.ts:495-499)
-          acc |= (uint64_t)((lc - (uint32_t)ZS_BASE_LENGTH[code]) & ((1u << xl) - 1)) << nb;
-          nb += xl;
-          const uint32_t dc = dist < 256 ? ZS_DIST_CODE[dist] : ZS_DIST_CODE[256 + (dist >> 7)];
-          const uint32_t e2 = tbl[ZS_L_CODES + dc];
-          acc |= (uint64_t)(e2 & 0xffffu) << nb;
-          nb += e2 >> 16;
-          acc |= (uint64_t)(dist - (uint32_t)ZS_BASE_DIST[dc]) << nb;
-          nb += (uint32_t)ZS_EXTRA_DBITS[dc];
+        if (x[k] & 0x80000000u) {  // compress_block (trees.ts:476-520)
+          const uint32_t lc = (x[k] >> 16) & 0xff, dist = (x[k] & 0xffffu) - 1;
+          const uint32_t le = ltab[lc];
+          const uint2 de = dt[dcode[dist < 256 ? dist : 256 + (dist >> 7)]];
+          uint32_t nb = le >> 24;
+          uint64_t acc = le & 0xffffffu;
+          acc |= (uint64_t)(de.x & 0xffffu) << nb;
+          nb += (de.x >> 16) & 0xffu;
+          acc |= (uint64_t)(dist - de.y) << nb;
+          nb += de.x >> 24;
           v[k] = acc;
           n[k] = nb;
         } else {
-          const uint32_t e = tbl[x];
+          const uint32_t e = tbl[x[k]];
           v[k] = e & 0xffffu;
           n[k] = e >> 16;
         }
@@ -765,7 +797,7 @@ __global__ __launch_bounds__(ZS_EMIT_THREADS) void zs_k_emit(
     const uint32_t pre = zs_block_scan(tot, scan_tmp, total);
     uint64_t rel = pos - wbase * 32 + pre;
 #pragma unroll
-    for (int k = 0; k < ZS_EMIT_PER_THREAD; k++) {
+    for (uint32_t k = 0; k < PT; k++) {
       zs_stage_or(stage, rel, v[k], n[k]);
       rel += n[k];
     }
@@ -781,12 +813,13 @@ __global__ __launch_bounds__(ZS_EMIT_THREADS) void zs_k_emit(
     const uint32_t nw = (uint32_t)(done_w - wbase);
     for (uint32_t i = threadIdx.x; i < nw; i += ZS_EMIT_THREADS) put_word(wbase + i, stage[i]);
     if (final_chunk) break;
-    __syncthreads();
     const uint32_t carry = stage[nw];
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < ZS_STAGE_WORDS + 4; i += ZS_EMIT_THREADS) stage[i] = i == 0 ? carry : 0u;
+    // only words 0 .. nw were written (no bit lies past pos): clear those, the
+    // partial one moved to the front (the next scan's barrier orders it before
+    // the next chunk's ORs)
+    for (uint32_t i = threadIdx.x; i <= nw; i += ZS_EMIT_THREADS) stage[i] = i == 0 ? carry : 0u;
     wbase = done_w;
-    __syncthreads();
   }
 }
 
