@@ -429,6 +429,13 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   const uint32_t* sy = syms + pos_base[s] + s + blk.sym_start;
   for (uint32_t i = lane; i < ZS_L_CODES + ZS_D_CODES; i += 64) w.hist[i] = 0;
   for (uint32_t i = lane; i < ZS_HDR_WORDS; i += 64) w.hdr[i] = 0;
+  // the length and distance code maps in LDS (the histogram's lookups would
+  // otherwise be a memory round trip each, behind the symbol's own load)
+  uint8_t* const lcode8 = reinterpret_cast<uint8_t*>(w.hk);  // hk is free until the heap
+  uint8_t* const dcode8 = lcode8 + 256;
+  static_assert(sizeof(w.hk) >= 768, "code maps in hk");
+  for (uint32_t i = lane; i < 256; i += 64) lcode8[i] = ZS_LENGTH_CODE[i];
+  for (uint32_t i = lane; i < 512; i += 64) dcode8[i] = ZS_DIST_CODE[i];
   __syncthreads();
   // histogram (deflate/utils.ts:55-81 tallies, done in parallel); ZS_HIST_INFLIGHT
   // symbol loads in flight per lane before their atomics, so the wave waits for
@@ -445,8 +452,8 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
       if (v[k] == 0xffffffffu) continue;
       if (v[k] & 0x80000000u) {
         const uint32_t lc = (v[k] >> 16) & 0xff, dist = (v[k] & 0xffffu) - 1;
-        atomicAdd(&w.hist[ZS_LENGTH_CODE[lc] + 257], 1u);
-        atomicAdd(&w.hist[ZS_L_CODES + (dist < 256 ? ZS_DIST_CODE[dist] : ZS_DIST_CODE[256 + (dist >> 7)])], 1u);
+        atomicAdd(&w.hist[lcode8[lc] + 257u], 1u);
+        atomicAdd(&w.hist[ZS_L_CODES + dcode8[dist < 256 ? dist : 256 + (dist >> 7)]], 1u);
       } else {
         atomicAdd(&w.hist[v[k]], 1u);
       }
