@@ -118,6 +118,9 @@ extern "C" int zs_parse_stats(unsigned long long* out) {
 #endif
 
 #define ZS_GATHER 16  // pass C: 64-symbol chunks loaded before any is stored
+#ifndef ZS_PARSE_WIN
+#define ZS_PARSE_WIN 32  // pass A's per-lane match-table window (A/B: 64)
+#endif
 
 
 template <uint32_t WIN, uint32_t SEG, uint32_t NWV>
@@ -469,8 +472,8 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
     zs_parse_body<WIN, SEG, NWV>(W[w_], T[w_], RS, in, in_off, in_len, pos_base, blk_base, mres, syms, blocks,      \
                                  streams, scratch, good, lazy);                                                     \
   }
-ZS_PARSE_KERNEL(zs_k_parse, 32, ZS_PARSE_SEG, 1)
+ZS_PARSE_KERNEL(zs_k_parse, ZS_PARSE_WIN, ZS_PARSE_SEG, 1)
 // two waves per stream, 512-position segments: half the speculative pass per lane (small batches)
-ZS_PARSE_KERNEL(zs_k_parse_2w, 32, ZS_PARSE2W_SEG, 2)
+ZS_PARSE_KERNEL(zs_k_parse_2w, ZS_PARSE_WIN, ZS_PARSE2W_SEG, 2)
 // four waves per stream, 256-position segments
-ZS_PARSE_KERNEL(zs_k_parse_4w, 32, ZS_PARSE4W_SEG, 4)
+ZS_PARSE_KERNEL(zs_k_parse_4w, ZS_PARSE_WIN, ZS_PARSE4W_SEG, 4)
