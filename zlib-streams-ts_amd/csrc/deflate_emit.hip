@@ -31,6 +31,9 @@ struct zs_tw {  // LDS workspace of one wave, common/types.ts DeflateState tree 
   int16_t heap[2 * ZS_L_CODES + 1];
   uint32_t hk[2 * ZS_L_CODES + 4] __attribute__((aligned(16)));  // working heap: freq << 17 | depth << 10 | node
                                                                    // (+2: the sift reads grandchildren 2j..2j+3)
+  // the distance tree's own heap arrays: it is built beside the literal/length tree
+  int16_t heapd[2 * ZS_D_CODES + 1];
+  uint32_t hkd[2 * ZS_D_CODES + 4] __attribute__((aligned(16)));
   uint16_t bl_count[16];
   uint32_t hist[ZS_L_CODES + ZS_D_CODES];
   uint32_t hdr[ZS_HDR_WORDS];
@@ -47,6 +50,9 @@ struct zs_tdesc {
 
 struct zs_tstate {
   zs_tw* w;
+  uint32_t* hk;     // the tree's heap entries (then gen_bitlen's ancestor words)
+  int16_t* heap;    // the tree's heap[] (trees.ts: s.heap), heap_size entries
+  int heap_size;
   int heap_len, heap_max;
   uint32_t opt_len, static_len;
   // header bit writer
@@ -67,7 +73,7 @@ static __device__ __forceinline__ uint32_t zs_hkey(uint32_t e) { return e >> 10;
 // past heap_len are read but never selected: the j < heap_len / j2 <= heap_len
 // tests guard them).
 static __device__ void zs_pqdownheap(zs_tstate& t, int k) {
-  uint32_t* hk = t.w->hk;
+  uint32_t* hk = t.hk;
   const uint32_t v = hk[k], kv = zs_hkey(v);
   const int len = t.heap_len;
   int j = k << 1;
@@ -97,7 +103,7 @@ static __device__ void zs_pqdownheap(zs_tstate& t, int k) {
 // entry that ends at k -- the new root for k = 1 -- so the merge loop reads
 // neither hk[1] back
 static __device__ uint32_t zs_pqdownheap_v(zs_tstate& t, int k, uint32_t v) {
-  uint32_t* hk = t.w->hk;
+  uint32_t* hk = t.hk;
   const uint32_t kv = zs_hkey(v);
   const int len = t.heap_len, k0 = k;
   uint32_t top = v;
@@ -156,7 +162,7 @@ static __device__ void zs_gen_codes_wave(const uint16_t* bl_count, const uint16_
 // the i-th symbol with a nonzero frequency, placed by a ballot prefix; all
 // lanes call it, before zs_build_tree on lane 0
 static __device__ void zs_tree_leaves_wave(zs_tstate& t, zs_tdesc& d, uint32_t lane) {
-  uint32_t* hk = t.w->hk;
+  uint32_t* hk = t.hk;
   const uint64_t below = (1ull << lane) - 1ull;
   int hl = 0, max_code = -1;
   for (int n0 = 0; n0 < d.elems; n0 += 64) {
@@ -180,7 +186,7 @@ static __device__ void zs_tree_leaves_wave(zs_tstate& t, zs_tdesc& d, uint32_t l
 // before a shallower one, and the nodes of one level own disjoint subtrees,
 // so sifting a level's nodes at once (one lane each) gives the same heap
 static __device__ void zs_tree_heapify_wave(zs_tstate& t, zs_tdesc& d, uint32_t lane) {
-  uint32_t* hk = t.w->hk;
+  uint32_t* hk = t.hk;
   int max_code = d.max_code;
   while (t.heap_len < 2) {
     const int node = max_code < 2 ? ++max_code : 0;
@@ -203,10 +209,10 @@ static __device__ void zs_tree_heapify_wave(zs_tstate& t, zs_tdesc& d, uint32_t 
 }
 
 static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:305-316, lane 0 (heap built)
-  int16_t* heap = t.w->heap;
-  uint32_t* hk = t.w->hk;
+  int16_t* heap = t.heap;
+  uint32_t* hk = t.hk;
   int node;
-  t.heap_max = ZS_HEAP_SIZE;
+  t.heap_max = t.heap_size;
   node = d.elems;
   uint32_t root = hk[1];
   do {
@@ -237,9 +243,9 @@ static __device__ void zs_build_tree(zs_tstate& t, zs_tdesc& d) {  // trees.ts:3
 // zs_build_tree on lane 0 (t.heap_max, d.max_code: lane 0's).
 #define ZS_GB_PER_LANE ((ZS_HEAP_SIZE + 63) / 64)
 static __device__ void zs_gen_bitlen_wave(zs_tstate& t, zs_tdesc& d, uint32_t lane) {
-  int16_t* heap = t.w->heap;
+  int16_t* heap = t.heap;
   uint16_t* bl_count = t.w->bl_count;
-  uint32_t* anc = t.w->hk;  // free after the build: anc[node] = ancestor << 16 | depth to it
+  uint32_t* anc = t.hk;  // free after the build: anc[node] = ancestor << 16 | depth to it
   const int hm = __builtin_amdgcn_readlane(t.heap_max, 0);
   const int max_code = __builtin_amdgcn_readlane(d.max_code, 0);
   const int root = heap[hm];
@@ -248,7 +254,7 @@ static __device__ void zs_gen_bitlen_wave(zs_tstate& t, zs_tdesc& d, uint32_t la
 #pragma unroll
   for (int r = 0; r < ZS_GB_PER_LANE; r++) {
     const int h = hm + (int)lane + 64 * r;
-    nd[r] = h < ZS_HEAP_SIZE ? heap[h] : -1;
+    nd[r] = h < t.heap_size ? heap[h] : -1;
     if (nd[r] >= 0) anc[nd[r]] = nd[r] == root ? (uint32_t)root << 16 : ((uint32_t)d.dad[nd[r]] << 16) | 1u;
   }
   __syncthreads();
@@ -299,7 +305,7 @@ static __device__ void zs_gen_bitlen_wave(zs_tstate& t, zs_tdesc& d, uint32_t la
   t.static_len += stat;
   __syncthreads();
   if (overflow == 0 || lane != 0) return;
-  int bits, n, m, h = ZS_HEAP_SIZE;  // trees.ts:222-258, serial
+  int bits, n, m, h = t.heap_size;  // trees.ts:222-258, serial
   do {
     bits = d.max_length - 1;
     while (bl_count[bits] == 0) bits--;
@@ -412,7 +418,21 @@ static __device__ uint32_t zs_send_tree_wave(const uint16_t* len, int max_code, 
   return base;
 }
 
-#define ZS_HIST_INFLIGHT 32u
+#ifndef ZS_HIST_INFLIGHT
+#define ZS_HIST_INFLIGHT 32u  // histogram: symbol loads in flight per lane before their atomics
+#endif
+#ifndef ZS_TR_PROF
+#define ZS_TR_PROF 0  // timing experiments: wall-clock per phase summed over blocks (0 in the product)
+#endif
+#if ZS_TR_PROF
+__device__ unsigned long long zs_tr_stat[8];  // histogram, L heap, L lengths + codes, D tree, bl tree, rest, blocks
+extern "C" int zs_trees_stats(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(zs_tr_stat), sizeof(zs_tr_stat));
+}
+#define TR_MARK(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = wall_clock64(); atomicAdd(&zs_tr_stat[i], t_ - tr_t); tr_t = t_; } } while (0)
+#else
+#define TR_MARK(i) do { } while (0)
+#endif
 __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                                                  const uint64_t* __restrict__ pos_base,
                                                  const uint32_t* __restrict__ blk_base,
@@ -427,6 +447,10 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   zs_block blk = blocks[bi];
   const uint32_t lane = threadIdx.x;
   const uint32_t* sy = syms + pos_base[s] + s + blk.sym_start;
+#if ZS_TR_PROF
+  unsigned long long tr_t = wall_clock64();
+  if (threadIdx.x == 0) atomicAdd(&zs_tr_stat[7], 1ull);
+#endif
   for (uint32_t i = lane; i < ZS_L_CODES + ZS_D_CODES; i += 64) w.hist[i] = 0;
   for (uint32_t i = lane; i < ZS_HDR_WORDS; i += 64) w.hdr[i] = 0;
   // the length and distance code maps in LDS (the histogram's lookups would
@@ -465,10 +489,14 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   for (uint32_t i = lane; i < ZS_D_CODES; i += 64) w.dfreq[i] = (uint16_t)w.hist[ZS_L_CODES + i];
   if (lane < ZS_BL_CODES) w.bfreq[lane] = 0;
   __syncthreads();
+  TR_MARK(0);
   // the serial parts run in lane 0 (its registers hold t and the max codes),
   // the code assignment in the whole wave between them
   zs_tstate t;
   t.w = &w;
+  t.hk = w.hk;
+  t.heap = w.heap;
+  t.heap_size = ZS_HEAP_SIZE;
   t.opt_len = 0;
   t.static_len = 0;
   t.hbits = 0;
@@ -476,24 +504,46 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   zs_tdesc D = {w.dfreq, w.dlen, w.ddad, w.dcode, ZS_STATIC_DTREE, ZS_EXTRA_DBITS, 0, ZS_D_CODES, 15, 0};
   zs_tdesc B = {w.bfreq, w.blen, w.bdad, w.bcode, nullptr, nullptr, 0, ZS_BL_CODES, 7, 0};
   B.extra = ZS_EXTRA_BLBITS;
+  // the literal/length and distance trees are independent until the bl tree:
+  // their heaps are built at once, lane 0 the first and lane 1 the second (one
+  // instruction stream, per-lane arrays), their sums added after
+  zs_tstate td = t;
+  td.hk = w.hkd;
+  td.heap = w.heapd;
+  td.heap_size = 2 * ZS_D_CODES + 1;
+  td.opt_len = 0;
+  td.static_len = 0;
   zs_tree_leaves_wave(t, L, lane);
   __syncthreads();
   zs_tree_heapify_wave(t, L, lane);
-  if (lane == 0) zs_build_tree(t, L);
+  zs_tree_leaves_wave(td, D, lane);
   __syncthreads();
+  zs_tree_heapify_wave(td, D, lane);
+  {
+    int hm = 0;
+    if (lane < 2) {
+      zs_tstate tt = lane ? td : t;
+      zs_tdesc dd = lane ? D : L;
+      zs_build_tree(tt, dd);
+      hm = tt.heap_max;
+    }
+    t.heap_max = __builtin_amdgcn_readlane(hm, 0);
+    td.heap_max = __builtin_amdgcn_readlane(hm, 1);
+  }
+  __syncthreads();
+  TR_MARK(1);
   zs_gen_bitlen_wave(t, L, lane);
   __syncthreads();
   zs_gen_codes_wave(w.bl_count, w.llen, w.lcode, __builtin_amdgcn_readlane(L.max_code, 0), lane);
   __syncthreads();
-  zs_tree_leaves_wave(t, D, lane);
-  __syncthreads();
-  zs_tree_heapify_wave(t, D, lane);
-  if (lane == 0) zs_build_tree(t, D);
-  __syncthreads();
-  zs_gen_bitlen_wave(t, D, lane);
+  TR_MARK(2);
+  zs_gen_bitlen_wave(td, D, lane);
   __syncthreads();
   zs_gen_codes_wave(w.bl_count, w.dlen, w.dcode, __builtin_amdgcn_readlane(D.max_code, 0), lane);
   __syncthreads();
+  t.opt_len += td.opt_len;
+  t.static_len += td.static_len;
+  TR_MARK(3);
   // build_bl_tree (trees.ts:416-432): scan_tree of both trees by runs (all lanes), then the tree (lane 0)
   const int lmax = __builtin_amdgcn_readlane(L.max_code, 0), dmax = __builtin_amdgcn_readlane(D.max_code, 0);
   if (lane < 32) w.b32[lane] = 0;
@@ -541,6 +591,7 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
     w.bc[1] = t.hbits;
   }
   __syncthreads();
+  TR_MARK(4);
   const uint32_t type = w.bc[0];
   uint32_t hbits = w.bc[1];
   if (type == 2) {
@@ -577,6 +628,7 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
     blk.data_bits = data_bits;
     blocks[bi] = blk;
   }
+  TR_MARK(5);
 }
 
 // --------------------------------------------------------------- layout
