@@ -20,20 +20,28 @@ static __device__ __forceinline__ zcode zpack(uint32_t op, uint32_t bits, uint32
   return (op << 24) | (bits << 16) | val;
 }
 
-// length/distance tables, inflate/constants.ts:8-45 (ops: 16 + extra, deflate64: 128 + extra)
+// length/distance tables, inflate/constants.ts:8-45 (ops: 16 + extra, deflate64: 128 + extra),
+// in closed form (a lookup in a constant array is a memory round trip per table entry):
+//   length code i < 28: extra e = i < 8 ? 0 : i / 4 - 1, base = 3 + i below 8, else ((4 + i % 4) << e) + 3
+//     (3, 4, .., 10, 11, 13, 15, 17, 19, 23, .., 227);
+//   distance code i < 30: extra e = i < 4 ? 0 : i / 2 - 1, base = 1 + i below 4, else ((2 + i % 2) << e) + 1
+//     (1, 2, 3, 4, 5, 7, 9, 13, .., 24577).
+// zs_inftab_selfcheck (and every golden) pins them to the reference's tables.
 static __device__ __forceinline__ void zs_lbase(uint32_t i, bool d64, uint32_t& base, uint32_t& op) {
-  static constexpr uint16_t lb[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-  static constexpr uint8_t le[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-  if (i < 28) { base = lb[i]; op = (d64 ? 128u : 16u) + le[i]; }
+  if (i < 28) {
+    const uint32_t e = i < 8u ? 0u : (i >> 2) - 1u;
+    base = i < 8u ? 3u + i : ((4u + (i & 3u)) << e) + 3u;
+    op = (d64 ? 128u : 16u) + e;
+  }
   else if (i == 28) { base = d64 ? 3u : 258u; op = d64 ? 144u : 16u; }
   else { base = 0; op = d64 ? (i == 29 ? 72u : 78u) : (i == 29 ? 73u : 200u); }
 }
 static __device__ __forceinline__ void zs_dbase(uint32_t i, bool d64, uint32_t& base, uint32_t& op) {
-  static constexpr uint16_t db[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,    65,    97,    129,
-                                      193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-  static constexpr uint8_t de[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-  if (i < 30) { base = db[i]; op = (d64 ? 128u : 16u) + de[i]; }
+  if (i < 30) {
+    const uint32_t e = i < 4u ? 0u : (i >> 1) - 1u;
+    base = i < 4u ? 1u + i : ((2u + (i & 1u)) << e) + 1u;
+    op = (d64 ? 128u : 16u) + e;
+  }
   else if (d64) { base = i == 30 ? 32769u : 49153u; op = 128u + 14u; }
   else { base = 0; op = 64u; }
 }
