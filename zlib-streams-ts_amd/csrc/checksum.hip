@@ -53,12 +53,12 @@ struct zs_ck_src {
   uint32_t sh, last;
 };
 static __device__ __forceinline__ uint4 zs_ck_load16(const zs_ck_src& S, uint32_t i) {
-  const uint32_t q = (i + S.sh) >> 2;
+  const uint32_t q = (i + S.sh) >> 2, r = (i + S.sh) & 3u;  // (r: any byte offset i)
   uint32_t x[5];
 #pragma unroll
   for (int k = 0; k < 5; k++) x[k] = S.w4[min(q + (uint32_t)k, S.last)];
-  return make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], S.sh), __builtin_amdgcn_alignbyte(x[2], x[1], S.sh),
-                    __builtin_amdgcn_alignbyte(x[3], x[2], S.sh), __builtin_amdgcn_alignbyte(x[4], x[3], S.sh));
+  return make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], r), __builtin_amdgcn_alignbyte(x[2], x[1], r),
+                    __builtin_amdgcn_alignbyte(x[3], x[2], r), __builtin_amdgcn_alignbyte(x[4], x[3], r));
 }
 static __device__ __forceinline__ uint32_t zs_ck_word(const uint4& d, uint32_t j) {
   return j == 0 ? d.x : j == 1 ? d.y : j == 2 ? d.z : d.w;
@@ -68,14 +68,21 @@ __global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ in_len, uint32_t* __restrict__ check,
                                                     int kind, const uint32_t* __restrict__ seeds) {
   __shared__ uint32_t T[4][256];  // slice-by-4 tables: T[k][b] = CRC of byte b followed by k zero bytes
-  __shared__ uint32_t seg_crc[64];
   const int s = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const uint32_t n = in_len[s];
   const uint8_t* src = in + in_off[s];
-  // lane i owns bytes [i per, (i + 1) per), per a multiple of 16
+  // Adler: lane i owns bytes [i per, (i + 1) per), per a multiple of 16.  CRC:
+  // segments counted from the stream's end, lane i owns [n - (64 - i) per,
+  // n - (63 - i) per) clipped at 0, so every segment but the first nonempty one
+  // is full (the combine below relies on it)
   const uint32_t per = (((n + 63) / 64) + 15u) & ~15u;
-  const uint32_t b0 = min(n, lane * per), b1 = min(n, b0 + per);
+  uint32_t b0 = min(n, lane * per), b1 = min(n, b0 + per);
+  if (kind == 2) {
+    const uint32_t back = (63u - lane) * per;
+    b1 = n > back ? n - back : 0u;
+    b0 = b1 > per ? b1 - per : 0u;
+  }
   zs_ck_src S;
   S.sh = (uint32_t)((uintptr_t)src & 3u);
   S.w4 = n ? reinterpret_cast<const uint32_t*>(src - S.sh) : in_len;  // an empty stream reads nothing it uses
@@ -114,22 +121,24 @@ __global__ __launch_bounds__(64) void zs_k_checksum(const uint8_t* __restrict__ 
         }
       }
     }
-    seg_crc[lane] = c ^ 0xffffffffu;
-    __syncthreads();
+    // crc32_combine over the 64 segments as a tree, all lanes at once: in round
+    // r lane l (a multiple of 2^(r+1)) appends the 2^r segments after its own
+    // run, crc = crc * x^(8 per 2^r) + crc' (mod P).  Every right-hand run is
+    // full; a run holding the short or empty segments has only empty ones
+    // (CRC 0) before it, so their shift does not matter.
+    uint32_t crc = c ^ 0xffffffffu;  // (0 for an empty segment)
+    uint32_t xp = n ? zs_x8nmodp(per) : 1u << 31;
+#pragma unroll 1
+    for (uint32_t r = 0; r < 6; r++) {
+      const uint32_t o = (uint32_t)__shfl_down((int)crc, 1 << r, 64);
+      const uint32_t cc = zs_multmodp(xp, crc) ^ o;
+      if ((lane & ((2u << r) - 1u)) == 0) crc = cc;
+      if (r < 5) xp = zs_multmodp(xp, xp);
+    }
     if (lane == 0) {
       const uint32_t seed = seeds ? seeds[s] : 0u;
-      uint32_t crc = seed;  // crc32 of nothing (crc32.ts:27-29): the seed
-      if (n) {
-        crc = seg_crc[0];
-        const uint32_t xp = zs_x8nmodp(per);
-        for (uint32_t i = 1; i < 64; i++) {
-          const uint32_t lo = min(n, i * per), hi = min(n, lo + per);
-          if (hi == lo) break;
-          const uint32_t xl = hi - lo == per ? xp : zs_x8nmodp(hi - lo);
-          crc = zs_multmodp(xl, crc) ^ seg_crc[i];
-        }
-        if (seed) crc ^= zs_multmodp(zs_x8nmodp(n), seed);
-      }
+      if (!n) crc = seed;  // crc32 of nothing (crc32.ts:27-29): the seed
+      else if (seed) crc ^= zs_multmodp(zs_x8nmodp(n), seed);
       check[s] = crc;
     }
   } else {
