@@ -25,8 +25,11 @@
 // ------------------------------------------------------------ tree building
 static constexpr int ZS_EXTRA_BLBITS[ZS_BL_CODES] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
 struct zs_tw {  // LDS workspace of one wave, common/types.ts DeflateState tree fields
-  uint16_t lfreq[ZS_HEAP_SIZE], llen[ZS_HEAP_SIZE], ldad[ZS_HEAP_SIZE], lcode[ZS_HEAP_SIZE];
-  uint16_t dfreq[2 * ZS_D_CODES + 1], dlen[2 * ZS_D_CODES + 1], ddad[2 * ZS_D_CODES + 1], dcode[2 * ZS_D_CODES + 1];
+  // (the length arrays 16-byte aligned: zs_run_at reads eight lengths at a time)
+  uint16_t llen[ZS_HEAP_SIZE] __attribute__((aligned(16)));
+  uint16_t dlen[2 * ZS_D_CODES + 1] __attribute__((aligned(16)));
+  uint16_t lfreq[ZS_HEAP_SIZE], ldad[ZS_HEAP_SIZE], lcode[ZS_HEAP_SIZE];
+  uint16_t dfreq[2 * ZS_D_CODES + 1], ddad[2 * ZS_D_CODES + 1], dcode[2 * ZS_D_CODES + 1];
   uint16_t bfreq[2 * ZS_BL_CODES + 1], blen[2 * ZS_BL_CODES + 1], bdad[2 * ZS_BL_CODES + 1], bcode[2 * ZS_BL_CODES + 1];
   int16_t heap[2 * ZS_L_CODES + 1];
   uint32_t hk[2 * ZS_L_CODES + 4] __attribute__((aligned(16)));  // working heap: freq << 17 | depth << 10 | node
@@ -375,8 +378,22 @@ static __device__ __forceinline__ bool zs_run_at(const uint16_t* len, int max_co
   if (n > max_code) return false;
   v = len[n];
   if (n > 0 && len[n - 1] == v) return false;
+  // the run's end (the guard ends every run): eight lengths per LDS read where
+  // aligned -- a run of unused symbols is often a hundred long (len is 16-byte
+  // aligned and holds max_code + 9 entries or more)
   int m = n + 1;
-  while (len[m] == v) m++;  // the guard ends every run
+  const uint32_t vv = v | (v << 16);
+  for (;;) {
+    if ((m & 7) == 0) {
+      const uint4 q = *reinterpret_cast<const uint4*>(&len[m]);
+      if (q.x == vv && q.y == vv && q.z == vv && q.w == vv) {
+        m += 8;
+        continue;
+      }
+    }
+    if (len[m] != v) break;
+    m++;
+  }
   r = (uint32_t)(m - n);
   return true;
 }
