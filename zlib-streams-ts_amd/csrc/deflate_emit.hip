@@ -694,7 +694,9 @@ __global__ void zs_k_layout(const uint32_t* __restrict__ blk_base, zs_block* __r
 
 // -------------------------------------------------------------------- emit
 #define ZS_EMIT_THREADS 256
-#define ZS_EMIT_PER_THREAD 8
+#ifndef ZS_EMIT_PER_THREAD
+#define ZS_EMIT_PER_THREAD 4  // symbols per thread and chunk (A/B: 2, 8, 16)
+#endif
 // the stage holds the block header, the dynamic tree header and one chunk's
 // bits (at most 15 + 5 + 15 + 13 = 48 per symbol) past the carried word
 #define ZS_STAGE_WORDS (ZS_HDR_WORDS + 2 + ZS_EMIT_THREADS * ZS_EMIT_PER_THREAD * 48 / 32)
