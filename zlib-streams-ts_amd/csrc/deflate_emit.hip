@@ -28,8 +28,8 @@ struct zs_tw {  // LDS workspace of one wave, common/types.ts DeflateState tree 
   // (the length arrays 16-byte aligned: zs_run_at reads eight lengths at a time)
   uint16_t llen[ZS_HEAP_SIZE] __attribute__((aligned(16)));
   uint16_t dlen[2 * ZS_D_CODES + 1] __attribute__((aligned(16)));
-  uint16_t lfreq[ZS_HEAP_SIZE], ldad[ZS_HEAP_SIZE], lcode[ZS_HEAP_SIZE];
-  uint16_t dfreq[2 * ZS_D_CODES + 1], ddad[2 * ZS_D_CODES + 1], dcode[2 * ZS_D_CODES + 1];
+  uint16_t lfreq[ZS_HEAP_SIZE], ldad[ZS_HEAP_SIZE];  // (the codes go straight to HBM: zs_gen_codes_out)
+  uint16_t dfreq[2 * ZS_D_CODES + 1], ddad[2 * ZS_D_CODES + 1];
   uint16_t bfreq[2 * ZS_BL_CODES + 1], blen[2 * ZS_BL_CODES + 1], bdad[2 * ZS_BL_CODES + 1], bcode[2 * ZS_BL_CODES + 1];
   int16_t heap[2 * ZS_L_CODES + 1];
   uint32_t hk[2 * ZS_L_CODES + 4] __attribute__((aligned(16)));  // working heap: freq << 17 | depth << 10 | node
@@ -38,7 +38,7 @@ struct zs_tw {  // LDS workspace of one wave, common/types.ts DeflateState tree 
   int16_t heapd[2 * ZS_D_CODES + 1];
   uint32_t hkd[2 * ZS_D_CODES + 4] __attribute__((aligned(16)));
   uint16_t bl_count[16];
-  uint32_t hist[ZS_L_CODES + ZS_D_CODES];
+  uint16_t tally[ZS_L_CODES + ZS_D_CODES];  // the block's true counts (the histogram itself lives in hk)
   uint32_t hdr[ZS_HDR_WORDS];
   uint32_t bc[4];  // lane 0 -> wave: type, max codes, header bits
   uint32_t b32[32];  // scan_tree's bl_tree frequencies (LDS atomics)
@@ -158,6 +158,33 @@ static __device__ void zs_gen_codes_wave(const uint16_t* bl_count, const uint16_
       fc[b] += (uint32_t)__popcll(mk);
     }
     if (l) code[n] = (uint16_t)(__builtin_bitreverse32(my) >> (32 - l));
+  }
+}
+
+// zs_gen_codes_wave for the literal/length and distance trees, written straight
+// to the block's code table in HBM as code | length << 16 (0 for an unused
+// symbol): all ncodes entries, so the workspace needs no code arrays
+static __device__ void zs_gen_codes_out(const uint16_t* bl_count, const uint16_t* len, uint32_t* out, int max_code,
+                                        int ncodes, uint32_t lane) {
+  uint32_t fc[16];
+  uint32_t c = 0;
+#pragma unroll
+  for (int b = 1; b <= 15; b++) {
+    c = (c + bl_count[b - 1]) << 1;
+    fc[b] = c;
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int n0 = 0; n0 < ncodes; n0 += 64) {
+    const int n = n0 + (int)lane;
+    const uint32_t l = n <= max_code ? len[n] : 0u;
+    uint32_t my = 0;
+#pragma unroll
+    for (int b = 1; b <= 15; b++) {
+      const uint64_t mk = __ballot(l == (uint32_t)b);
+      my = l == (uint32_t)b ? fc[b] + (uint32_t)__popcll(mk & below) : my;
+      fc[b] += (uint32_t)__popcll(mk);
+    }
+    if (n < ncodes) out[n] = l ? (__builtin_bitreverse32(my) >> (32 - l)) | (l << 16) : 0u;
   }
 }
 
@@ -468,7 +495,9 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   unsigned long long tr_t = wall_clock64();
   if (threadIdx.x == 0) atomicAdd(&zs_tr_stat[7], 1ull);
 #endif
-  for (uint32_t i = lane; i < ZS_L_CODES + ZS_D_CODES; i += 64) w.hist[i] = 0;
+  uint32_t* const hist = w.hk + 192;  // the histogram: hk past the code maps, free until the heap
+  static_assert(sizeof(w.hk) >= 4 * (192 + ZS_L_CODES + ZS_D_CODES), "histogram in hk");
+  for (uint32_t i = lane; i < ZS_L_CODES + ZS_D_CODES; i += 64) hist[i] = 0;
   for (uint32_t i = lane; i < ZS_HDR_WORDS; i += 64) w.hdr[i] = 0;
   // the length and distance code maps in LDS (the histogram's lookups would
   // otherwise be a memory round trip each, behind the symbol's own load)
@@ -493,17 +522,18 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
       if (v[k] == 0xffffffffu) continue;
       if (v[k] & 0x80000000u) {
         const uint32_t lc = (v[k] >> 16) & 0xff, dist = (v[k] & 0xffffu) - 1;
-        atomicAdd(&w.hist[lcode8[lc] + 257u], 1u);
-        atomicAdd(&w.hist[ZS_L_CODES + dcode8[dist < 256 ? dist : 256 + (dist >> 7)]], 1u);
+        atomicAdd(&hist[lcode8[lc] + 257u], 1u);
+        atomicAdd(&hist[ZS_L_CODES + dcode8[dist < 256 ? dist : 256 + (dist >> 7)]], 1u);
       } else {
-        atomicAdd(&w.hist[v[k]], 1u);
+        atomicAdd(&hist[v[k]], 1u);
       }
     }
   }
   __syncthreads();
   // init_block (trees.ts:90-103) + tally counts
-  for (uint32_t i = lane; i < ZS_L_CODES; i += 64) w.lfreq[i] = i == ZS_END_BLOCK ? 1 : (uint16_t)w.hist[i];
-  for (uint32_t i = lane; i < ZS_D_CODES; i += 64) w.dfreq[i] = (uint16_t)w.hist[ZS_L_CODES + i];
+  for (uint32_t i = lane; i < ZS_L_CODES + ZS_D_CODES; i += 64) w.tally[i] = (uint16_t)hist[i];  // <= 16,383
+  for (uint32_t i = lane; i < ZS_L_CODES; i += 64) w.lfreq[i] = i == ZS_END_BLOCK ? 1 : (uint16_t)hist[i];
+  for (uint32_t i = lane; i < ZS_D_CODES; i += 64) w.dfreq[i] = (uint16_t)hist[ZS_L_CODES + i];
   if (lane < ZS_BL_CODES) w.bfreq[lane] = 0;
   __syncthreads();
   TR_MARK(0);
@@ -517,8 +547,9 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   t.opt_len = 0;
   t.static_len = 0;
   t.hbits = 0;
-  zs_tdesc L = {w.lfreq, w.llen, w.ldad, w.lcode, ZS_STATIC_LTREE, ZS_EXTRA_LBITS, 257, ZS_L_CODES, 15, 0};
-  zs_tdesc D = {w.dfreq, w.dlen, w.ddad, w.dcode, ZS_STATIC_DTREE, ZS_EXTRA_DBITS, 0, ZS_D_CODES, 15, 0};
+  zs_tdesc L = {w.lfreq, w.llen, w.ldad, nullptr, ZS_STATIC_LTREE, ZS_EXTRA_LBITS, 257, ZS_L_CODES, 15, 0};
+  zs_tdesc D = {w.dfreq, w.dlen, w.ddad, nullptr, ZS_STATIC_DTREE, ZS_EXTRA_DBITS, 0, ZS_D_CODES, 15, 0};
+  uint32_t* const cout = codes + (size_t)bi * (ZS_L_CODES + ZS_D_CODES);  // (used by emit for dynamic blocks only)
   zs_tdesc B = {w.bfreq, w.blen, w.bdad, w.bcode, nullptr, nullptr, 0, ZS_BL_CODES, 7, 0};
   B.extra = ZS_EXTRA_BLBITS;
   // the literal/length and distance trees are independent until the bl tree:
@@ -551,12 +582,12 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   TR_MARK(1);
   zs_gen_bitlen_wave(t, L, lane);
   __syncthreads();
-  zs_gen_codes_wave(w.bl_count, w.llen, w.lcode, __builtin_amdgcn_readlane(L.max_code, 0), lane);
+  zs_gen_codes_out(w.bl_count, w.llen, cout, __builtin_amdgcn_readlane(L.max_code, 0), ZS_L_CODES, lane);
   __syncthreads();
   TR_MARK(2);
   zs_gen_bitlen_wave(td, D, lane);
   __syncthreads();
-  zs_gen_codes_wave(w.bl_count, w.dlen, w.dcode, __builtin_amdgcn_readlane(D.max_code, 0), lane);
+  zs_gen_codes_out(w.bl_count, w.dlen, cout + ZS_L_CODES, __builtin_amdgcn_readlane(D.max_code, 0), ZS_D_CODES, lane);
   __syncthreads();
   t.opt_len += td.opt_len;
   t.static_len += td.static_len;
@@ -620,12 +651,12 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
   uint32_t data_bits = 0;
   if (type != 0) {
     for (uint32_t i = lane; i < ZS_L_CODES; i += 64) {
-      const uint32_t f = i == ZS_END_BLOCK ? 1u : w.hist[i];
+      const uint32_t f = i == ZS_END_BLOCK ? 1u : w.tally[i];
       const uint32_t len = type == 1 ? ZS_STATIC_LTREE[i] >> 16 : w.llen[i];
       if (f) data_bits += f * (len + (i >= 257 ? (uint32_t)ZS_EXTRA_LBITS[i - 257] : 0u));
     }
     if (lane < ZS_D_CODES) {
-      const uint32_t f = w.hist[ZS_L_CODES + lane];
+      const uint32_t f = w.tally[ZS_L_CODES + lane];
       const uint32_t len = type == 1 ? 5u : w.dlen[lane];
       if (f) data_bits += f * (len + (uint32_t)ZS_EXTRA_DBITS[lane]);
     }
@@ -633,9 +664,6 @@ __global__ __launch_bounds__(64) void zs_k_trees(const uint8_t* __restrict__ in,
     for (int d = 32; d >= 1; d >>= 1) data_bits += __shfl_xor(data_bits, d, 64);
   }
   if (type == 2) {
-    uint32_t* cout = codes + (size_t)bi * (ZS_L_CODES + ZS_D_CODES);
-    for (uint32_t i = lane; i < ZS_L_CODES; i += 64) cout[i] = w.lcode[i] | ((uint32_t)w.llen[i] << 16);
-    if (lane < ZS_D_CODES) cout[ZS_L_CODES + lane] = w.dcode[lane] | ((uint32_t)w.dlen[lane] << 16);
     uint32_t* hout = hdr + (size_t)bi * ZS_HDR_WORDS;
     for (uint32_t i = lane; i < (hbits + 31) / 32; i += 64) hout[i] = w.hdr[i];
   }
