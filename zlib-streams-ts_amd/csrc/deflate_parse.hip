@@ -74,11 +74,12 @@ struct zs_round_state {
 // (10 KiB) and measured faster in round 2: 1.54 vs 1.77 ms at 4096 streams,
 // 2.99 ms with direct loads (WIN = 0); 0.40 / 0.42 / 0.54 ms at 512.  Only
 // WIN = 32 is built.
+// The input byte each step needs, in[p - 1], rides in the staged entry of p
+// (round 6; before, 2 KiB of staged input words per wave: 19 KiB per workgroup,
+// eight per CU, parse 1.55 ms at 4,096 streams; now 16 KiB, ten per CU, 1.47 ms).
 template <uint32_t WIN>
 struct zs_parse_win {
   uint4 m[WIN / 2][64];
-  uint32_t s[WIN / 4][64];
-  uint32_t b[64];  // in[w - 1]
 };
 template <>
 struct zs_parse_win<0> {};
@@ -88,6 +89,14 @@ struct zs_seg_tab {
   uint32_t off[65];  // first run symbol of each segment in the round (exclusive prefix; off[64] = round total)
   uint32_t nf[64];   // catch-up symbols
   uint32_t from[64]; // first speculative symbol kept (ZS_NONE: none)
+};
+
+// a wave's window (pass A) and its segment table (passes B, C) are never live
+// at once: the workgroup of one wave needs 16 KiB, ten per CU
+template <uint32_t WIN>
+union zs_parse_lds {
+  zs_parse_win<WIN> W;
+  zs_seg_tab T;
 };
 
 static __device__ __forceinline__ uint32_t zs_sym_len(uint32_t v) {
@@ -220,31 +229,39 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
 #pragma unroll
               for (uint32_t j = 0; j < WIN / 2; j++) W.m[j][lane] = mv[j];
             };
+            // in[p - 1] rides in the entry of p: bits 25..31 of x (L <= 258 uses bits 16..24) and bit 31 of
+            // y; the parse masks them (zs_parse_step), so the window holds no input bytes
+            uint32_t sv[WIN / 4], bw;
             if (aligned) {  // aligned words holding at least one byte of the stream never leave its pages
               load_m();
               const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
               const uint32_t slast = (n - 1u) >> 2;
-              uint32_t sv[WIN / 4];
 #pragma unroll
               for (uint32_t j = 0; j < WIN / 4; j++) sv[j] = s4[min(w / 4 + j, slast)];
-              const uint32_t bw = s4[w ? w / 4 - 1 : 0u] >> 24;
-              store_m();
-#pragma unroll
-              for (uint32_t j = 0; j < WIN / 4; j++) W.s[j][lane] = sv[j];
-              W.b[lane] = w ? bw : 0u;
+              bw = w ? s4[w / 4 - 1] >> 24 : 0u;
             } else {
               load_m();
 #pragma unroll
-              for (uint32_t j = 0; j < WIN / 4; j++) W.s[j][lane] = zs_load_word(src, n, w + 4 * j);
-              W.b[lane] = w ? (uint32_t)src[w - 1] : 0u;
-              store_m();
+              for (uint32_t j = 0; j < WIN / 4; j++) sv[j] = zs_load_word(src, n, w + 4 * j);
+              bw = w ? (uint32_t)src[w - 1] : 0u;
             }
+            auto byte_at = [&](uint32_t k) __attribute__((always_inline)) {  // in[w + k]
+              return (sv[k >> 2] >> (8u * (k & 3u))) & 0xffu;
+            };
+#pragma unroll
+            for (uint32_t j = 0; j < WIN / 2; j++) {
+              const uint32_t l0 = j == 0 ? bw : byte_at(2 * j - 1), l1 = byte_at(2 * j);
+              mv[j].x |= l0 << 25;
+              mv[j].y |= (l0 >> 7) << 31;
+              mv[j].z |= l1 << 25;
+              mv[j].w |= (l1 >> 7) << 31;
+            }
+            store_m();
           }
           while (st.p < b && st.p < w + WIN) {
-            const uint32_t o = st.p - w, q = o - 1;  // in[p - 1] is staged byte o - 1 (o > 0)
+            const uint32_t o = st.p - w;
             const uint2 e = reinterpret_cast<const uint2*>(&W.m[o >> 1][lane])[o & 1];
-            const uint32_t lb = reinterpret_cast<const uint8_t*>(&W.s[(q >> 2) & (WIN / 4 - 1)][lane])[q & 3];
-            step(e, o == 0 ? W.b[lane] : lb);
+            step(e, (e.x >> 25) | ((e.y >> 31) << 7));
           }
         }
       }
@@ -465,11 +482,10 @@ static __device__ __forceinline__ void zs_parse_body(zs_parse_win<WIN>& W, zs_se
       const uint64_t* __restrict__ pos_base, const uint32_t* __restrict__ blk_base, const uint2* __restrict__ mres,  \
       uint32_t* __restrict__ syms, zs_block* __restrict__ blocks, zs_stream* __restrict__ streams,                  \
       uint32_t* __restrict__ scratch, int good, int lazy) {                                                         \
-    __shared__ zs_parse_win<WIN> W[NWV];                                                                            \
-    __shared__ zs_seg_tab T[NWV];                                                                                   \
+    __shared__ zs_parse_lds<WIN> U[NWV];                                                                            \
     __shared__ zs_round_state RS;                                                                                   \
     const uint32_t w_ = threadIdx.x >> 6;                                                                           \
-    zs_parse_body<WIN, SEG, NWV>(W[w_], T[w_], RS, in, in_off, in_len, pos_base, blk_base, mres, syms, blocks,      \
+    zs_parse_body<WIN, SEG, NWV>(U[w_].W, U[w_].T, RS, in, in_off, in_len, pos_base, blk_base, mres, syms, blocks,  \
                                  streams, scratch, good, lazy);                                                     \
   }
 ZS_PARSE_KERNEL(zs_k_parse, ZS_PARSE_WIN, ZS_PARSE_SEG, 1)

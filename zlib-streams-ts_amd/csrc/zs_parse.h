@@ -25,9 +25,10 @@ static __device__ __forceinline__ uint32_t zs_parse_step(zs_pstate& st, uint2 e,
   // head slot emptied by a slide at exactly this position
   const bool nil = ((e.x & 0x8000u) != 0) & (p >= ZS_SLIDE_AT) & (((p - ZS_SLIDE_AT) & 32767u) == 0) &
                    (n - p < (uint32_t)ZS_MIN_LOOKAHEAD);
-  const bool search = ((e.x >> 16) != 0) & (pl < (uint32_t)lazy) & !nil;  // deflate.ts:1376
+  // (lengths are bits 16..24: the parse may carry a byte in the bits above, deflate_parse.hip)
+  const bool search = (((e.x >> 16) & 0x1ffu) != 0) & (pl < (uint32_t)lazy) & !nil;  // deflate.ts:1376
   const uint32_t u = pl >= (uint32_t)good ? e.y : e.x;  // chain >> 2 when prev_length >= good (deflate.ts:1075-1077)
-  const uint32_t L = u >> 16, D = u & 0x7fffu;
+  const uint32_t L = (u >> 16) & 0x1ffu, D = u & 0x7fffu;
   const bool take = search & (L > pl);
   const uint32_t ms = take ? p - D : pm;
   const bool too_far = (L == ZS_MIN_MATCH) & (D > ZS_TOO_FAR);  // deflate.ts:1381-1387
